@@ -1,0 +1,200 @@
+"""bench.py - images/s of the SD1.5 W8A8 (SmoothQuant fake-quant) 512x512 batch-4 50-step
+denoising loop on MI355X (BASELINE.json metric / configs[1]), 1..N GPUs of one node.
+
+One "step" = one generate() over the per-GPU batch: RCCL broadcast of the text embeddings
+from rank 0, 50 graph-replayed denoising steps (UNet on the CFG batch 2B, CFG combine, DDIM),
+gather of the final latents.  Weak scaling: every rank denoises B=4 prompts per step.
+
+Also reported (rank 0):
+  roofline      the dominant kernel (the largest conv implicit GEMM of the UNet) timed live
+                with HIP events on the stream it runs on; ALGORITHMIC flops / duration vs the
+                fp16 dense MFMA peak (the path computes fake-quant operands in fp16)
+  path_roofline whole-loop FLOP rate (803.3 GFLOP per UNet eval per sample)
+  cpu_baseline  the CPU oracle (reference fake-quant math, torch-CPU fp16 ops) timed on this
+                box's host cores on a bounded sample: one W8A8 UNet eval at CFG batch 2
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+UNET_GFLOP_PER_SAMPLE = 803.3   # SURVEY.md Appendix B (analytic, SD1.5 512^2)
+PEAK_F16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: dense BF16/FP16 MFMA
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=4, help="prompts per GPU")
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--denoise-steps", type=int, default=50)
+    ap.add_argument("--mode", default="w8a8-sq", choices=["w8a8-sq", "w8a8", "w4a16", "fp16"])
+    ap.add_argument("--calib-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+QCFG = {
+    "w8a8-sq": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
+    "w8a8": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
+    "w4a16": dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
+}
+
+
+def build_model(args, dev):
+    from qdiff.models import StableDiffusion1_x
+    model = StableDiffusion1_x.from_pretrained("synthetic:sd15", device=dev, seed=0)
+    sd_cpu = None
+    if args.mode != "fp16":
+        qc = dict(QCFG[args.mode])
+        if args.mode == "w8a8-sq":
+            model.quantize(quant_config=qc, quantType="sq", quantUnet=True,
+                           calibration=dict(n_samples=args.batch, batch_size=args.batch,
+                                            num_inference_steps=args.calib_steps))
+        else:
+            model.quantize(quant_config=qc, quantUnet=True)
+    return model
+
+
+def dominant_kernel_roofline(dev, iters=20):
+    """Time the largest conv implicit GEMM of the SD1.5 UNet at CFG batch 8 (down/up block 0
+    conv 320->320 3x3 @ 64x64: M = 32768, N = 320, K = 2880) with HIP events on its stream."""
+    import torch
+    from qdiff import kernels as K
+    n, h, w, c = 8, 64, 64, 320
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(n, h, w, c, generator=g).half().to(dev)
+    wt = (torch.randn(c, 3, 3, c, generator=g) / 54).half().to(dev)
+    b = torch.zeros(c, dtype=torch.float16, device=dev)
+    amax = torch.empty(n * c, dtype=torch.float32, device=dev)
+    for _ in range(3):
+        K.conv2d_nhwc(x, wt, c, 1, 1, bias=b, amax=amax)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        K.conv2d_nhwc(x, wt, c, 1, 1, bias=b, amax=amax)
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * (n * h * w) * c * (9 * c)
+    tflops = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
+            "kernel": "k_gemm<AM_CONV,F16> conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880)",
+            "avg_us": round(ms * 1e3, 2)}
+
+
+def cpu_baseline(threads):
+    """The CPU oracle (reference fake-quant semantics, torch-CPU fp16) on a bounded sample."""
+    import dataclasses
+
+    import torch
+    from oracle.unet_ref import RefUNet
+    from qdiff.unet import SD15, UNet2DConditionModel
+    torch.set_num_threads(threads)
+    u = UNet2DConditionModel(SD15).half().init_synthetic(0)
+    cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(SD15).items()}
+    ref = RefUNet(cd, u.state_dict(), dict(QCFG["w8a8"]))
+    del u
+    g = torch.Generator().manual_seed(42)
+    x = torch.randn(2, 4, 64, 64, generator=g).half()
+    ctx = torch.randn(2, 77, 768, generator=g).half()
+    t0 = time.time()
+    ref.forward(x, 981, ctx)
+    dt = time.time() - t0
+    return {"value": round(1.0 / (50 * dt), 6), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"1 W8A8 UNet eval at CFG batch 2 (1 image), 64x64 latents, {dt:.2f} s, x50 steps",
+            "seconds_per_unet_eval": round(dt, 3)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import qdiff_boot  # noqa: F401
+    from qdiff import dist as qdist
+    from qdiff.pipeline import synthetic_text_embeddings
+
+    rank, world, local = qdist.init_from_env()
+    if world != args.gpus and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    n_gpus = world
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    model = build_model(args, dev)
+    B = args.batch
+    hw = args.res // 8
+    loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.5, use_graph=True)
+    # full CFG context for all ranks' prompts, created on rank 0 and broadcast each step
+    full_ctx = torch.empty(2 * B * world, 77, 768, dtype=torch.float16, device=dev)
+    if rank == 0:
+        prompts = [f"a photograph of synthetic scene {i}" for i in range(B * world)]
+        full_ctx.copy_(torch.cat([synthetic_text_embeddings([""] * (B * world), device=dev),
+                                  synthetic_text_embeddings(prompts, device=dev)]))
+    g = torch.Generator().manual_seed(42 + rank)
+    lat = torch.randn(B, 4, hw, hw, generator=g).half().to(dev)
+
+    def one_step():
+        qdist.broadcast_context(full_ctx, 0)
+        ctx = qdist.shard_context(full_ctx, rank, world)
+        out = loop.run(lat, ctx)
+        return qdist.gather_latents(out, 0)
+
+    for _ in range(args.warmup):
+        one_step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    images = B * world * args.steps
+    value = images / dt
+    if rank == 0:
+        assert out is not None and torch.isfinite(out.float()).all(), "non-finite latents"
+        roof = dominant_kernel_roofline(dev)
+        evals_per_s = value * args.denoise_steps  # UNet evals per image per step: 50 steps at CFG batch 2
+        path_tflops = evals_per_s * 2 * UNET_GFLOP_PER_SAMPLE / 1e3
+        line = {
+            "metric": "images/sec SD1.5 W8A8 512x512 50-step",
+            "value": round(value, 4), "unit": "images/s", "n_gpus": n_gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+            "data": "synthetic (random-init SD1.5 UNet weights N(0,1/fan_in), synthetic text embeddings and latents)",
+            "config": {"workload": f"SD1.5 UNet {args.mode} fake-quant, {args.res}x{args.res}, {B} prompts/GPU "
+                                   f"(CFG batch {2 * B}), {args.denoise_steps} DDIM steps, HIP graph per step",
+                       "global_batch": B * world, "seq_len": 77, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "path_roofline": {"achieved": round(path_tflops / world, 1), "peak": PEAK_F16_TFLOPS,
+                              "unit": "TFLOP/s per GPU", "frac": round(path_tflops / world / PEAK_F16_TFLOPS, 4),
+                              "flop_per_image": 2 * args.denoise_steps * UNET_GFLOP_PER_SAMPLE * 1e9},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+/*
+ * libqdiff — C ABI of the MI355X (gfx950) quantized-diffusion denoising path.
+ *
+ * The reference (maani3/Quantization---Diffusion-Models) has no FFI: its boundary is the
+ * nn.Module swap of quantize/quantizer.py:517,533 that replaces every nn.Linear / nn.Conv2d of
+ * the UNet with WxAxLinear / WxAxConv2d (quantize/fake_quant.py:170-398), whose forward calls
+ * F.linear / F.conv2d on fp16 fake-quantized operands.  The Python host package mirrors those
+ * module classes (same names, from_float keywords, buffers and errors) and calls the entry
+ * points below; each entry point cites the reference computation it replaces.
+ *
+ * Conventions
+ *   - Plain pointers to caller-allocated DEVICE memory; fp16 tensors are IEEE binary16.
+ *   - `stream` is a hipStream_t passed as void*; every call is stream-ordered, enqueues work
+ *     only (no host sync, no allocation), and is capturable into a hipGraph.
+ *   - Return 0 on success, QD_ERR_ARG on a bad argument (nothing launched), or the hipError_t
+ *     of a failed launch.  qd_last_error() returns a static message for the last failure.
+ *   - Activations of the fused UNet path are NHWC ([N, H, W, C], C fastest) == token layout
+ *     [N, H*W, C]; the drop-in modules also accept NCHW.
+ */
+#ifndef QDIFF_H
+#define QDIFF_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QD_OK 0
+#define QD_ERR_ARG 1000
+
+/* granularities (fake_quant.py names) */
+#define QD_GRAN_PER_TOKEN 0    /* quantize_activation_per_token_absmax   fake_quant.py:108-118 */
+#define QD_GRAN_PER_CHANNEL 1  /* quantize_activation_per_channel_absmax fake_quant.py:123-131 */
+#define QD_GRAN_PER_TENSOR 2   /* quantize_activation_per_tensor_absmax  fake_quant.py:157-167 */
+#define QD_GRAN_PER_GROUP 3    /* quantize_activation_per_channel_group_absmax :133-153 */
+
+#define QD_LAYOUT_NCHW 0
+#define QD_LAYOUT_NHWC 1
+
+/* weight storage formats of the GEMM B operand */
+#define QD_WFMT_F16 0   /* dequantized fp16 (the reference's own buffer format) */
+#define QD_WFMT_I8 1    /* int8 codes [N][K] + fp16 scales [N][K/group] */
+#define QD_WFMT_I4 2    /* int4 codes packed 2/byte along K (low nibble = even k) + scales */
+
+int qd_version(void);
+const char* qd_last_error(void);
+int qd_device_arch(char* buf, int len); /* writes gcnArchName of the current device */
+
+/* ---------------- activation fake-quant ---------------------------------------------- */
+/* Reduction pass: amax[...] = max |x| over the granularity's reduction set.  `amax` is fp32,
+ * sized N*C (per_channel), rows (per_token), 1 (per_tensor), N*C*(H/g)*(W/g) (per_group);
+ * it is zeroed by the call.  x is [n, c, h, w] in `layout` (per_token: rows = n*h*w... see
+ * qd_act_fakequant). */
+int qd_act_absmax(const void* x, int layout, int n, int c, int h, int w, int gran, int group,
+                  float* amax, void* stream);
+/* Full quantize->dequantize of an activation tensor (both passes), y may alias x.
+ * Replaces quantize_activation_{per_token,per_channel,per_tensor,per_channel_group}_absmax
+ * (fake_quant.py:108-167).  per_token: x is viewed as [n*h*w... rows = n, cols = c] i.e. pass
+ * (n = rows, c = cols, h = w = 1).  per_group: NCHW only, `group` already shrunk by the host
+ * rule of fake_quant.py:138-139.  `amax_ws` is an fp32 workspace of the qd_act_absmax size. */
+int qd_act_fakequant(const void* x, void* y, int layout, int n, int c, int h, int w, int gran,
+                     int group, int n_bits, float* amax_ws, void* stream);
+/* Quantize with a precomputed amax (second pass only).  For NHWC per_channel, group > 0 means
+ * only the first `group` channels are real (the rest is zero channel padding, copied as is). */
+int qd_act_apply(const void* x, void* y, int layout, int n, int c, int h, int w, int gran,
+                 int group, int n_bits, const float* amax, void* stream);
+
+/* ---------------- weight fake-quant (offline, on device) ----------------------------- */
+/* Row-group absmax RTN of quantize_weight_absmax / _per_channel_ / _per_tensor_
+ * (fake_quant.py:21-105).  w is [rows, cols] fp16 (a 4-D conv weight is [Co*Ci*kh, kw]);
+ * groups of `group` consecutive elements along cols (group == cols for per_channel;
+ * per_tensor: group = rows*cols with rows = 1).  Any of codes (int8 [rows, cols]),
+ * scales (fp16 [rows, cols/group]) and w_dq (fp16 [rows, cols]) may be NULL. */
+int qd_weight_quant(const void* w, int rows, int cols, int group, int n_bits, int8_t* codes,
+                    void* scales, void* w_dq, void* stream);
+/* pack int8 codes in [-8, 7] to int4, 2 per byte along cols (cols even). */
+int qd_pack_int4(const int8_t* codes, int rows, int cols, uint8_t* packed, void* stream);
+/* conv weight [Co][Ci][kh][kw] -> GEMM B layout [Co][kh][kw][Ci_pad] (zero-padded Ci). */
+int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pad, void* out,
+                        void* stream);
+
+/* ---------------- GEMMs (fp16 MFMA, fp32 accumulate) --------------------------------- */
+/* Epilogue flags */
+#define QD_EPI_BIAS 1        /* + bias[N] (fp16), then round to fp16 (F.linear/F.conv2d out) */
+#define QD_EPI_RESIDUAL 2    /* out = half(y + residual[M, N]) */
+#define QD_EPI_AMAX 4        /* per-(sample, col) amax of the rounded y into amax[M/rows_per_sample][N]
+                                (zeroed by the call itself, then atomically max-reduced) */
+#define QD_EPI_GEGLU 8       /* B holds [hidden; gate] halves (N = 2*I): out[M, I] = h * gelu(g) */
+
+/* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
+ * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
+ * wfmt: QD_WFMT_*; wscale [N][K/group] fp16 for I8/I4.  lda/ldy in elements.
+ * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32). */
+int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
+                  const void* wscale, int group, const void* bias, const void* residual,
+                  void* y, int N, int ldy, int epi, float* amax, int rows_per_sample,
+                  void* stream);
+
+/* NHWC implicit-GEMM Conv2d: y[N, Ho, Wo, Co] = conv(x[N, H, W, Ci], W[Co][kh][kw][Ci_pad]).
+ * WxAxConv2d.forward's F.conv2d (fake_quant.py:339); groups = dilation = 1.
+ * x channel stride is Ci_pad (>= Ci, multiple of 8, padded channels zero).
+ * upsample2x != 0: x is the pre-upsample tensor [N, H/2, W/2, Ci] read with nearest
+ * indexing (diffusers Upsample2D interpolate + conv fused).  QD_EPI_AMAX: per-(n, co) amax of
+ * the rounded output into amax[N][Co] (zeroed by the call). */
+int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co,
+                  int kh, int kw, int stride, int pad, int upsample2x, const void* bias,
+                  const void* residual, void* y, int epi, float* amax, void* stream);
+
+/* Conv output fake-quant + fused adds (the q_y = output_quant(y) of fake_quant.py:340 followed
+ * by the diffusers residual / temb add): out = half(fq(y; amax[n][c]) + res) with res either a
+ * full [N, HW, C] tensor (`residual`), or a per-(n, c) vector (`chan_add`, the time embedding
+ * projection), or none.  n_bits == 0 disables the quantization. */
+int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
+                   const void* residual, const void* chan_add, void* out, void* stream);
+
+/* ---------------- normalisation / activations (diffusers UNet ops, fp16 I/O) --------- */
+/* GroupNorm(groups, eps, affine) on NHWC [N, HW, C] (+ SiLU) (+ per-(n, c) fake-quant of the
+ * result with q_bits, i.e. the input quant of the conv that consumes it, fused because a
+ * workgroup owns a whole (n, group) slab).  x may be two tensors concatenated along C:
+ * x2 != NULL -> channels [0, c1) from x (row stride c1), [c1, c) from x2 (row stride c - c1). */
+int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
+                 float eps, const void* gamma, const void* beta, int silu, int q_bits,
+                 void* y, void* stream);
+/* LayerNorm over the last dim C of [rows, C]. */
+int qd_layernorm(const void* x, int rows, int c, float eps, const void* gamma, const void* beta,
+                 void* y, void* stream);
+/* GEGLU (diffusers): h[M, 2I] -> out[M, I] = h[:, :I] * gelu(h[:, I:]). */
+int qd_geglu(const void* h, int m, int inner, void* out, void* stream);
+/* out = silu(x) elementwise (count elements). */
+int qd_silu(const void* x, void* y, int64_t count, void* stream);
+/* out = a + b (fp16) */
+int qd_add(const void* a, const void* b, void* y, int64_t count, void* stream);
+/* NHWC channel concat: out[M, c1+c2] = [a | b] */
+int qd_concat_c(const void* a, int c1, const void* b, int c2, int64_t m, void* out, void* stream);
+/* layout transposes for the drop-in NCHW modules */
+int qd_nchw_to_nhwc(const void* x, int n, int c, int hw, int c_pad, void* y, void* stream);
+int qd_nhwc_to_nchw(const void* x, int n, int c, int hw, int c_pad, void* y, void* stream);
+
+/* ---------------- attention ----------------------------------------------------------- */
+/* softmax(Q K^T * scale) V per (batch, head); Q [B, Sq, ldq] with head h at columns
+ * [h*D, h*D + D), same for K/V/O.  The SDPA of diffusers AttnProcessor2_0 (fp16 I/O, fp32
+ * softmax/accumulation). */
+int qd_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                 int ldo, int b, int heads, int sq, int skv, int d, float scale, void* stream);
+
+/* ---------------- time embedding / scheduler ---------------------------------------- */
+/* diffusers Timesteps(dim, flip_sin_to_cos, downscale_freq_shift) on timesteps[step_idx[0]]
+ * for b rows: out[b, dim] fp16. `timesteps` fp32 device array, `step_idx` int32 device scalar. */
+int qd_timestep_embedding(const float* timesteps, const int* step_idx, int b, int dim,
+                          int flip_sin_to_cos, float shift, void* out, void* stream);
+/* CFG + DDIM step (eta = 0) on fp16 latents [B, L]: eps = u + g*(c - u) from the UNet output
+ * [2B, L] (uncond first), x_{t-1} = sqrt(a_prev) * x0 + sqrt(1 - a_prev) * eps,
+ * x0 = (x - sqrt(1-a_t) eps)/sqrt(a_t).  alphas: fp32 [steps] a_t, [steps] a_prev; the
+ * step index is read from and then incremented in `step_idx` (graph-replayable).
+ * Also writes the next UNet input [2B, L] (latents duplicated, NHWC with c_pad channels). */
+int qd_cfg_ddim_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
+                     const float* alpha_t, const float* alpha_prev, int* step_idx,
+                     void* next_in, int c, int c_pad, void* stream);
+
+/* ---------------- calibration (SmoothQuant) ------------------------------------------ */
+/* Mean_Max_Activation_Hook (utils/calib_data.py:105-124): per-channel max |x| of x[rows, C]
+ * for one forward call, accumulated into sum[C] (fp32) for the later mean over calls
+ * (StableDiffusion1_x.py:104-112).  amax_out (fp16 [C]) optional: this call's values. */
+int qd_channel_absmax_accum(const void* x, int64_t rows, int c, float* amax_ws, float* sum,
+                            void* amax_out, void* stream);
+/* smooth_ln_fcs scales (quantizer_SQ.py:416-424): s = clamp(a^alpha / w^(1-alpha), 1e-5) in
+ * fp16 op order, a = act_mean (fp16 [C]), w = max over the nfc weight matrices [Ni][C] of
+ * max_k |W[k][c]| clamp 1e-5.  Applies ln.w /= s, ln.b /= s (ln_b may be NULL),
+ * W_i *= s in place.  fc_w / fc_rows are HOST arrays of nfc device pointers / row counts;
+ * wmax_ws is an fp32 [C] workspace. */
+int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const int* fc_rows, int nfc, int c,
+                   const void* act_mean, float alpha, float* wmax_ws, void* scales_out,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QDIFF_H */

@@ -1,0 +1,249 @@
+"""CPU oracle of the fake-quantized SD UNet denoising step (TEST INFRASTRUCTURE / CPU BASELINE).
+
+Independent of the product package: it consumes a flat diffusers-keyed state dict and a config
+dict, quantizes the weights with the golden-pinned numpy restatement (oracle/fake_quant_np.py)
+following the reference's diffusion swap decisions (quantizer.py:491-533), and runs the
+forward with torch-CPU fp16 NCHW ops in diffusers' op order - the same library calls the
+reference makes through diffusers (F.conv2d / F.linear from fake_quant.py:223,339, group_norm,
+layer_norm, SDPA, GEGLU, SiLU, nearest interpolate).
+
+Parity status: the fake-quant math is PINNED (golden vectors from the reference module); the
+UNet architecture/op order is restated from diffusers' published UNet2DConditionModel, which is
+not installed here -> that part is UNPINNED.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import fake_quant_np as FQ
+from . import fake_quant_torch as FT
+
+F16 = torch.float16
+
+
+# ------------------------------------------------------------------ weight quantization
+def quantize_state_dict(sd, qc):
+    """Return (qsd, flags): fake-quantized fp16 weights and per-layer activation flags.
+
+    qc keys (AwqConfig): w_bit, a_bit, q_group_size, weight_quant_type, weight_quant_conv_type,
+    act_quant_conv_type, quantize_act.  Linear = 2-D weight, Conv2d = 4-D weight.
+    """
+    qsd = dict(sd)
+    flags = {}
+    for key, w in sd.items():
+        if not key.endswith(".weight") or w.dim() not in (2, 4):
+            continue
+        name = key[: -len(".weight")]
+        child = name.split(".")[-1]
+        wn = w.to(F16).numpy()
+        if w.dim() == 2:
+            wt = qc.get("weight_quant_type", "group")
+            if wt == "group":
+                q = FQ.quantize_weight_absmax(wn, qc["w_bit"], qc.get("q_group_size", 128))
+            elif wt == "per_channel":
+                q = FQ.quantize_weight_per_channel_absmax(wn, qc["w_bit"])
+            elif wt == "per_tensor":
+                q = FQ.quantize_weight_per_tensor_absmax(wn, qc["w_bit"])
+            else:
+                raise ValueError(wt)
+            qout = "k_proj" in child or "v_proj" in child or "q_proj" in child
+            flags[name] = {"kind": "linear", "out_quant": qout, "a_bit": qc["a_bit"]}
+        else:
+            wt = qc.get("weight_quant_conv_type", "per_channel")
+            if wt == "per_channel":
+                q = FQ.quantize_weight_per_channel_absmax(wn, qc["w_bit"])
+            elif wt == "per_tensor":
+                q = FQ.quantize_weight_per_tensor_absmax(wn, qc["w_bit"])
+            else:
+                raise ValueError(wt)
+            flags[name] = {"kind": "conv", "act": qc.get("act_quant_conv_type", "per_channel"),
+                           "quant": bool(qc.get("quantize_act", False)), "a_bit": qc["a_bit"]}
+        qsd[key] = torch.from_numpy(np.ascontiguousarray(q))
+    return qsd, flags
+
+
+# ------------------------------------------------------------------ diffusers ops
+def timestep_embedding(t, dim, flip_sin_to_cos=True, shift=0.0, max_period=10000):
+    half = dim // 2
+    exponent = -math.log(max_period) * torch.arange(0, half, dtype=torch.float32)
+    exponent = exponent / (half - shift)
+    emb = torch.exp(exponent)
+    emb = t[:, None].float() * emb[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    return emb
+
+
+class RefUNet:
+    def __init__(self, cfg, sd, qc=None):
+        """cfg: dict of UNetConfig fields; sd: {key: fp16 cpu tensor}; qc: AwqConfig dict or None."""
+        self.cfg = cfg
+        sd = {k: v.detach().to("cpu", F16).contiguous() for k, v in sd.items()}
+        if qc is not None:
+            self.sd, self.flags = quantize_state_dict(sd, qc)
+        else:
+            self.sd, self.flags = sd, {}
+        self.hooks = None  # optional {linear name: callable(x)} for calibration
+
+    # ---- layers
+    def lin(self, name, x):
+        if self.hooks is not None and name in self.hooks:
+            self.hooks[name](x)
+        y = F.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias"))
+        f = self.flags.get(name)
+        if f and f["out_quant"]:
+            y = FT.per_token(y, f["a_bit"])
+        return y
+
+    def conv(self, name, x, stride=1, padding=None):
+        w = self.sd[name + ".weight"]
+        if padding is None:
+            padding = w.shape[-1] // 2
+        f = self.flags.get(name)
+        quant = f is not None and f["quant"]
+        if quant:
+            x = self._act(f, x)
+        y = F.conv2d(x, w, self.sd.get(name + ".bias"), stride, padding)
+        if quant:
+            y = self._act(f, y)
+        return y
+
+    def _act(self, f, x):
+        if f["act"] == "per_group":
+            return FT.per_group(x, 1, f["a_bit"])
+        return FT.ACT[f["act"]](x, f["a_bit"])
+
+    def gn(self, name, x, groups, eps):
+        return F.group_norm(x, groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)
+
+    def ln(self, name, x):
+        return F.layer_norm(x, (x.shape[-1],), self.sd[name + ".weight"], self.sd[name + ".bias"], 1e-5)
+
+    # ---- blocks
+    def resnet(self, p, x, temb):
+        g, eps = self.cfg["norm_num_groups"], self.cfg["norm_eps"]
+        h = F.silu(self.gn(p + ".norm1", x, g, eps))
+        h = self.conv(p + ".conv1", h)
+        t = self.lin(p + ".time_emb_proj", F.silu(temb))[:, :, None, None]
+        h = h + t
+        h = F.silu(self.gn(p + ".norm2", h, g, eps))
+        h = self.conv(p + ".conv2", h)
+        if p + ".conv_shortcut.weight" in self.sd:
+            x = self.conv(p + ".conv_shortcut", x)
+        return x + h
+
+    def attention(self, p, x, ctx, heads):
+        q = self.lin(p + ".to_q", x)
+        k = self.lin(p + ".to_k", ctx)
+        v = self.lin(p + ".to_v", ctx)
+        b = x.shape[0]
+        d = q.shape[-1] // heads
+        q = q.view(b, -1, heads, d).transpose(1, 2)
+        k = k.view(b, -1, heads, d).transpose(1, 2)
+        v = v.view(b, -1, heads, d).transpose(1, 2)
+        o = F.scaled_dot_product_attention(q, k, v, dropout_p=0.0, is_causal=False)
+        o = o.transpose(1, 2).reshape(b, -1, heads * d).to(q.dtype)
+        return self.lin(p + ".to_out.0", o)
+
+    def block(self, p, t, ctx, heads):
+        n = self.ln(p + ".norm1", t)
+        t = self.attention(p + ".attn1", n, n, heads) + t
+        n = self.ln(p + ".norm2", t)
+        t = self.attention(p + ".attn2", n, ctx, heads) + t
+        n = self.ln(p + ".norm3", t)
+        h, gate = self.lin(p + ".ff.net.0.proj", n).chunk(2, dim=-1)
+        return self.lin(p + ".ff.net.2", h * F.gelu(gate)) + t
+
+    def transformer(self, p, x, ctx, heads, layers):
+        b, c, hh, ww = x.shape
+        res = x
+        h = self.gn(p + ".norm", x, self.cfg["norm_num_groups"], 1e-6)
+        if self.cfg.get("use_linear_projection"):
+            h = h.permute(0, 2, 3, 1).reshape(b, hh * ww, c)
+            h = self.lin(p + ".proj_in", h)
+        else:
+            h = self.conv(p + ".proj_in", h)
+            h = h.permute(0, 2, 3, 1).reshape(b, hh * ww, c)
+        for i in range(layers):
+            h = self.block(f"{p}.transformer_blocks.{i}", h, ctx, heads)
+        if self.cfg.get("use_linear_projection"):
+            h = self.lin(p + ".proj_out", h)
+            h = h.reshape(b, hh, ww, c).permute(0, 3, 1, 2).contiguous()
+        else:
+            h = h.reshape(b, hh, ww, c).permute(0, 3, 1, 2).contiguous()
+            h = self.conv(p + ".proj_out", h)
+        return h + res
+
+    def _heads(self, i):
+        h = self.cfg["attention_head_dim"]
+        return h[i] if isinstance(h, (list, tuple)) else h
+
+    def _layers(self, i):
+        t = self.cfg.get("transformer_layers_per_block", 1)
+        return t[i] if isinstance(t, (list, tuple)) else t
+
+    @torch.no_grad()
+    def forward(self, x, t, ctx):
+        """x [2B, 4, h, w] fp16, t int timestep, ctx [2B, S, D] fp16 -> eps [2B, 4, h, w] fp16."""
+        cfg = self.cfg
+        ch = cfg["block_out_channels"]
+        b = x.shape[0]
+        temb = timestep_embedding(torch.full((b,), t, dtype=torch.int64), ch[0], cfg.get("flip_sin_to_cos", True),
+                                  cfg.get("freq_shift", 0)).to(F16)
+        temb = self.lin("time_embedding.linear_2", F.silu(self.lin("time_embedding.linear_1", temb)))
+        h = self.conv("conv_in", x)
+        skips = [h]
+        nlev = len(ch)
+        for i, typ in enumerate(cfg["down_block_types"]):
+            for j in range(cfg["layers_per_block"]):
+                h = self.resnet(f"down_blocks.{i}.resnets.{j}", h, temb)
+                if typ == "CrossAttnDownBlock2D":
+                    h = self.transformer(f"down_blocks.{i}.attentions.{j}", h, ctx, self._heads(i), self._layers(i))
+                skips.append(h)
+            if i < nlev - 1:
+                h = self.conv(f"down_blocks.{i}.downsamplers.0.conv", h, stride=2, padding=1)
+                skips.append(h)
+        h = self.resnet("mid_block.resnets.0", h, temb)
+        h = self.transformer("mid_block.attentions.0", h, ctx, self._heads(nlev - 1), self._layers(nlev - 1))
+        h = self.resnet("mid_block.resnets.1", h, temb)
+        for i, typ in enumerate(cfg["up_block_types"]):
+            lvl = nlev - 1 - i
+            for j in range(cfg["layers_per_block"] + 1):
+                h = torch.cat([h, skips.pop()], dim=1)
+                h = self.resnet(f"up_blocks.{i}.resnets.{j}", h, temb)
+                if typ == "CrossAttnUpBlock2D":
+                    h = self.transformer(f"up_blocks.{i}.attentions.{j}", h, ctx, self._heads(lvl), self._layers(lvl))
+            if i < nlev - 1:
+                h = F.interpolate(h, scale_factor=2.0, mode="nearest")
+                h = self.conv(f"up_blocks.{i}.upsamplers.0.conv", h)
+        h = F.silu(self.gn("conv_norm_out", h, cfg["norm_num_groups"], cfg["norm_eps"]))
+        return self.conv("conv_out", h)
+
+
+# ------------------------------------------------------------------ scheduler / loop
+def ddim_step(eps_cfg_in, t_idx, latents, a_t, a_p, guidance):
+    """CFG combine + DDIMScheduler.step (eta 0) in diffusers' op order (fp16 tensors, fp32
+    0-d scheduler scalars)."""
+    u, c = eps_cfg_in.chunk(2)
+    eps = u + guidance * (c - u)
+    at = a_t[t_idx]
+    ap = a_p[t_idx]
+    bt = 1 - at
+    x0 = (latents - bt ** 0.5 * eps) / at ** 0.5
+    direction = (1 - ap) ** 0.5 * eps
+    return ap ** 0.5 * x0 + direction
+
+
+@torch.no_grad()
+def denoise(unet, latents, ctx, timesteps, a_t, a_p, guidance=7.5, steps=None):
+    """The reference's pipeline loop on CPU: returns latents after `steps` steps."""
+    lat = latents.to(F16)
+    n = len(timesteps) if steps is None else steps
+    for i in range(n):
+        x = torch.cat([lat] * 2)
+        eps = unet.forward(x, int(timesteps[i]), ctx)
+        lat = ddim_step(eps, i, lat, a_t, a_p, guidance)
+    return lat

@@ -1,0 +1,89 @@
+"""ctypes binding of libqdiff.so (the C ABI declared in include/qdiff.h).
+
+The library is built in-tree (``csrc/Makefile`` -> ``libqdiff.so`` next to this file).  There is
+no fallback: if the library is missing or fails to load, every op raises ``RuntimeError``.
+torch is imported (and its HIP runtime loaded) before the library so that libqdiff resolves
+``libamdhip64.so.7`` to the runtime torch already uses: one HIP runtime, one set of streams.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libqdiff.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+F = ctypes.c_float
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    "qd_version": [],
+    "qd_device_arch": [ctypes.c_char_p, I],
+    "qd_act_absmax": [P, I, I, I, I, I, I, I, P, P],
+    "qd_act_fakequant": [P, P, I, I, I, I, I, I, I, I, P, P],
+    "qd_act_apply": [P, P, I, I, I, I, I, I, I, I, P, P],
+    "qd_weight_quant": [P, I, I, I, I, P, P, P, P],
+    "qd_pack_int4": [P, I, I, P, P],
+    "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
+    "qd_linear_fwd": [P, I, I, I, P, I, P, I, P, P, P, I, I, I, P, I, P],
+    "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P],
+    "qd_fq_finalize": [P, P, I, I, I, I, P, P, P, P],
+    "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P],
+    "qd_layernorm": [P, I, I, F, P, P, P, P],
+    "qd_geglu": [P, I, I, P, P],
+    "qd_silu": [P, P, I64, P],
+    "qd_add": [P, P, P, I64, P],
+    "qd_concat_c": [P, I, P, I, I64, P, P],
+    "qd_nchw_to_nhwc": [P, I, I, I, I, P, P],
+    "qd_nhwc_to_nchw": [P, I, I, I, I, P, P],
+    "qd_attention": [P, I, P, I, P, I, P, I, I, I, I, I, I, F, P],
+    "qd_timestep_embedding": [P, P, I, I, I, F, P, P],
+    "qd_cfg_ddim_step": [P, P, I, I64, F, P, P, P, P, I, I, P],
+    "qd_channel_absmax_accum": [P, I64, I, P, P, P, P],
+    "qd_smooth_fold": [P, P, P, P, I, I, P, F, P, P, P],
+}
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load libqdiff.so once; raise RuntimeError (never fall back) if it is unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise RuntimeError(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = (f"libqdiff.so not found at {LIB_PATH}; build it with "
+                       "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        raise RuntimeError(_load_error)
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - depends on the box
+        _load_error = f"failed to load {LIB_PATH}: {e}"
+        raise RuntimeError(_load_error) from e
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = I
+    lib.qd_last_error.argtypes = []
+    lib.qd_last_error.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke an ``int``-returning entry point; non-zero status -> RuntimeError."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.qd_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def exported_symbols():
+    return list(SIGNATURES) + ["qd_last_error"]

@@ -1,0 +1,268 @@
+"""BaseAWQForDiffusion: the public from_pretrained() / quantize() / generate() /
+save_quantized() / from_quantized() surface of models/base.py:120-850, on MI355X.
+
+Divergences from the reference, all deliberate and documented in DESIGN.md:
+* the pipeline lives on the GPU; quantize() quantizes weights there (the reference moves the
+  pipeline to CPU first, base.py:423) - the fp16 buffers are bit-identical;
+* generate() honours height / width / num_inference_steps / guidance_scale (the reference
+  passes only prompt, 50 steps, generator, latents, output_type: base.py:848).  The defaults
+  equal the reference's effective values, so default calls match;
+* there is no CLIP text encoder or VAE (SURVEY.md §8f "next"): prompts map to deterministic
+  synthetic embeddings unless prompt_embeds are given, and generate() returns latents;
+* from_pretrained() never contacts the hub; the hard-coded access token default of
+  base.py:188 is not reproduced.
+"""
+import json
+import os
+from typing import List, Optional, Union
+
+import torch
+from torch import nn
+
+from .config import AwqConfig
+from .fake_quant import WxAxConv2d, WxAxLinear
+from .pipeline import DenoiseLoop, synthetic_text_embeddings
+from .pipeline_io import QDiffPipeline, load_config, load_pipeline
+from .quantizer import AwqQuantizer, MyTraversal, SqQuantizer
+
+QUANTISABLE_COMPONENTS = ["unet", "text_encoder", "vae", "transformer"]
+
+
+class _HybridMethod:
+    """Callable on the class (constructs) or on an instance (reloads in place), because the
+    reference defines from_quantized as an instance method (base.py:736)."""
+
+    def __init__(self, f):
+        self.f = f
+
+    def __get__(self, obj, cls):
+        def bound(*a, **k):
+            return self.f(obj if obj is not None else cls, *a, **k)
+        return bound
+
+
+class BaseAWQForDiffusion(nn.Module):
+    def __init__(self, pipeline, model_type, is_quantized, config, quant_config):
+        super().__init__()
+        self.model_type = model_type
+        self.is_quantized = is_quantized
+        self.config = config
+        self.pipeline = pipeline
+        self.search_result = None
+        self.quant_config = quant_config
+        self._loops = {}
+
+    def to(self, device):
+        if self.pipeline is None:
+            raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
+        self.pipeline.to(device)
+        self._loops = {}
+        return self
+
+    # ---------------------------------------------------------------- loading
+    @classmethod
+    def from_pretrained(cls, model_path, model_type=None, torch_dtype=torch.float16, trust_remote_code=True,
+                        safetensors=True, device_map="auto", download_kwargs=None, low_cpu_mem_usage=True,
+                        use_cache=False, refiner_path=None, token=None, device="cuda", seed=0,
+                        **model_init_kwargs):
+        """base.py:143-212 (local directories / synthetic names only; fp16 always, as base.py:199)."""
+        pipe = load_pipeline(model_path, device=device, seed=seed)
+        quant_config = AwqConfig.from_pretrained(model_path, is_diffusion_model=True)
+        config = load_config(model_path)
+        model_type = config["_class_name"]
+        return cls(pipe, model_type, is_quantized=False, config=config, quant_config=quant_config,
+                   refiner_path=refiner_path, access_token=token)
+
+    # ---------------------------------------------------------------- quantize
+    @torch.no_grad()
+    def quantize(self, tokenizer=None, quant_config={}, calib_data="pileval", split="train", text_column="text",
+                 duo_scaling=True, export_compatible=False, quant_act=False, apply_clip=True, applyScale=True,
+                 samples=512, calib_data_type="", blocksize=512, n_parallel_calib_samples=None,
+                 max_calib_samples=128, max_calib_seq_len=512, max_chunk_memory=1024 * 1024 * 1024,
+                 quantizer_cls=AwqQuantizer, quantType="awq", LLM_ViT_serial=False, quantVision=False,
+                 quantText=True, quantVisionProjection=False, quantTextProjection=False, quantUnet=False,
+                 quantTextEncoder=False, quantVAE=False, quantTransformer=False, diffusion_model=True,
+                 codeBookQuantInd=False, debugPlot=False, debugAttentionMap=False, debugSavePath="",
+                 calibration=None, **kwargs):
+        """base.py:215-528.  quantType 'awq' = RTN swap; 'sq' = SmoothQuant fold + swap."""
+        if quant_act and quant_config.get("version", "fake_act").lower() != "fake_act":
+            print("With activation quantization set to True, you can only use the fake quant kernel fake_act! "
+                  "Changing to that....")
+            quant_config["version"] = "fake_act"
+        self.quant_config = AwqConfig.from_dict(quant_config)
+        if hasattr(self, "modules_to_not_convert"):
+            self.quant_config.modules_to_not_convert = self.modules_to_not_convert
+        qc = self.quant_config
+        common = dict(modules_to_not_convert=qc.modules_to_not_convert, export_compatible=export_compatible,
+                      quant_act=quant_act, apply_clip=apply_clip, applyScale=applyScale, samples=samples,
+                      calib_data_type=calib_data_type, blocksize=blocksize, quantUnet=quantUnet,
+                      quantTextEncoder=quantTextEncoder, quantVAE=quantVAE, quantTransformer=quantTransformer,
+                      diffusion_model=True, codeBookQuantInd=codeBookQuantInd)
+        args = (self, None, None, qc.quantize_act, qc.weight_quant_conv_type, qc.weight_quant_type,
+                qc.act_quant_conv_type, qc.act_quant_conv_group_size, qc.w_bit, qc.wv_bit, qc.a_bit,
+                qc.q_group_size, qc.zero_point, qc.version, calib_data, split, text_column, duo_scaling)
+        if quantType.lower() == "awq":
+            self.quantizer = quantizer_cls(*args, **common, **kwargs)
+        elif quantType.lower() == "sq":
+            self.quantizer = SqQuantizer(*args, **common, calibration=calibration)
+        else:
+            raise NotImplementedError("Only awq and sq are supported for now.")
+        self.quantizer.quantize(debugSavePath, debugPlot)
+        self.is_quantized = True
+        self._loops = {}
+
+    # ---------------------------------------------------------------- generate
+    def _text_context(self, prompt, negative_prompt, prompt_embeds, negative_prompt_embeds):
+        dim = self.pipeline.unet.config.cross_attention_dim
+        dev = self.pipeline.device
+        if prompt_embeds is None:
+            prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+            prompt_embeds = synthetic_text_embeddings(prompts, dim=dim, device=dev)
+        if negative_prompt_embeds is None:
+            b = prompt_embeds.shape[0]
+            neg = negative_prompt if negative_prompt is not None else ""
+            negs = [neg] * b if isinstance(neg, str) else list(neg)
+            negative_prompt_embeds = synthetic_text_embeddings(negs, seq_len=prompt_embeds.shape[1], dim=dim,
+                                                               device=dev)
+        return torch.cat([negative_prompt_embeds.to(dev), prompt_embeds.to(dev)]).to(torch.float16).contiguous()
+
+    def get_loop(self, batch, height, width, steps, guidance, use_graph=True):
+        key = (batch, height, width, steps, float(guidance), use_graph)
+        if key not in self._loops:
+            self._loops[key] = DenoiseLoop(self.pipeline.unet, batch, height, width, steps, guidance,
+                                           device=self.pipeline.device, use_graph=use_graph,
+                                           sched_cfg=self.pipeline.scheduler_config)
+        return self._loops[key]
+
+    @torch.no_grad()
+    def generate(self, prompt=None, height=512, width=512, num_inference_steps=50, guidance_scale=7.5,
+                 negative_prompt=None, num_images_per_prompt=1, generator=None, device="cpu", lat=None,
+                 output_type=None, prompt_embeds=None, negative_prompt_embeds=None, use_graph=True, **kwargs):
+        """base.py:828-850 -> the device denoising loop; returns latents [B, 4, h, w] fp16."""
+        if self.pipeline is None:
+            raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
+        if output_type not in (None, "latent"):
+            raise NotImplementedError("VAE decoding is not part of this build (SURVEY.md §8f); use output_type='latent'")
+        ctx = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds)
+        if num_images_per_prompt > 1:
+            b0 = ctx.shape[0] // 2
+            ctx = torch.cat([ctx[:b0].repeat_interleave(num_images_per_prompt, 0),
+                             ctx[b0:].repeat_interleave(num_images_per_prompt, 0)])
+        b = ctx.shape[0] // 2
+        cin = self.pipeline.unet.config.in_channels
+        shape = (b, cin, height // 8, width // 8)
+        if lat is None:
+            lat = torch.randn(shape, generator=generator, dtype=torch.float32).to(torch.float16)
+        loop = self.get_loop(b, height, width, num_inference_steps, guidance_scale, use_graph)
+        return loop.run(lat.to(self.pipeline.device), ctx)
+
+    # ---------------------------------------------------------------- save / load
+    def save_quantized(self, save_dir, safetensors=True, shard_size="5GB", export_compatible=False, quant_act=False):
+        """base.py:530-582: pipeline files + quantization_config in each quantized component's
+        config.json + quant_components.json (reference-compatible fp16 dequantized buffers), plus
+        our extension: the integer codes / scales (unet/qdiff_codes.safetensors) and the full
+        quant config (qdiff_quant.json)."""
+        from safetensors.torch import save_file
+        save_dir = save_dir[:-1] if save_dir.endswith("/") else save_dir
+        os.makedirs(save_dir, exist_ok=True)
+        self.pipeline.save_pretrained(save_dir, safe_serialization=safetensors)
+        for comp in self.quantized_components:
+            cpath = os.path.join(save_dir, comp, "config.json")
+            if not os.path.exists(cpath):
+                continue
+            with open(cpath) as f:
+                cfg = json.load(f)
+            cfg["quantization_config"] = self.quant_config.to_transformers_dict()
+            with open(cpath, "w") as f:
+                json.dump(cfg, f, indent=2)
+        with open(os.path.join(save_dir, "quant_components.json"), "w") as f:
+            json.dump(self.quantized_components, f, indent=2)
+        with open(os.path.join(save_dir, "qdiff_quant.json"), "w") as f:
+            json.dump(self.quant_config.full_dict(), f, indent=2)
+        codes = {}
+        for name, m in self.pipeline.unet.named_modules():
+            if isinstance(m, WxAxLinear) and m.qcodes is not None:
+                codes[f"{name}.qcodes"] = m.qcodes.detach().cpu().contiguous()
+                codes[f"{name}.qscales"] = m.qscales.detach().cpu().contiguous()
+                codes[f"{name}.qmeta"] = torch.tensor([m.qgroup, m.n_bits_W], dtype=torch.int32)
+        if codes:
+            save_file(codes, os.path.join(save_dir, "unet", "qdiff_codes.safetensors"))
+
+    def _load_quantized_modules(self, module, bitWidth=4, group_size=128, act_bits=16, full_config=None):
+        return load_quantized_modules(module, bitWidth, group_size, act_bits, full_config)
+
+
+    @_HybridMethod
+    def from_quantized(self_or_cls, model_path, model_type=None, model_filename="", torch_dtype=torch.float16,
+                       safetensors=True, fuse_layers=True, use_ipex=False, device_map="balanced", max_memory=None,
+                       offload_folder=None, download_kwargs=None, device="cuda"):
+        """base.py:736-826 (usable on an instance, as in the reference, or on the class)."""
+        from safetensors.torch import load_file
+        from .unet import UNet2DConditionModel, UNetConfig
+        with open(os.path.join(model_path, "quant_components.json")) as f:
+            comps = json.load(f)
+        with open(os.path.join(model_path, "unet", "config.json")) as f:
+            ucfg_d = json.load(f)
+        unet = UNet2DConditionModel(UNetConfig.from_diffusers(ucfg_d)).half().to(device)
+        qc = ucfg_d["quantization_config"]
+        full = None
+        fpath = os.path.join(model_path, "qdiff_quant.json")
+        if os.path.exists(fpath):
+            with open(fpath) as f:
+                full = json.load(f)
+        qcfg = AwqConfig(**full) if full else AwqConfig(**AwqConfig.from_transformers_dict(AwqConfig, qc))
+        load_quantized_modules(unet, bitWidth=qc["bits"], group_size=qc["group_size"], act_bits=qc["act_bits"],
+                               full_config=full)
+        sd = load_file(os.path.join(model_path, "unet", "diffusion_pytorch_model.safetensors"))
+        unet.load_state_dict({k: v.to(device) for k, v in sd.items()}, strict=True)
+        cpath = os.path.join(model_path, "unet", "qdiff_codes.safetensors")
+        if os.path.exists(cpath):
+            codes = load_file(cpath)
+            for name, m in unet.named_modules():
+                if isinstance(m, WxAxLinear) and f"{name}.qcodes" in codes:
+                    g, nb = codes[f"{name}.qmeta"].tolist()
+                    m.qcodes = codes[f"{name}.qcodes"].to(device)
+                    m.qscales = codes[f"{name}.qscales"].to(device)
+                    m.qgroup, m.n_bits_W = g, nb
+                    m.qfmt = "i4" if nb <= 4 else "i8"
+        with open(os.path.join(model_path, "model_index.json")) as f:
+            cls_name = json.load(f)["_class_name"]
+        pipe = QDiffPipeline(unet, cls_name, config={"_class_name": cls_name})
+        if isinstance(self_or_cls, type):
+            obj = self_or_cls(pipe, cls_name, is_quantized=True, config={"_class_name": cls_name}, quant_config=qcfg)
+        else:
+            obj = self_or_cls
+            obj.pipeline = pipe
+            obj.is_quantized = True
+            obj.quant_config = qcfg
+            obj._loops = {}
+        obj.quantized_components = comps
+        return obj
+
+
+def load_quantized_modules(module, bitWidth=4, group_size=128, act_bits=16, full_config=None):
+    """base.py:658-692: init_only WxAx modules in place of every Linear / Conv2d.  Without our
+    qdiff_quant.json (a reference checkpoint) conv layers get quantize_output=True and
+    per_channel act quant, exactly as base.py:680-690 forces."""
+    for name, child in module.named_children():
+        trav = MyTraversal()
+        trav.traverse(name, child, module)
+        for parent, lname, layer in trav.get_lin_conv():
+            qbmm = "k_proj" in lname or "v_proj" in lname or "q_proj" in lname
+            if isinstance(layer, nn.Linear):
+                fake = WxAxLinear.from_float(layer, init_only=True, weight_quant="group", act_quant="per_token",
+                                             quantize_output=qbmm, n_bits_W=bitWidth, n_bits_A=act_bits,
+                                             group_size_W=group_size)
+            else:
+                if full_config is not None:
+                    fake = WxAxConv2d.from_float(layer, init_only=True,
+                                                 weight_quant=full_config["weight_quant_conv_type"],
+                                                 act_quant=full_config["act_quant_conv_type"],
+                                                 act_group_size=full_config["act_quant_conv_group_size"],
+                                                 quantize_output=full_config["quantize_act"],
+                                                 n_bits_W=bitWidth, n_bits_A=act_bits)
+                else:
+                    fake = WxAxConv2d.from_float(layer, init_only=True, weight_quant="per_channel",
+                                                 act_quant="per_channel", n_bits_W=bitWidth, n_bits_A=act_bits,
+                                                 quantize_output=True)
+            setattr(parent, lname, fake)

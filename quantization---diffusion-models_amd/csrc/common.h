@@ -1,0 +1,75 @@
+// Shared device helpers for libqdiff (gfx950 / CDNA4, wave64).
+//
+// Numerics contract (pinned by tests/golden/*.npz): every fake-quant op
+// is an fp16 op computed in fp32 and rounded to fp16 once (round-to-nearest-even), exactly as
+// PyTorch-CPU Half arithmetic does in the reference (quantize/fake_quant.py:44-46, 72, 114-117).
+// Division must be the IEEE-correct fp32 divide (hipcc default; never build with -ffast-math).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include "../../include/qdiff.h"
+
+typedef _Float16 f16;
+typedef f16 f16x4 __attribute__((ext_vector_type(4)));
+typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define QD_WAVE 64
+
+namespace qd {
+
+// half(1e-5): the fp16 image of clamp_(min=1e-5) (no fp16 lies strictly between 1e-5 and it).
+__device__ __forceinline__ float clamp_min_f16() { return (float)(f16)1e-5f; }
+
+// s = half( half(max(amax, 1e-5)) / qmax )     fake_quant.py:44-46, 114-116, 127-129
+__device__ __forceinline__ float fq_scale(float amax, int qmax) {
+  float a = fmaxf(amax, clamp_min_f16());
+  return (float)(f16)(a / (float)qmax);
+}
+
+// y = half( rint(half(x / s)) * s )            fake_quant.py:72, 117, 130
+__device__ __forceinline__ f16 fq_apply(float x, float s) {
+  f16 t = (f16)(x / s);
+  float q = __builtin_rintf((float)t);
+  return (f16)(q * s);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// non-negative float max through the uint image (valid for +0 and positive finite/inf)
+__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
+  atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+// exact-erf GELU as torch's F.gelu(approximate='none')
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+}  // namespace qd
+
+#define QD_CHECK_LAUNCH()                                              \
+  do {                                                                 \
+    hipError_t _e = hipGetLastError();                                 \
+    if (_e != hipSuccess) return qd_set_error((int)_e, hipGetErrorString(_e)); \
+  } while (0)
+
+#define QD_REQUIRE(cond, msg)                                          \
+  do {                                                                 \
+    if (!(cond)) return qd_set_error(QD_ERR_ARG, msg);                 \
+  } while (0)
+
+extern "C" int qd_set_error(int code, const char* msg);

@@ -1,0 +1,427 @@
+// UNet elementwise / normalisation kernels (diffusers ops the reference runs in fp16 on CPU):
+// GroupNorm(+SiLU)(+fused per-(n,c) act fake-quant), LayerNorm, GEGLU, SiLU, add, channel
+// concat, NCHW<->NHWC, Timesteps embedding, CFG + DDIM step.
+//
+// Op-boundary rounding follows PyTorch-CPU Half: each torch op computes in fp32 and rounds
+// its output to fp16 (GroupNorm output, then SiLU output, then the fake-quant chain).
+#include "common.h"
+
+using namespace qd;
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static int grid1(long count, int per_block = 256) { return (int)((count + per_block - 1) / per_block); }
+
+// ---------------------------------------------------------------------------------------
+// GroupNorm on NHWC [N, HW, C] with an optional second source for channels [c1, C).
+// One 256-thread workgroup per (n, group).  Thread t owns channel pair p = t % P (P = cg/2) and
+// visits rows t/P, t/P + R, ... (R = 256 / P), so per-channel amax stays in registers.
+// Passes: mean, variance (two-pass, fp32), then [amax of the final fp16 output], then write.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ const f16* gn_src(const f16* x, const f16* x2, int c1, int c, long row,
+                                             int ch) {
+  return ch < c1 ? x + row * c1 + ch : x2 + row * (c - c1) + (ch - c1);
+}
+
+__global__ void __launch_bounds__(256) k_groupnorm(const f16* __restrict__ x, const f16* __restrict__ x2,
+                                                   int c1, int hw, int c, int groups, float eps,
+                                                   const f16* __restrict__ gamma,
+                                                   const f16* __restrict__ beta, int silu, int qmax,
+                                                   f16* __restrict__ y) {
+  __shared__ float red[8];
+  __shared__ float chmax[256];
+  const int n = blockIdx.x / groups;
+  const int g = blockIdx.x % groups;
+  const int cg = c / groups;
+  const int P = cg >> 1;
+  const int R = 256 / P;
+  const int t = threadIdx.x;
+  const bool active = t < P * R;
+  const int p = t % P;
+  const int r0 = t / P;
+  const int ch = g * cg + 2 * p;
+  const long rowbase = (long)n * hw;
+
+  // pass 1: mean
+  float s = 0.f;
+  if (active)
+    for (int r = r0; r < hw; r += R) {
+      const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
+      s += (float)__low2float(v) + (float)__high2float(v);
+    }
+  s = wave_sum(s);
+  if ((t & 63) == 0) red[t >> 6] = s;
+  __syncthreads();
+  const float cnt = (float)cg * (float)hw;
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / cnt;
+  __syncthreads();
+  // pass 2: variance (population)
+  float v2 = 0.f;
+  if (active)
+    for (int r = r0; r < hw; r += R) {
+      const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
+      const float a = __low2float(v) - mean, b = __high2float(v) - mean;
+      v2 += a * a + b * b;
+    }
+  v2 = wave_sum(v2);
+  if ((t & 63) == 0) red[4 + (t >> 6)] = v2;
+  __syncthreads();
+  const float var = (red[4] + red[5] + red[6] + red[7]) / cnt;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const float sc0 = rstd * (float)gamma[ch], sc1 = rstd * (float)gamma[ch + 1];
+  const float bi0 = fmaf(-sc0, mean, (float)beta[ch]), bi1 = fmaf(-sc1, mean, (float)beta[ch + 1]);
+
+  auto out_val = [&](float xv, float sc, float bi) -> float {
+    f16 o = (f16)fmaf(xv, sc, bi);
+    if (silu) o = (f16)silu_f((float)o);
+    return (float)o;
+  };
+
+  float s0 = 0.f, s1 = 0.f;
+  if (qmax > 0) {
+    // pass 3: per-channel amax of the rounded output (fake_quant.py:125 reduction)
+    float m0 = 0.f, m1 = 0.f;
+    if (active)
+      for (int r = r0; r < hw; r += R) {
+        const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
+        m0 = fmaxf(m0, fabsf(out_val(__low2float(v), sc0, bi0)));
+        m1 = fmaxf(m1, fabsf(out_val(__high2float(v), sc1, bi1)));
+      }
+    // reduce over the R row-lanes sharing a pair: through LDS
+    chmax[t] = m0;
+    __syncthreads();
+    if (t < P) {
+      float m = 0.f;
+      for (int i = 0; i < R; ++i) m = fmaxf(m, chmax[t + i * P]);
+      chmax[t] = m;  // slot t < P now holds channel 2t's amax
+    }
+    __syncthreads();
+    const float a0 = chmax[p];
+    __syncthreads();
+    chmax[t] = m1;
+    __syncthreads();
+    if (t < P) {
+      float m = 0.f;
+      for (int i = 0; i < R; ++i) m = fmaxf(m, chmax[t + i * P]);
+      chmax[t] = m;
+    }
+    __syncthreads();
+    const float a1 = chmax[p];
+    s0 = fq_scale(a0, qmax);
+    s1 = fq_scale(a1, qmax);
+  }
+  // pass 4: write
+  if (active)
+    for (int r = r0; r < hw; r += R) {
+      const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
+      float o0 = out_val(__low2float(v), sc0, bi0);
+      float o1 = out_val(__high2float(v), sc1, bi1);
+      f16 h0, h1;
+      if (qmax > 0) {
+        h0 = fq_apply(o0, s0);
+        h1 = fq_apply(o1, s1);
+      } else {
+        h0 = (f16)o0;
+        h1 = (f16)o1;
+      }
+      f16* dst = y + (rowbase + r) * c + ch;
+      dst[0] = h0;
+      dst[1] = h1;
+    }
+}
+
+extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
+                            float eps, const void* gamma, const void* beta, int silu, int q_bits,
+                            void* y, void* stream) {
+  QD_REQUIRE(x && gamma && beta && y, "null pointer");
+  QD_REQUIRE(groups > 0 && c % groups == 0, "groups must divide C");
+  const int cg = c / groups;
+  QD_REQUIRE(cg % 2 == 0 && cg <= 512, "channels per group must be even and <= 512");
+  if (x2) QD_REQUIRE(c1 % 2 == 0 && c1 > 0 && c1 < c, "bad concat split");
+  else c1 = c;
+  QD_REQUIRE(q_bits == 0 || (q_bits >= 2 && q_bits <= 16), "bad q_bits");
+  if ((long)n * hw == 0) return 0;
+  k_groupnorm<<<n * groups, 256, 0, S(stream)>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, eps,
+                                                 (const f16*)gamma, (const f16*)beta, silu,
+                                                 q_bits ? (1 << (q_bits - 1)) - 1 : 0, (f16*)y);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// LayerNorm over the last dim: one wave per row, row held in registers (C <= 4096).
+// ---------------------------------------------------------------------------------------
+template <int PER>  // half2 pairs per lane
+__global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, long rows, int c, float eps,
+                                                   const f16* __restrict__ gamma,
+                                                   const f16* __restrict__ beta, f16* __restrict__ y) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int pairs = c >> 1;
+  const __half2* p = reinterpret_cast<const __half2*>(x + row * c);
+  float v[2 * PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + i * 64;
+    if (j < pairs) {
+      const __half2 h = p[j];
+      v[2 * i] = __low2float(h);
+      v[2 * i + 1] = __high2float(h);
+    } else {
+      v[2 * i] = v[2 * i + 1] = 0.f;
+    }
+    s += v[2 * i] + v[2 * i + 1];
+  }
+  const float mean = wave_sum(s) / (float)c;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + i * 64;
+    if (j < pairs) {
+      const float a = v[2 * i] - mean, b = v[2 * i + 1] - mean;
+      q += a * a + b * b;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)c + eps);
+  __half2* o = reinterpret_cast<__half2*>(y + row * c);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + i * 64;
+    if (j < pairs) {
+      const int ch = 2 * j;
+      const float a = fmaf((v[2 * i] - mean) * rstd, (float)gamma[ch], (float)beta[ch]);
+      const float b = fmaf((v[2 * i + 1] - mean) * rstd, (float)gamma[ch + 1], (float)beta[ch + 1]);
+      o[j] = __floats2half2_rn(a, b);
+    }
+  }
+}
+
+extern "C" int qd_layernorm(const void* x, int rows, int c, float eps, const void* gamma,
+                            const void* beta, void* y, void* stream) {
+  QD_REQUIRE(x && gamma && beta && y, "null pointer");
+  QD_REQUIRE(c % 2 == 0 && c <= 8192, "LayerNorm needs even C <= 8192");
+  if (rows == 0) return 0;
+  const int pairs = c / 2;
+  const int per = (pairs + 63) / 64;
+  dim3 grid(grid1(rows, 4));
+  hipStream_t st = S(stream);
+  if (per <= 4) k_layernorm<4><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
+  else if (per <= 8) k_layernorm<8><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
+  else if (per <= 16) k_layernorm<16><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
+  else if (per <= 32) k_layernorm<32><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
+  else k_layernorm<64><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// GEGLU, SiLU, add, concat, layout transposes
+// ---------------------------------------------------------------------------------------
+__global__ void k_geglu(const f16* __restrict__ h, long m, int inner, f16* __restrict__ out) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // index into out (pairs)
+  const long total = m * inner / 2;
+  if (e >= total) return;
+  const long row = (2 * e) / inner;
+  const int col = (int)((2 * e) % inner);
+  const __half2 a = *reinterpret_cast<const __half2*>(h + row * 2 * inner + col);
+  const __half2 g = *reinterpret_cast<const __half2*>(h + row * 2 * inner + inner + col);
+  const f16 g0 = (f16)gelu_f(__low2float(g)), g1 = (f16)gelu_f(__high2float(g));
+  const f16 o0 = (f16)(__low2float(a) * (float)g0), o1 = (f16)(__high2float(a) * (float)g1);
+  f16* dst = out + row * inner + col;
+  dst[0] = o0;
+  dst[1] = o1;
+}
+
+extern "C" int qd_geglu(const void* h, int m, int inner, void* out, void* stream) {
+  QD_REQUIRE(h && out && inner % 2 == 0, "bad geglu args");
+  const long total = (long)m * inner / 2;
+  if (total == 0) return 0;
+  k_geglu<<<grid1(total), 256, 0, S(stream)>>>((const f16*)h, m, inner, (f16*)out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void k_silu(const f16* __restrict__ x, f16* __restrict__ y, long count) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < count) y[e] = (f16)silu_f((float)x[e]);
+}
+
+extern "C" int qd_silu(const void* x, void* y, int64_t count, void* stream) {
+  QD_REQUIRE(x && y, "null pointer");
+  if (count == 0) return 0;
+  k_silu<<<grid1(count), 256, 0, S(stream)>>>((const f16*)x, (f16*)y, count);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void k_add(const f16* __restrict__ a, const f16* __restrict__ b, f16* __restrict__ y, long count) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < count) y[e] = (f16)((float)a[e] + (float)b[e]);
+}
+
+extern "C" int qd_add(const void* a, const void* b, void* y, int64_t count, void* stream) {
+  QD_REQUIRE(a && b && y, "null pointer");
+  if (count == 0) return 0;
+  k_add<<<grid1(count), 256, 0, S(stream)>>>((const f16*)a, (const f16*)b, (f16*)y, count);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void k_concat(const f16* __restrict__ a, int c1, const f16* __restrict__ b, int c2, long m,
+                         f16* __restrict__ out) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const int c = c1 + c2;
+  if (e >= m * c) return;
+  const long r = e / c;
+  const int ch = e % c;
+  out[e] = ch < c1 ? a[r * c1 + ch] : b[r * c2 + ch - c1];
+}
+
+extern "C" int qd_concat_c(const void* a, int c1, const void* b, int c2, int64_t m, void* out, void* stream) {
+  QD_REQUIRE(a && b && out, "null pointer");
+  if (m == 0) return 0;
+  k_concat<<<grid1(m * (c1 + c2)), 256, 0, S(stream)>>>((const f16*)a, c1, (const f16*)b, c2, m, (f16*)out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// 64x64 tiled transpose through LDS: [N][C][HW] <-> [N][HW][Cp]
+__global__ void k_nchw_to_nhwc(const f16* __restrict__ x, int c, int hw, int cp, f16* __restrict__ y) {
+  __shared__ f16 tile[64][65];
+  const int n = blockIdx.z;
+  const int c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+  const f16* xs = x + (long)n * c * hw;
+  f16* ys = y + (long)n * hw * cp;
+  for (int i = threadIdx.y; i < 64; i += 4) {
+    const int ch = c0 + i, p = p0 + threadIdx.x;
+    tile[i][threadIdx.x] = (ch < c && p < hw) ? xs[(long)ch * hw + p] : (f16)0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 64; i += 4) {
+    const int p = p0 + i, ch = c0 + threadIdx.x;
+    if (p < hw && ch < cp) ys[(long)p * cp + ch] = tile[threadIdx.x][i];
+  }
+}
+
+__global__ void k_nhwc_to_nchw(const f16* __restrict__ x, int c, int hw, int cp, f16* __restrict__ y) {
+  __shared__ f16 tile[64][65];
+  const int n = blockIdx.z;
+  const int c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+  const f16* xs = x + (long)n * hw * cp;
+  f16* ys = y + (long)n * c * hw;
+  for (int i = threadIdx.y; i < 64; i += 4) {
+    const int p = p0 + i, ch = c0 + threadIdx.x;
+    tile[i][threadIdx.x] = (p < hw && ch < c) ? xs[(long)p * cp + ch] : (f16)0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 64; i += 4) {
+    const int ch = c0 + i, p = p0 + threadIdx.x;
+    if (ch < c && p < hw) ys[(long)ch * hw + p] = tile[threadIdx.x][i];
+  }
+}
+
+extern "C" int qd_nchw_to_nhwc(const void* x, int n, int c, int hw, int c_pad, void* y, void* stream) {
+  QD_REQUIRE(x && y && c_pad >= c, "bad args");
+  if ((long)n * hw == 0) return 0;
+  dim3 grid((hw + 63) / 64, (c_pad + 63) / 64, n);
+  k_nchw_to_nhwc<<<grid, dim3(64, 4), 0, S(stream)>>>((const f16*)x, c, hw, c_pad, (f16*)y);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int qd_nhwc_to_nchw(const void* x, int n, int c, int hw, int c_pad, void* y, void* stream) {
+  QD_REQUIRE(x && y && c_pad >= c, "bad args");
+  if ((long)n * hw == 0) return 0;
+  dim3 grid((hw + 63) / 64, (c + 63) / 64, n);
+  k_nhwc_to_nchw<<<grid, dim3(64, 4), 0, S(stream)>>>((const f16*)x, c, hw, c_pad, (f16*)y);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// diffusers Timesteps / get_timestep_embedding (max_period 10000, scale 1)
+// ---------------------------------------------------------------------------------------
+__global__ void k_temb(const float* __restrict__ ts, const int* __restrict__ step_idx, int b, int dim,
+                       int flip, float shift, f16* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int half_dim = dim / 2;
+  if (i >= b * half_dim) return;
+  const int row = i / half_dim, k = i % half_dim;
+  const float t = ts[step_idx ? step_idx[0] : 0];
+  const float ex = (-9.210340371976184f * (float)k) / ((float)half_dim - shift);  // -ln(1e4)*k/(h-s)
+  const float arg = t * expf(ex);
+  const float sv = sinf(arg), cv = cosf(arg);
+  f16* o = out + (long)row * dim;
+  if (flip) {
+    o[k] = (f16)cv;
+    o[half_dim + k] = (f16)sv;
+  } else {
+    o[k] = (f16)sv;
+    o[half_dim + k] = (f16)cv;
+  }
+}
+
+extern "C" int qd_timestep_embedding(const float* timesteps, const int* step_idx, int b, int dim,
+                                     int flip_sin_to_cos, float shift, void* out, void* stream) {
+  QD_REQUIRE(timesteps && out && dim % 2 == 0, "bad args");
+  k_temb<<<grid1((long)b * dim / 2), 256, 0, S(stream)>>>(timesteps, step_idx, b, dim, flip_sin_to_cos,
+                                                          shift, (f16*)out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// CFG combine + DDIM step (eta = 0), diffusers op order with fp16 rounding per torch op:
+//   eps  = u + g * (c - u)                       pipeline_stable_diffusion.py (CFG)
+//   x0   = (x - sqrt(1 - a_t) * eps) / sqrt(a_t) DDIMScheduler.step
+//   prev = sqrt(a_prev) * x0 + sqrt(1 - a_prev) * eps
+// latents / unet_out are NHWC with c_pad channel stride (only c used); next_in = [x; x].
+// ---------------------------------------------------------------------------------------
+__global__ void k_cfg_ddim(f16* __restrict__ lat, const f16* __restrict__ uo, int b, long l, float g,
+                           const float* __restrict__ at, const float* __restrict__ ap,
+                           const int* __restrict__ step_idx, f16* __restrict__ next_in, int c, int cp) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // over b * l (l = pixels * cp)
+  if (e >= (long)b * l) return;
+  const int ch = e % cp;
+  const int si = step_idx[0];
+  const float a_t = at[si], a_p = ap[si];
+  f16 out;
+  if (ch < c) {
+    const long bi = e / l, off = e % l;
+    const float u = (float)uo[bi * l + off];
+    const float cc = (float)uo[((long)b + bi) * l + off];
+    const f16 diff = (f16)(cc - u);
+    const f16 gd = (f16)(g * (float)diff);
+    const f16 eps = (f16)(u + (float)gd);
+    const float sb = sqrtf(1.0f - a_t), sa = sqrtf(a_t);
+    const f16 t1 = (f16)(sb * (float)eps);
+    const f16 t2 = (f16)((float)lat[e] - (float)t1);
+    const f16 x0 = (f16)((float)t2 / sa);
+    const f16 dir = (f16)(sqrtf(1.0f - a_p) * (float)eps);
+    const f16 t3 = (f16)(sqrtf(a_p) * (float)x0);
+    out = (f16)((float)t3 + (float)dir);
+  } else {
+    out = (f16)0.f;
+  }
+  lat[e] = out;
+  if (next_in) {
+    next_in[e] = out;
+    next_in[(long)b * l + e] = out;
+  }
+}
+
+__global__ void k_step_inc(int* step_idx) { step_idx[0] += 1; }
+
+extern "C" int qd_cfg_ddim_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
+                                const float* alpha_t, const float* alpha_prev, int* step_idx,
+                                void* next_in, int c, int c_pad, void* stream) {
+  QD_REQUIRE(latents && unet_out && alpha_t && alpha_prev && step_idx, "null pointer");
+  QD_REQUIRE(c_pad >= c && l % c_pad == 0, "bad channel padding");
+  hipStream_t st = S(stream);
+  k_cfg_ddim<<<grid1((long)b * l), 256, 0, st>>>((f16*)latents, (const f16*)unet_out, b, l, guidance,
+                                                 alpha_t, alpha_prev, step_idx, (f16*)next_in, c, c_pad);
+  k_step_inc<<<1, 1, 0, st>>>(step_idx);
+  QD_CHECK_LAUNCH();
+  return 0;
+}

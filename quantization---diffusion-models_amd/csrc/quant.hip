@@ -1,0 +1,517 @@
+// Fake-quant kernels: activation / weight absmax RTN (quantize/fake_quant.py:21-167),
+// the conv-output finalize pass, SmoothQuant calibration reductions and the SQ fold
+// (utils/calib_data.py:105-124, quantizer_SQ.py:395-431).
+//
+// Bit-exactness: every kernel reproduces the reference's fp16 op-boundary rounding (common.h);
+// tests/test_gpu_quant.py compares them bit-for-bit with tests/golden/fake_quant_golden.npz.
+#include "common.h"
+
+#include <atomic>
+#include <cstring>
+
+using namespace qd;
+
+static thread_local char g_err[256] = "";
+extern "C" int qd_set_error(int code, const char* msg) {
+  std::strncpy(g_err, msg ? msg : "", sizeof(g_err) - 1);
+  g_err[sizeof(g_err) - 1] = 0;
+  return code;
+}
+extern "C" const char* qd_last_error(void) { return g_err; }
+extern "C" int qd_version(void) { return 1; }
+extern "C" int qd_device_arch(char* buf, int len) {
+  int dev = 0;
+  hipDeviceProp_t p;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess)
+    return qd_set_error(QD_ERR_ARG, "no HIP device");
+  std::strncpy(buf, p.gcnArchName, len - 1);
+  buf[len - 1] = 0;
+  return 0;
+}
+
+static inline int qmax_of(int bits) { return (1 << (bits - 1)) - 1; }
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------------------
+// amax reductions
+// ---------------------------------------------------------------------------------------
+
+// NHWC per-(n, c) column max over rows.  block (64, 4): x = 8-channel chunk, y = row lane.
+// grid (ceil(c/8/64), n, row_splits).  requires c % 8 == 0.
+__global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, int hw, int c,
+                                                     int rows_per_split, float* __restrict__ amax) {
+  __shared__ float red[4][64][8];
+  const int chunk = blockIdx.x * 64 + threadIdx.x;
+  const int n = blockIdx.y;
+  const int r0 = blockIdx.z * rows_per_split;
+  const int r1 = min(hw, r0 + rows_per_split);
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = 0.f;
+  if (chunk * 8 < c) {
+    const f16* base = x + (size_t)n * hw * c + chunk * 8;
+    for (int r = r0 + threadIdx.y; r < r1; r += 4) {
+      f16x8 v = *reinterpret_cast<const f16x8*>(base + (size_t)r * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)v[j]));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.y][threadIdx.x][j] = m[j];
+  __syncthreads();
+  if (threadIdx.y == 0 && chunk * 8 < c) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = fmaxf(fmaxf(red[0][threadIdx.x][j], red[1][threadIdx.x][j]),
+                      fmaxf(red[2][threadIdx.x][j], red[3][threadIdx.x][j]));
+      atomic_max_pos(&amax[(size_t)n * c + chunk * 8 + j], v);
+    }
+  }
+}
+
+// contiguous-row max: one wave per row of length len (NCHW per-(n,c) rows, per-token rows).
+__global__ void __launch_bounds__(256) k_rowmax(const f16* __restrict__ x, long rows, int len,
+                                                float* __restrict__ amax) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const f16* p = x + row * len;
+  float m = 0.f;
+  if ((len & 7) == 0 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+    for (int i = lane * 8; i < len; i += 512) {
+      f16x8 v = *reinterpret_cast<const f16x8*>(p + i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)v[j]));
+    }
+  } else {
+    for (int i = lane; i < len; i += 64) m = fmaxf(m, fabsf((float)p[i]));
+  }
+  m = wave_max(m);
+  if (lane == 0) amax[row] = m;
+}
+
+// global max |x| (per-tensor); one atomic per block.
+__global__ void __launch_bounds__(256) k_tensormax(const f16* __restrict__ x, long count,
+                                                   float* __restrict__ amax) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < count; i += (long)gridDim.x * 256)
+    m = fmaxf(m, fabsf((float)x[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// per (n, c, g x g patch) max, NCHW.  one thread per patch.
+__global__ void k_patchmax(const f16* __restrict__ x, int nc, int h, int w, int g,
+                           float* __restrict__ amax) {
+  const int gh = h / g, gw = w / g;
+  const long pid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pid >= (long)nc * gh * gw) return;
+  const int pw = pid % gw;
+  const int ph = (pid / gw) % gh;
+  const long ch = pid / ((long)gw * gh);
+  const f16* base = x + ch * h * w + (long)ph * g * w + (long)pw * g;
+  float m = 0.f;
+  for (int i = 0; i < g; ++i)
+    for (int j = 0; j < g; ++j) m = fmaxf(m, fabsf((float)base[(long)i * w + j]));
+  amax[pid] = m;
+}
+
+// ---------------------------------------------------------------------------------------
+// apply passes
+// ---------------------------------------------------------------------------------------
+
+// NHWC per-channel apply: 8 channels per thread (c % 8 == 0).
+__global__ void __launch_bounds__(256) k_apply_nhwc(const f16* __restrict__ x, f16* __restrict__ y,
+                                                    long count8, int hw, int c, int c_valid, int qmax,
+                                                    const float* __restrict__ amax) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count8) return;
+  const long e = i * 8;
+  const int ch = (int)(e % c);
+  const long n = e / ((long)hw * c);
+  f16x8 v = *reinterpret_cast<const f16x8*>(x + e);
+  const float* a = amax + n * c + ch;
+  f16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = ch + j < c_valid ? fq_apply((float)v[j], fq_scale(a[j], qmax)) : v[j];
+  *reinterpret_cast<f16x8*>(y + e) = o;
+}
+
+// generic apply with a scale index computed per element:
+//   mode 0: idx = e / div            (NCHW per-channel: div = hw; per-token: div = cols)
+//   mode 1: idx = 0                  (per-tensor)
+//   mode 2: NCHW g x g patches       (per-group)
+__global__ void __launch_bounds__(256) k_apply_generic(const f16* __restrict__ x, f16* __restrict__ y,
+                                                       long count, int mode, long div, int h,
+                                                       int w, int g, int qmax,
+                                                       const float* __restrict__ amax) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= count) return;
+  long idx;
+  if (mode == 0) {
+    idx = e / div;
+  } else if (mode == 1) {
+    idx = 0;
+  } else {
+    const int ww = e % w;
+    const int hh = (e / w) % h;
+    const long ch = e / ((long)w * h);
+    idx = (ch * (h / g) + hh / g) * (w / g) + ww / g;
+  }
+  y[e] = fq_apply((float)x[e], fq_scale(amax[idx], qmax));
+}
+
+// per-token in one kernel: wave per row, amax then apply (row re-read hits L1/L2).
+__global__ void __launch_bounds__(256) k_per_token(const f16* __restrict__ x, f16* __restrict__ y,
+                                                   long rows, int cols, int qmax) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const f16* p = x + row * cols;
+  f16* q = y + row * cols;
+  float m = 0.f;
+  for (int i = lane; i < cols; i += 64) m = fmaxf(m, fabsf((float)p[i]));
+  m = wave_max(m);
+  const float s = fq_scale(m, qmax);
+  for (int i = lane; i < cols; i += 64) q[i] = fq_apply((float)p[i], s);
+}
+
+static int grid1(long count, int per_block = 256) { return (int)((count + per_block - 1) / per_block); }
+
+static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, int gran, int group,
+                         float* amax, hipStream_t st) {
+  const long hw = (long)h * w;
+  if (gran == QD_GRAN_PER_CHANNEL) {
+    (void)hipMemsetAsync(amax, 0, sizeof(float) * n * c, st);
+    if (layout == QD_LAYOUT_NHWC) {
+      QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
+      const int chunks = c / 8;
+      int rps = 64;
+      while (rps < hw && ((hw + rps - 1) / rps) * n * ((chunks + 63) / 64) > 2048) rps *= 2;
+      dim3 grid((chunks + 63) / 64, n, (int)((hw + rps - 1) / rps));
+      k_colmax_nhwc<<<grid, dim3(64, 4), 0, st>>>((const f16*)x, (int)hw, c, rps, amax);
+    } else {
+      const long rows = (long)n * c;
+      k_rowmax<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, rows, (int)hw, amax);
+    }
+  } else if (gran == QD_GRAN_PER_TOKEN) {
+    const long rows = (long)n * hw;  // rows of length c (caller passes h = w = 1 normally)
+    k_rowmax<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, rows, c, amax);
+  } else if (gran == QD_GRAN_PER_TENSOR) {
+    (void)hipMemsetAsync(amax, 0, sizeof(float), st);
+    const long count = (long)n * c * hw;
+    k_tensormax<<<(int)std::min<long>(2048, grid1(count)), 256, 0, st>>>((const f16*)x, count, amax);
+  } else if (gran == QD_GRAN_PER_GROUP) {
+    QD_REQUIRE(layout == QD_LAYOUT_NCHW, "per_group needs NCHW");
+    QD_REQUIRE(group > 0 && h % group == 0 && w % group == 0, "per_group: group must divide H and W");
+    const long patches = (long)n * c * (h / group) * (w / group);
+    k_patchmax<<<grid1(patches), 256, 0, st>>>((const f16*)x, n * c, h, w, group, amax);
+  } else {
+    return qd_set_error(QD_ERR_ARG, "unknown granularity");
+  }
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+static int launch_apply(const void* x, void* y, int layout, int n, int c, int h, int w, int gran,
+                        int group, int bits, const float* amax, hipStream_t st) {
+  QD_REQUIRE(bits >= 2 && bits <= 16, "n_bits must be in [2, 16]");
+  const int qm = qmax_of(bits);
+  const long hw = (long)h * w;
+  const long count = (long)n * c * hw;
+  if (count == 0) return 0;
+  if (gran == QD_GRAN_PER_CHANNEL && layout == QD_LAYOUT_NHWC) {
+    QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
+    const int c_valid = group > 0 ? std::min(group, c) : c;
+    k_apply_nhwc<<<grid1(count / 8), 256, 0, st>>>((const f16*)x, (f16*)y, count / 8, (int)hw, c, c_valid, qm, amax);
+  } else if (gran == QD_GRAN_PER_CHANNEL) {
+    k_apply_generic<<<grid1(count), 256, 0, st>>>((const f16*)x, (f16*)y, count, 0, hw, h, w, 1, qm, amax);
+  } else if (gran == QD_GRAN_PER_TOKEN) {
+    k_apply_generic<<<grid1(count), 256, 0, st>>>((const f16*)x, (f16*)y, count, 0, c, h, w, 1, qm, amax);
+  } else if (gran == QD_GRAN_PER_TENSOR) {
+    k_apply_generic<<<grid1(count), 256, 0, st>>>((const f16*)x, (f16*)y, count, 1, 1, h, w, 1, qm, amax);
+  } else if (gran == QD_GRAN_PER_GROUP) {
+    QD_REQUIRE(layout == QD_LAYOUT_NCHW, "per_group needs NCHW");
+    QD_REQUIRE(group > 0 && h % group == 0 && w % group == 0, "per_group: group must divide H and W");
+    k_apply_generic<<<grid1(count), 256, 0, st>>>((const f16*)x, (f16*)y, count, 2, 1, h, w, group, qm, amax);
+  } else {
+    return qd_set_error(QD_ERR_ARG, "unknown granularity");
+  }
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int qd_act_absmax(const void* x, int layout, int n, int c, int h, int w, int gran,
+                             int group, float* amax, void* stream) {
+  QD_REQUIRE(x && amax, "null pointer");
+  QD_REQUIRE(n >= 0 && c >= 0 && h >= 0 && w >= 0, "negative shape");
+  if ((long)n * c * h * w == 0) return 0;
+  return launch_absmax(x, layout, n, c, h, w, gran, group, amax, S(stream));
+}
+
+extern "C" int qd_act_apply(const void* x, void* y, int layout, int n, int c, int h, int w, int gran,
+                            int group, int n_bits, const float* amax, void* stream) {
+  QD_REQUIRE(x && y && amax, "null pointer");
+  return launch_apply(x, y, layout, n, c, h, w, gran, group, n_bits, amax, S(stream));
+}
+
+extern "C" int qd_act_fakequant(const void* x, void* y, int layout, int n, int c, int h, int w,
+                                int gran, int group, int n_bits, float* amax_ws, void* stream) {
+  QD_REQUIRE(x && y, "null pointer");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "n_bits must be in [2, 16]");
+  QD_REQUIRE(n >= 0 && c >= 0 && h >= 0 && w >= 0, "negative shape");
+  if ((long)n * c * h * w == 0) return 0;
+  hipStream_t st = S(stream);
+  if (gran == QD_GRAN_PER_TOKEN) {
+    const long rows = (long)n * h * w;
+    k_per_token<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, (f16*)y, rows, c, qmax_of(n_bits));
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
+  QD_REQUIRE(amax_ws, "amax workspace required");
+  int rc = launch_absmax(x, layout, n, c, h, w, gran, group, amax_ws, st);
+  if (rc) return rc;
+  return launch_apply(x, y, layout, n, c, h, w, gran, group, n_bits, amax_ws, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// weight quantization (offline)
+// ---------------------------------------------------------------------------------------
+
+// one wave per group of g consecutive elements
+__global__ void __launch_bounds__(256) k_weight_group(const f16* __restrict__ w, long groups, int g,
+                                                      int qmax, int8_t* __restrict__ codes,
+                                                      f16* __restrict__ scales, f16* __restrict__ wdq) {
+  const long gid = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (gid >= groups) return;
+  const f16* p = w + gid * g;
+  float m = 0.f;
+  for (int i = lane; i < g; i += 64) m = fmaxf(m, fabsf((float)p[i]));
+  m = wave_max(m);
+  const float s = fq_scale(m, qmax);
+  if (scales && lane == 0) scales[gid] = (f16)s;
+  for (int i = lane; i < g; i += 64) {
+    const f16 t = (f16)((float)p[i] / s);
+    const float q = __builtin_rintf((float)t);
+    if (codes) codes[gid * g + i] = (int8_t)q;
+    if (wdq) wdq[gid * g + i] = (f16)(q * s);
+  }
+}
+
+// per-tensor (single huge group): amax from a separate reduction
+__global__ void __launch_bounds__(256) k_weight_tensor_apply(const f16* __restrict__ w, long count,
+                                                             int qmax, const float* __restrict__ amax,
+                                                             int8_t* __restrict__ codes,
+                                                             f16* __restrict__ scales,
+                                                             f16* __restrict__ wdq) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const float s = fq_scale(amax[0], qmax);
+  if (e == 0 && scales) scales[0] = (f16)s;
+  if (e >= count) return;
+  const f16 t = (f16)((float)w[e] / s);
+  const float q = __builtin_rintf((float)t);
+  if (codes) codes[e] = (int8_t)q;
+  if (wdq) wdq[e] = (f16)(q * s);
+}
+
+extern "C" int qd_weight_quant(const void* w, int rows, int cols, int group, int n_bits,
+                               int8_t* codes, void* scales, void* w_dq, void* stream) {
+  QD_REQUIRE(w, "null weight");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 8, "weight n_bits must be in [2, 8] for int8 codes");
+  QD_REQUIRE(rows >= 0 && cols > 0 && group > 0, "bad shape");
+  const long count = (long)rows * cols;
+  if (count == 0) return 0;
+  hipStream_t st = S(stream);
+  if (group >= (1 << 16) || (long)group > cols) {
+    QD_REQUIRE((long)group == count, "a group longer than a row must be the whole tensor");
+    // per-tensor: reduce then apply.  amax workspace = first 4 bytes of a small buffer
+    float* ws = nullptr;
+    hipError_t e = hipMallocAsync((void**)&ws, sizeof(float), st);
+    if (e != hipSuccess) return qd_set_error((int)e, "workspace alloc");
+    (void)hipMemsetAsync(ws, 0, sizeof(float), st);
+    k_tensormax<<<(int)std::min<long>(2048, grid1(count)), 256, 0, st>>>((const f16*)w, count, ws);
+    k_weight_tensor_apply<<<grid1(count), 256, 0, st>>>((const f16*)w, count, qmax_of(n_bits), ws,
+                                                        codes, (f16*)scales, (f16*)w_dq);
+    (void)hipFreeAsync(ws, st);
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
+  QD_REQUIRE(cols % group == 0, "group must divide cols (apply the shrink rule on the host)");
+  const long groups = count / group;
+  k_weight_group<<<grid1(groups, 4), 256, 0, st>>>((const f16*)w, groups, group, qmax_of(n_bits),
+                                                   codes, (f16*)scales, (f16*)w_dq);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void k_pack_int4(const int8_t* __restrict__ codes, long pairs, uint8_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= pairs) return;
+  const uint8_t lo = (uint8_t)codes[2 * i] & 0xF;
+  const uint8_t hi = (uint8_t)codes[2 * i + 1] & 0xF;
+  out[i] = lo | (hi << 4);
+}
+
+extern "C" int qd_pack_int4(const int8_t* codes, int rows, int cols, uint8_t* packed, void* stream) {
+  QD_REQUIRE(codes && packed, "null pointer");
+  QD_REQUIRE(cols % 2 == 0, "int4 packing needs even cols");
+  const long pairs = (long)rows * cols / 2;
+  if (pairs == 0) return 0;
+  k_pack_int4<<<grid1(pairs), 256, 0, S(stream)>>>(codes, pairs, packed);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void k_conv_w_khwc(const f16* __restrict__ w, int co, int ci, int kh, int kw, int cip,
+                              f16* __restrict__ out) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)co * kh * kw * cip;
+  if (e >= total) return;
+  const int c = e % cip;
+  const int x = (e / cip) % kw;
+  const int y = (e / ((long)cip * kw)) % kh;
+  const long o = e / ((long)cip * kw * kh);
+  out[e] = c < ci ? w[((o * ci + c) * kh + y) * kw + x] : (f16)0.f;
+}
+
+extern "C" int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pad,
+                                   void* out, void* stream) {
+  QD_REQUIRE(w && out, "null pointer");
+  QD_REQUIRE(ci_pad >= ci, "ci_pad < ci");
+  const long total = (long)co * kh * kw * ci_pad;
+  if (total == 0) return 0;
+  k_conv_w_khwc<<<grid1(total), 256, 0, S(stream)>>>((const f16*)w, co, ci, kh, kw, ci_pad, (f16*)out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// conv-output finalize: out = half(fq(y) + residual | + chan_add[n][c])
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, const float* __restrict__ amax,
+                                                  long count8, int hw, int c, int qmax,
+                                                  const f16* __restrict__ res,
+                                                  const f16* __restrict__ cadd, f16* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count8) return;
+  const long e = i * 8;
+  const int ch = (int)(e % c);
+  const long n = e / ((long)hw * c);
+  f16x8 v = *reinterpret_cast<const f16x8*>(y + e);
+  f16x8 o;
+  if (qmax > 0) {
+    const float* a = amax + n * c + ch;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fq_apply((float)v[j], fq_scale(a[j], qmax));
+  } else {
+    o = v;
+  }
+  if (res) {
+    f16x8 r = *reinterpret_cast<const f16x8*>(res + e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)r[j]);
+  } else if (cadd) {
+    f16x8 r = *reinterpret_cast<const f16x8*>(cadd + n * c + ch);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)r[j]);
+  }
+  *reinterpret_cast<f16x8*>(out + e) = o;
+}
+
+extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
+                              const void* residual, const void* chan_add, void* out, void* stream) {
+  QD_REQUIRE(y && out, "null pointer");
+  QD_REQUIRE(c % 8 == 0, "finalize needs C % 8 == 0");
+  QD_REQUIRE(n_bits == 0 || (amax && n_bits >= 2 && n_bits <= 16), "bad n_bits / amax");
+  const long count8 = (long)n * hw * c / 8;
+  if (count8 == 0) return 0;
+  k_finalize<<<grid1(count8), 256, 0, S(stream)>>>((const f16*)y, amax, count8, hw, c,
+                                                   n_bits ? qmax_of(n_bits) : 0, (const f16*)residual,
+                                                   (const f16*)chan_add, (f16*)out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// SmoothQuant calibration + fold
+// ---------------------------------------------------------------------------------------
+__global__ void k_accum_sum(const float* __restrict__ amax, int c, float* __restrict__ sum,
+                            f16* __restrict__ amax_out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= c) return;
+  if (sum) sum[i] += amax[i];
+  if (amax_out) amax_out[i] = (f16)amax[i];
+}
+
+extern "C" int qd_channel_absmax_accum(const void* x, int64_t rows, int c, float* amax_ws, float* sum,
+                                       void* amax_out, void* stream) {
+  QD_REQUIRE(x && amax_ws, "null pointer");
+  QD_REQUIRE(c % 8 == 0, "channel absmax needs C % 8 == 0");
+  QD_REQUIRE(rows > 0 && rows < (1L << 31), "bad rows");
+  hipStream_t st = S(stream);
+  int rc = launch_absmax(x, QD_LAYOUT_NHWC, 1, c, (int)rows, 1, QD_GRAN_PER_CHANNEL, 0, amax_ws, st);
+  if (rc) return rc;
+  k_accum_sum<<<grid1(c), 256, 0, st>>>(amax_ws, c, sum, (f16*)amax_out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// column |W| max of a [rows][c] fp16 matrix into wmax (atomic), c % 8 == 0 not required.
+__global__ void k_colabsmax(const f16* __restrict__ w, int rows, int c, float* __restrict__ wmax) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= c) return;
+  const int r0 = blockIdx.y * 64, r1 = min(rows, r0 + 64);
+  float m = 0.f;
+  for (int r = r0; r < r1; ++r) m = fmaxf(m, fabsf((float)w[(long)r * c + col]));
+  atomic_max_pos(&wmax[col], m);
+}
+
+__global__ void k_smooth_scales(const float* __restrict__ wmax, const f16* __restrict__ act, int c,
+                                float ea, float eb, f16* __restrict__ scales, f16* __restrict__ lnw,
+                                f16* __restrict__ lnb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= c) return;
+  const float cl = clamp_min_f16();
+  const float ws = fmaxf(wmax[i], cl);  // exact fp16 value
+  const f16 num = (f16)powf((float)act[i], ea);
+  const f16 den = (f16)powf(ws, eb);
+  const float s = fmaxf((float)(f16)((float)num / (float)den), cl);
+  scales[i] = (f16)s;
+  lnw[i] = (f16)((float)lnw[i] / s);
+  if (lnb) lnb[i] = (f16)((float)lnb[i] / s);
+}
+
+__global__ void k_scale_cols(f16* __restrict__ w, long count, int c, const f16* __restrict__ s) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= count) return;
+  w[e] = (f16)((float)w[e] * (float)s[e % c]);
+}
+
+extern "C" int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const int* fc_rows, int nfc,
+                              int c, const void* act_mean, float alpha, float* wmax_ws,
+                              void* scales_out, void* stream) {
+  QD_REQUIRE(ln_w && fc_w && fc_rows && act_mean && wmax_ws && scales_out, "null pointer");
+  QD_REQUIRE(nfc > 0 && c > 0, "bad shape");
+  hipStream_t st = S(stream);
+  (void)hipMemsetAsync(wmax_ws, 0, sizeof(float) * c, st);
+  for (int i = 0; i < nfc; ++i) {
+    QD_REQUIRE(fc_w[i] && fc_rows[i] > 0, "bad fc");
+    dim3 grid((c + 255) / 256, (fc_rows[i] + 63) / 64);
+    k_colabsmax<<<grid, 256, 0, st>>>((const f16*)fc_w[i], fc_rows[i], c, wmax_ws);
+  }
+  // exponents are rounded to fp16 first, as torch's Half pow(Scalar) does (oracle note)
+  const float ea = (float)(f16)alpha;
+  const float eb = (float)(f16)(1.0f - alpha);
+  k_smooth_scales<<<grid1(c), 256, 0, st>>>(wmax_ws, (const f16*)act_mean, c, ea, eb, (f16*)scales_out,
+                                            (f16*)ln_w, (f16*)ln_b);
+  for (int i = 0; i < nfc; ++i) {
+    const long count = (long)fc_rows[i] * c;
+    k_scale_cols<<<grid1(count), 256, 0, st>>>((f16*)fc_w[i], count, c, (const f16*)scales_out);
+  }
+  QD_CHECK_LAUNCH();
+  return 0;
+}

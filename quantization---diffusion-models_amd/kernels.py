@@ -1,0 +1,318 @@
+"""Torch-facing wrappers over the libqdiff C ABI.
+
+PyTorch is plumbing here: it owns device memory (caching allocator) and the current HIP stream;
+every computation is a libqdiff kernel.  Each wrapper validates device / dtype / contiguity on
+the host and raises ``ValueError`` before anything is launched, mirroring the reference's
+argument errors; kernel failures surface as ``RuntimeError`` from ``_lib.call``.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+GRAN = {"per_token": 0, "per_channel": 1, "per_tensor": 2, "per_group": 3}
+NCHW, NHWC = 0, 1
+WFMT = {"f16": 0, "i8": 1, "i4": 2}
+EPI_BIAS, EPI_RESIDUAL, EPI_AMAX = 1, 2, 4
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _chk(t, name, dtype=torch.float16):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP (cuda) tensor, got {t.device}")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def device_arch():
+    buf = ctypes.create_string_buffer(64)
+    _lib.call("qd_device_arch", buf, 64)
+    return buf.value.decode()
+
+
+# ---------------------------------------------------------------- activation fake-quant
+def act_fakequant(x, gran, n_bits, layout=NCHW, group=0, out=None):
+    """quantize_activation_<gran>_absmax (fake_quant.py:108-167) on device.
+
+    per_token: any shape, rows = numel / shape[-1].  per_channel / per_group: 4-D in `layout`.
+    per_tensor: any shape.
+    """
+    _chk(x, "x")
+    y = out if out is not None else torch.empty_like(x)
+    g = GRAN[gran]
+    if gran == "per_token":
+        c = x.shape[-1]
+        n, h, w = x.numel() // max(c, 1), 1, 1
+        ws = None
+    elif gran == "per_tensor":
+        n, c, h, w = 1, x.numel(), 1, 1
+        ws = torch.empty(1, dtype=torch.float32, device=x.device)
+    else:
+        if x.dim() != 4:
+            raise ValueError(f"{gran} activation quant needs a 4-D tensor")
+        if layout == NCHW:
+            n, c, h, w = x.shape
+        else:
+            n, h, w, c = x.shape
+        if gran == "per_channel":
+            ws = torch.empty(n * c, dtype=torch.float32, device=x.device)
+        else:
+            ws = torch.empty(n * c * (h // group) * (w // group), dtype=torch.float32, device=x.device)
+    _lib.call("qd_act_fakequant", _p(x), _p(y), layout, n, c, h, w, g, group, n_bits, _p(ws), _stream())
+    return y
+
+
+def act_absmax(x, gran, layout=NHWC, group=0):
+    _chk(x, "x")
+    if gran == "per_channel":
+        if layout == NCHW:
+            n, c, h, w = x.shape
+        else:
+            n, h, w, c = x.shape
+        out = torch.empty(n * c, dtype=torch.float32, device=x.device)
+    else:
+        raise ValueError("act_absmax wrapper supports per_channel only")
+    _lib.call("qd_act_absmax", _p(x), layout, n, c, h, w, GRAN[gran], group, _p(out), _stream())
+    return out
+
+
+def act_apply_nhwc(x, amax, n_bits, out=None, c_valid=0):
+    """Second pass of per-channel quant on NHWC [N, H, W, C] with precomputed amax[N*C].
+    c_valid > 0: channels >= c_valid are zero padding and are copied unchanged."""
+    _chk(x, "x")
+    n, h, w, c = x.shape
+    y = out if out is not None else torch.empty_like(x)
+    _lib.call("qd_act_apply", _p(x), _p(y), NHWC, n, c, h, w, GRAN["per_channel"], c_valid, n_bits, _p(amax),
+              _stream())
+    return y
+
+
+# ---------------------------------------------------------------- weight quant
+def weight_quant(w2d, group, n_bits, want_codes=True, want_scales=True, want_dq=True):
+    """Row-group absmax RTN of a [rows, cols] fp16 weight (fake_quant.py:21-105)."""
+    _chk(w2d, "weight")
+    rows, cols = w2d.shape
+    codes = torch.empty(rows, cols, dtype=torch.int8, device=w2d.device) if want_codes else None
+    ngr = 1 if group > cols else cols // group
+    scales = torch.empty(rows, ngr, dtype=torch.float16, device=w2d.device) if want_scales else None
+    wdq = torch.empty_like(w2d) if want_dq else None
+    _lib.call("qd_weight_quant", _p(w2d), rows, cols, group, n_bits, _p(codes), _p(scales), _p(wdq),
+              _stream())
+    return codes, scales, wdq
+
+
+def pack_int4(codes):
+    _chk(codes, "codes", torch.int8)
+    rows, cols = codes.shape
+    out = torch.empty(rows, cols // 2, dtype=torch.uint8, device=codes.device)
+    _lib.call("qd_pack_int4", _p(codes), rows, cols, _p(out), _stream())
+    return out
+
+
+def conv_weight_khwc(w, ci_pad):
+    _chk(w, "conv weight")
+    co, ci, kh, kw = w.shape
+    out = torch.empty(co, kh, kw, ci_pad, dtype=torch.float16, device=w.device)
+    _lib.call("qd_conv_weight_khwc", _p(w), co, ci, kh, kw, ci_pad, _p(out), _stream())
+    return out
+
+
+# ---------------------------------------------------------------- GEMMs
+def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
+           amax=None, rows_per_sample=0):
+    """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K)."""
+    if x2d.dtype != torch.float16 or not x2d.is_cuda:
+        raise ValueError("x must be an fp16 HIP tensor")
+    if x2d.dim() != 2 or x2d.stride(1) != 1:
+        raise ValueError("x must be 2-D with unit column stride")
+    M, K = x2d.shape
+    N = weight.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float16, device=x2d.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
+          (EPI_AMAX if amax is not None else 0)
+    if residual is not None:
+        _chk(residual, "residual")
+    _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(weight), WFMT[wfmt], _p(scales), group,
+              _p(bias), _p(residual), _p(out), N, out.stride(0), epi, _p(amax), rows_per_sample, _stream())
+    return out
+
+
+def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, residual=None, out=None,
+                amax=None):
+    """NHWC implicit-GEMM conv; x [N, H, W, Cip], w_khwc [Co, kh, kw, Cip]."""
+    _chk(x, "x")
+    _chk(w_khwc, "weight")
+    n, h, w, cip = x.shape
+    co, kh, kw, cip_w = w_khwc.shape
+    if cip_w != cip:
+        raise ValueError(f"channel padding mismatch: x has {cip}, weight {cip_w}")
+    H, W = (2 * h, 2 * w) if upsample2x else (h, w)
+    ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = torch.empty(n, ho, wo, co, dtype=torch.float16, device=x.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
+          (EPI_AMAX if amax is not None else 0)
+    _lib.call("qd_conv2d_fwd", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad,
+              1 if upsample2x else 0, _p(bias), _p(residual), _p(out), epi, _p(amax), _stream())
+    return out
+
+
+def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
+    """out = half(fq(y) + residual | + chan_add[n, c]); y NHWC [N, H, W, C] (or [N, HW, C])."""
+    _chk(y, "y")
+    n, c = y.shape[0], y.shape[-1]
+    hw = y.numel() // (n * c)
+    o = out if out is not None else torch.empty_like(y)
+    _lib.call("qd_fq_finalize", _p(y), _p(amax), n, hw, c, n_bits, _p(residual), _p(chan_add), _p(o),
+              _stream())
+    return o
+
+
+# ---------------------------------------------------------------- norms / elementwise
+def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, out=None):
+    _chk(x, "x")
+    n = x.shape[0]
+    c1 = x.shape[-1]
+    c = c1 + (x2.shape[-1] if x2 is not None else 0)
+    hw = x.numel() // (n * c1)
+    if out is None:
+        out = torch.empty(*x.shape[:-1], c, dtype=torch.float16, device=x.device)
+    _lib.call("qd_groupnorm", _p(x), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma), _p(beta),
+              1 if silu else 0, q_bits, _p(out), _stream())
+    return out
+
+
+def layernorm(x, eps, gamma, beta, out=None):
+    _chk(x, "x")
+    c = x.shape[-1]
+    rows = x.numel() // c
+    o = out if out is not None else torch.empty_like(x)
+    _lib.call("qd_layernorm", _p(x), rows, c, float(eps), _p(gamma), _p(beta), _p(o), _stream())
+    return o
+
+
+def geglu(h, out=None):
+    _chk(h, "h")
+    inner = h.shape[-1] // 2
+    m = h.numel() // h.shape[-1]
+    o = out if out is not None else torch.empty(*h.shape[:-1], inner, dtype=torch.float16, device=h.device)
+    _lib.call("qd_geglu", _p(h), m, inner, _p(o), _stream())
+    return o
+
+
+def silu(x, out=None):
+    _chk(x, "x")
+    o = out if out is not None else torch.empty_like(x)
+    _lib.call("qd_silu", _p(x), _p(o), x.numel(), _stream())
+    return o
+
+
+def add(a, b, out=None):
+    _chk(a, "a")
+    _chk(b, "b")
+    o = out if out is not None else torch.empty_like(a)
+    _lib.call("qd_add", _p(a), _p(b), _p(o), a.numel(), _stream())
+    return o
+
+
+def concat_c(a, b, out=None):
+    _chk(a, "a")
+    _chk(b, "b")
+    c1, c2 = a.shape[-1], b.shape[-1]
+    m = a.numel() // c1
+    o = out if out is not None else torch.empty(*a.shape[:-1], c1 + c2, dtype=torch.float16, device=a.device)
+    _lib.call("qd_concat_c", _p(a), c1, _p(b), c2, m, _p(o), _stream())
+    return o
+
+
+def nchw_to_nhwc(x, c_pad=None, out=None):
+    _chk(x, "x")
+    n, c, h, w = x.shape
+    cp = c_pad or c
+    if out is not None:
+        _chk(out, "out")
+        if tuple(out.shape) != (n, h, w, cp):
+            raise ValueError(f"out must be {(n, h, w, cp)}")
+    y = out if out is not None else torch.empty(n, h, w, cp, dtype=torch.float16, device=x.device)
+    _lib.call("qd_nchw_to_nhwc", _p(x), n, c, h * w, cp, _p(y), _stream())
+    return y
+
+
+def nhwc_to_nchw(x, c=None):
+    _chk(x, "x")
+    n, h, w, cp = x.shape
+    c = c or cp
+    y = torch.empty(n, c, h, w, dtype=torch.float16, device=x.device)
+    _lib.call("qd_nhwc_to_nchw", _p(x), n, c, h * w, cp, _p(y), _stream())
+    return y
+
+
+def attention(q, k, v, heads, out=None, b=None):
+    """q [B, Sq, C], k/v [B, Skv, C] (row strides may exceed C); returns o [B, Sq, C]."""
+    B, sq, c = q.shape
+    skv = k.shape[1]
+    d = c // heads
+    if out is None:
+        out = torch.empty(B, sq, c, dtype=torch.float16, device=q.device)
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        if t.dtype != torch.float16 or not t.is_cuda or t.stride(2) != 1:
+            raise ValueError(f"{nm} must be fp16 HIP with unit last stride")
+    _lib.call("qd_attention", _p(q), q.stride(1), _p(k), k.stride(1), _p(v), v.stride(1), _p(out), out.stride(1),
+              B, heads, sq, skv, d, float(d ** -0.5), _stream())
+    return out
+
+
+def timestep_embedding(timesteps_f32, step_idx, b, dim, flip_sin_to_cos=True, shift=0.0, out=None):
+    o = out if out is not None else torch.empty(b, dim, dtype=torch.float16, device=timesteps_f32.device)
+    _lib.call("qd_timestep_embedding", _p(timesteps_f32), _p(step_idx), b, dim, 1 if flip_sin_to_cos else 0,
+              float(shift), _p(o), _stream())
+    return o
+
+
+def cfg_ddim_step(latents, unet_out, guidance, alpha_t, alpha_prev, step_idx, next_in=None, c=None):
+    """latents [B, H, W, Cp] NHWC (updated in place); unet_out [2B, H, W, Cp]."""
+    _chk(latents, "latents")
+    _chk(unet_out, "unet_out")
+    b = latents.shape[0]
+    cp = latents.shape[-1]
+    l = latents.numel() // b
+    _lib.call("qd_cfg_ddim_step", _p(latents), _p(unet_out), b, l, float(guidance), _p(alpha_t), _p(alpha_prev),
+              _p(step_idx), _p(next_in), c or cp, cp, _stream())
+    return latents
+
+
+def channel_absmax_accum(x2d, ws, sum_buf=None, amax_out=None):
+    _chk(x2d, "x")
+    rows, c = x2d.shape
+    _lib.call("qd_channel_absmax_accum", _p(x2d), rows, c, _p(ws), _p(sum_buf), _p(amax_out), _stream())
+
+
+def smooth_fold(ln_weight, ln_bias, fc_weights, act_mean, alpha=0.8):
+    """quantizer_SQ.smooth_ln_fcs on device (in place); returns the fp16 scales."""
+    c = ln_weight.numel()
+    for w in fc_weights:
+        _chk(w, "fc weight")
+        if w.shape[1] != c:
+            raise AssertionError("ln.weight.numel() == fc.in_features == act_scales.numel()")
+    if act_mean.numel() != c:
+        raise AssertionError("ln.weight.numel() == fc.in_features == act_scales.numel()")
+    ptrs_arr = (ctypes.c_void_p * len(fc_weights))(*[w.data_ptr() for w in fc_weights])
+    rows_arr = (ctypes.c_int * len(fc_weights))(*[w.shape[0] for w in fc_weights])
+    ptrs = ctypes.cast(ptrs_arr, ctypes.c_void_p)
+    rows = ctypes.cast(rows_arr, ctypes.c_void_p)
+    ws = torch.empty(c, dtype=torch.float32, device=ln_weight.device)
+    scales = torch.empty(c, dtype=torch.float16, device=ln_weight.device)
+    _lib.call("qd_smooth_fold", _p(ln_weight), _p(ln_bias), ptrs, rows, len(fc_weights), c,
+              _p(act_mean.to(torch.float16).contiguous()), float(alpha), _p(ws), _p(scales), _stream())
+    return scales

@@ -1,0 +1,187 @@
+"""Diffusion adapters: StableDiffusion1_x, StableDiffusionXL, StableDiffusion3_5 and the AWQ
+facade (models/StableDiffusion1_x.py, StableDiffusionXL.py, StableDiffusion3_5.py; README's
+``AWQ.from_pretrained`` dispatching on model_index.json ``_class_name``).
+
+Component discovery, layer lists and the SmoothQuant groups follow the reference adapters:
+  set_quantizable_components   StableDiffusion1_x.py:19-33
+  get_model_layers_unet        :39-47  (top-level (name, child) of each unet)
+  get_model_layers_te / _vae   :49-67  (vae: decoder children only)
+  get_smoothing_blocks         :96-102 (every BasicTransformerBlock)
+  mean_of_dict                 :104-112
+  get_layers_for_scaling_unet  :115-150 (norm1 -> attn1.to_q/k/v, norm3 -> ff.net.0.proj;
+                                         activation = mean of attn1.to_q's / ff.net.0.proj's hook)
+"""
+import torch
+
+from .base import QUANTISABLE_COMPONENTS, BaseAWQForDiffusion
+from .calib import synthetic_calibration_set
+from .pipeline import synthetic_text_embeddings
+from .pipeline_io import load_config
+from .unet import BasicTransformerBlock
+
+
+class _DiffusionAdapter(BaseAWQForDiffusion):
+    has_unet = True
+    has_transformer = False
+
+    def __init__(self, pipeline, model_type, is_quantized, config, quant_config, refiner_path=None,
+                 access_token=None):
+        super().__init__(pipeline, model_type, is_quantized, config, quant_config)
+        self.quantizable_components = {"unet": [], "text_encoder": [], "vae": [], "transformer": []}
+        self.quantized_components = []
+        self.refiner_pipeline = None
+        self.set_quantizable_components()
+
+    def set_quantizable_components(self):
+        for component, obj in self.pipeline.components.items():
+            if obj is None or not isinstance(obj, torch.nn.Module):
+                continue
+            for key in QUANTISABLE_COMPONENTS:
+                if key in component:
+                    self.quantizable_components[key].append(component)
+                    break
+
+    def _layers(self, key, sub=None):
+        out = []
+        for comp in self.quantizable_components[key]:
+            mod = getattr(self.pipeline, comp)
+            if sub is not None:
+                mod = getattr(mod, sub)
+            out.append([(n, m) for n, m in mod.named_children()])
+        return out
+
+    def get_model_layers_unet(self):
+        if not self.has_unet:
+            raise Exception("NO UNET IN THIS MODEL")
+        return self._layers("unet")
+
+    def get_model_layers_te(self):
+        return self._layers("text_encoder")
+
+    def get_model_layers_vae(self):
+        return self._layers("vae", "decoder")
+
+    def get_model_layers_transformers(self):
+        if not self.has_transformer:
+            raise Exception(f"There is no transformer in this model, {type(self).__name__}")
+        return self._layers("transformer")
+
+    def get_root(self, component, idx):
+        return getattr(self.pipeline, self.quantizable_components[component][idx])
+
+    def get_components(self):
+        return self.quantizable_components
+
+    def get_unet(self):
+        return self.pipeline.unet
+
+    def get_pipeline(self):
+        return self.pipeline
+
+    def set_quantized_components(self, component):
+        self.quantized_components.append(component)
+
+    def get_debugModuleNames(self, *a, **k):
+        return []
+
+    def get_scalingStates(self, *a, **k):
+        return []
+
+    def get_projectionNames(self, *a, **k):
+        return []
+
+    # ---------------------------------------------------------------- SmoothQuant hooks
+    def get_smoothing_blocks(self):
+        return {name: m for name, m in self.pipeline.unet.named_modules() if isinstance(m, BasicTransformerBlock)}
+
+    @staticmethod
+    def mean_of_dict(hook):
+        return hook.mean()
+
+    def get_layers_for_scaling_unet(self, module, hooks):
+        return [
+            dict(prev_op=module.norm1, layers=[module.attn1.to_q, module.attn1.to_k, module.attn1.to_v],
+                 activations_max=[self.mean_of_dict(hooks["attn1.to_q"]), self.mean_of_dict(hooks["attn1.to_k"]),
+                                  self.mean_of_dict(hooks["attn1.to_v"])]),
+            dict(prev_op=module.norm3, layers=[module.ff.net[0].proj],
+                 activations_max=[self.mean_of_dict(hooks["ff.net.0.proj"])]),
+        ]
+
+    @torch.no_grad()
+    def run_sq_calibration(self, n_samples=96, batch_size=8, seed=42, num_inference_steps=50, guidance_scale=7.5,
+                           height=None, width=None):
+        """run_calibration (calib_data.py:227-245) on device, eager (hooks fire per call)."""
+        cfg = self.pipeline.unet.config
+        hh = height or cfg.sample_size * 8
+        ww = width or cfg.sample_size * 8
+        samples = synthetic_calibration_set(n_samples, batch_size, seed, (cfg.in_channels, hh // 8, ww // 8))
+        for prompts, lat in samples:
+            self.generate(prompt=prompts, height=hh, width=ww, num_inference_steps=num_inference_steps,
+                          guidance_scale=guidance_scale, lat=lat, output_type="latent", use_graph=False)
+        self._loops = {}
+
+
+class StableDiffusion1_x(_DiffusionAdapter):
+    def __init__(self, pipeline, model_type, is_quantized, config, quant_config, access_token=None,
+                 refiner_path=None):
+        if refiner_path is not None:
+            raise Exception("StableDiffusion1.5 has no refiner model, if there is its not supported")
+        super().__init__(pipeline, model_type, is_quantized, config, quant_config)
+
+    def checkQuantStatus(self, quantUnet=True, quantTextEncoder=False, quantVAE=False, quantTransformer=True):
+        if quantTransformer:
+            raise Exception("There is no Transformer in this Diffusion Model")
+
+
+class StableDiffusionXL(_DiffusionAdapter):
+    def checkQuantStatus(self, quantUnet=True, quantTextEncoder=False, quantVAE=False, quantTransformer=True):
+        if quantTransformer:
+            raise Exception("There is no Transformer in this Diffusion Model")
+
+    def get_quantized_components(self):
+        return self.quantizable_components
+
+
+class StableDiffusion3_5(_DiffusionAdapter):
+    """SD3.5 MMDiT adapter surface (StableDiffusion3_5.py).  The MMDiT transformer itself is not
+    built in this round (DESIGN.md 'next')."""
+    has_unet = False
+    has_transformer = True
+
+    def __init__(self, pipeline, model_type, is_quantized, config, quant_config, refiner_path=None,
+                 access_token=None):
+        if refiner_path is not None:
+            raise Exception("StableDiffusion3.5 has no refiner model, if there is its not supported")
+        super().__init__(pipeline, model_type, is_quantized, config, quant_config)
+
+    def checkQuantStatus(self, quantUnet=True, quantTextEncoder=False, quantVAE=False, quantTransformer=True):
+        if quantUnet:
+            raise Exception("There is no UNET in StableDiffusion3_5")
+
+    def get_transformer(self):
+        return self.pipeline.transformer
+
+
+CLASS_MAP = {
+    "StableDiffusionPipeline": StableDiffusion1_x,
+    "StableDiffusionXLPipeline": StableDiffusionXL,
+    "StableDiffusion3Pipeline": StableDiffusion3_5,
+}
+
+
+class AWQ:
+    """Facade of the README (``AWQ.from_pretrained(model_id)``): dispatch on _class_name."""
+
+    @staticmethod
+    def from_pretrained(model_path, model_type=None, **kwargs):
+        cls_name = load_config(model_path)["_class_name"]
+        if cls_name not in CLASS_MAP:
+            raise NotImplementedError(f"{cls_name} is not supported")
+        if cls_name == "StableDiffusion3Pipeline":
+            raise NotImplementedError("the SD3.5 MMDiT transformer is not part of this build yet (DESIGN.md)")
+        return CLASS_MAP[cls_name].from_pretrained(model_path, model_type, **kwargs)
+
+    @staticmethod
+    def from_quantized(model_path, model_type=None, **kwargs):
+        cls_name = load_config(model_path)["_class_name"]
+        return CLASS_MAP[cls_name].from_quantized(model_path, model_type, **kwargs)

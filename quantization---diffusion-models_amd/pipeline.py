@@ -1,0 +1,130 @@
+"""The denoising loop on device: CFG batch, UNet, DDIM step - one HIP graph per step.
+
+Replaces the hot loop of diffusers ``StableDiffusionPipeline.__call__`` that the reference
+enters through ``BaseAWQForDiffusion.generate`` (models/base.py:828-850): for t in timesteps:
+UNet(cat([latents]*2), t, text_emb) -> CFG combine -> scheduler.step.
+
+Device-resident state: latents (NHWC, channels padded 4 -> 8), the duplicated UNet input, the
+per-step scheduler constants and a device step counter that the fused CFG+DDIM kernel
+increments, so one captured graph is replayed ``num_inference_steps`` times with no host work
+between steps.
+"""
+import zlib
+
+import torch
+
+from . import kernels as K
+from .scheduler import DDIMConfig, ddim_tables
+
+C_PAD = 8
+
+
+def synthetic_text_embeddings(prompts, seq_len=77, dim=768, device="cuda"):
+    """Deterministic stand-in for the CLIP text encoder (out of scope): each prompt
+    string seeds a CPU generator (crc32) that draws N(0,1) [seq_len, dim] fp16 features."""
+    if isinstance(prompts, str):
+        prompts = [prompts]
+    embs = []
+    for p in prompts:
+        g = torch.Generator("cpu").manual_seed(zlib.crc32(p.encode()) & 0x7FFFFFFF)
+        embs.append(torch.randn(seq_len, dim, generator=g))
+    return torch.stack(embs).to(torch.float16).to(device)
+
+
+class DenoiseLoop:
+    """Static-shape denoising loop for a fixed (batch, resolution, steps)."""
+
+    def __init__(self, unet, batch, height=512, width=512, num_inference_steps=50, guidance_scale=7.5,
+                 device="cuda", use_graph=True, sched_cfg=DDIMConfig(), ctx_len=77):
+        self.unet = unet
+        self.B = batch
+        self.h, self.w = height // 8, width // 8
+        self.steps = num_inference_steps
+        self.guidance = float(guidance_scale)
+        self.device = torch.device(device)
+        self.use_graph = use_graph
+        cfg = unet.config
+        self.c0 = cfg.block_out_channels[0]
+        self.cin = cfg.in_channels
+        ts, a_t, a_p = ddim_tables(num_inference_steps, sched_cfg)
+        self.timesteps = ts
+        self.ts_f32 = ts.to(torch.float32).to(self.device)
+        self.a_t = a_t.to(self.device)
+        self.a_p = a_p.to(self.device)
+        f16 = dict(dtype=torch.float16, device=self.device)
+        self.lat = torch.zeros(batch, self.h, self.w, C_PAD, **f16)
+        self.next_in = torch.zeros(2 * batch, self.h, self.w, C_PAD, **f16)
+        self.temb_in = torch.zeros(2 * batch, self.c0, **f16)
+        self.step_idx = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.ctx = torch.zeros(2 * batch, ctx_len, cfg.cross_attention_dim, **f16)
+        self.ctx_kv = None
+        self.graph = None
+        self.last_out = None
+
+    # ---------------------------------------------------------------- inputs
+    @torch.no_grad()
+    def set_inputs(self, latents, ctx):
+        """latents [B, 4, h, w] fp16 (NCHW, like diffusers); ctx [2B, S, D] fp16 (uncond first)."""
+        if latents.shape != (self.B, self.cin, self.h, self.w):
+            raise ValueError(f"latents must be {(self.B, self.cin, self.h, self.w)}, got {tuple(latents.shape)}")
+        if ctx.shape != self.ctx.shape:
+            raise ValueError(f"context must be {tuple(self.ctx.shape)}, got {tuple(ctx.shape)}")
+        lat = latents.to(device=self.device, dtype=torch.float16).contiguous()
+        K.nchw_to_nhwc(lat, C_PAD, out=self.lat)
+        K.nchw_to_nhwc(lat, C_PAD, out=self.next_in[: self.B])
+        K.nchw_to_nhwc(lat, C_PAD, out=self.next_in[self.B:])
+        self.ctx.copy_(ctx)
+        self.step_idx.zero_()
+        if self.ctx_kv is None:
+            self.ctx_kv = self.unet.prepare_context(self.ctx)
+        else:
+            fresh = self.unet.prepare_context(self.ctx)
+            for key, (k, v) in fresh.items():
+                self.ctx_kv[key][0].copy_(k)
+                self.ctx_kv[key][1].copy_(v)
+
+    # ---------------------------------------------------------------- one step
+    @torch.no_grad()
+    def step(self):
+        K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
+                             shift=float(self.unet.config.freq_shift), out=self.temb_in)
+        out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
+        K.cfg_ddim_step(self.lat, out, self.guidance, self.a_t, self.a_p, self.step_idx, self.next_in,
+                        c=self.cin)
+        self.last_out = out
+        return out
+
+    @torch.no_grad()
+    def capture(self):
+        """Warm up eagerly (allocations, weight caches), then capture one step into a graph."""
+        if self.ctx_kv is None:
+            raise RuntimeError("set_inputs() before capture()")
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step()
+        self.graph = g
+
+    @torch.no_grad()
+    def run(self, latents=None, ctx=None):
+        """Run all steps; returns the final latents [B, 4, h, w] fp16 (NCHW)."""
+        if latents is not None:
+            self.set_inputs(latents, ctx)
+        if self.use_graph and self.graph is None:
+            self.capture()
+            if latents is not None:  # the warm-up step consumed the inputs: restage them
+                self.set_inputs(latents, ctx)
+        for _ in range(self.steps):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.step()
+        return self.latents_nchw()
+
+    def latents_nchw(self):
+        return K.nhwc_to_nchw(self.lat, self.cin)

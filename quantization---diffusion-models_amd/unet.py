@@ -1,0 +1,464 @@
+"""SD1.5 / SDXL UNet2DConditionModel on MI355X: module tree with diffusers parameter names,
+NHWC fused forward through libqdiff kernels.
+
+The reference runs the third-party diffusers UNet (absent here) with its nn.Linear / nn.Conv2d
+children swapped for WxAxLinear / WxAxConv2d (quantizer.py:491-533).  This module rebuilds the
+same tree - same attribute names, so ``state_dict`` keys equal diffusers'
+``unet/diffusion_pytorch_model.safetensors`` keys and the reference's traversal
+(quantizer.py:142-159) finds exactly the same 184 Linear + 98 Conv2d layers for SD1.5 - and
+implements the forward itself, MI355X-first:
+
+* activations are NHWC fp16 (== token layout [N, HW, C]); no NCHW<->tokens permutes exist;
+* every conv is an implicit GEMM; the input fake-quant of a conv is fused into the
+  GroupNorm(+SiLU) that produces it (a workgroup owns a whole (n, group) slab, so the
+  per-(n, c) amax is workgroup-local); the output fake-quant amax is reduced in the GEMM
+  epilogue and applied by one finalize pass that also adds the residual / time embedding;
+* the nearest-2x upsample is folded into the following conv's address computation;
+* the cross-attention K/V projections of the (step-invariant) text context are computed once
+  per generate() instead of once per step (identical values);
+* the whole step is captured into a HIP graph by the pipeline.
+
+Architecture restated from diffusers' published UNet2DConditionModel (parity of the third-party
+architecture is UNPINNED: diffusers is not installed; see DESIGN.md and oracle/unet_ref.py).
+"""
+from dataclasses import dataclass, field
+from typing import Optional, Sequence, Tuple, Union
+
+import torch
+from torch import nn
+
+from . import kernels as K
+from .fake_quant import WxAxConv2d, WxAxLinear
+
+
+@dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_out_channels: Tuple[int, ...] = (320, 640, 1280, 1280)
+    down_block_types: Tuple[str, ...] = ("CrossAttnDownBlock2D", "CrossAttnDownBlock2D",
+                                         "CrossAttnDownBlock2D", "DownBlock2D")
+    up_block_types: Tuple[str, ...] = ("UpBlock2D", "CrossAttnUpBlock2D", "CrossAttnUpBlock2D",
+                                       "CrossAttnUpBlock2D")
+    layers_per_block: int = 2
+    cross_attention_dim: int = 768
+    attention_head_dim: Union[int, Tuple[int, ...]] = 8   # diffusers legacy: = number of heads
+    transformer_layers_per_block: Union[int, Tuple[int, ...]] = 1
+    norm_num_groups: int = 32
+    norm_eps: float = 1e-5
+    use_linear_projection: bool = False
+    sample_size: int = 64
+    flip_sin_to_cos: bool = True
+    freq_shift: int = 0
+    # SDXL "text_time" additional embedding
+    addition_embed_type: Optional[str] = None
+    addition_time_embed_dim: Optional[int] = None
+    projection_class_embeddings_input_dim: Optional[int] = None
+
+    def heads(self, i):
+        h = self.attention_head_dim
+        return h[i] if isinstance(h, (tuple, list)) else h
+
+    def tlayers(self, i):
+        t = self.transformer_layers_per_block
+        return t[i] if isinstance(t, (tuple, list)) else t
+
+    @classmethod
+    def from_diffusers(cls, cfg: dict):
+        keys = set(cls.__dataclass_fields__)
+        kw = {k: (tuple(v) if isinstance(v, list) else v) for k, v in cfg.items() if k in keys}
+        return cls(**kw)
+
+
+SD15 = UNetConfig()
+SDXL = UNetConfig(block_out_channels=(320, 640, 1280),
+                  down_block_types=("DownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D"),
+                  up_block_types=("CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "UpBlock2D"),
+                  cross_attention_dim=2048, attention_head_dim=(5, 10, 20),
+                  transformer_layers_per_block=(1, 2, 10), use_linear_projection=True, sample_size=128,
+                  addition_embed_type="text_time", addition_time_embed_dim=256,
+                  projection_class_embeddings_input_dim=2816)
+
+
+def tiny_config(**kw):
+    """A small SD1.5-shaped config for parity tests (same block structure)."""
+    base = dict(block_out_channels=(64, 128), down_block_types=("CrossAttnDownBlock2D", "DownBlock2D"),
+                up_block_types=("UpBlock2D", "CrossAttnUpBlock2D"), cross_attention_dim=64,
+                attention_head_dim=2, sample_size=16, norm_num_groups=32)
+    base.update(kw)
+    return UNetConfig(**base)
+
+
+# ------------------------------------------------------------------ module tree (diffusers names)
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin, cout, temb, groups, eps):
+        super().__init__()
+        self.groups, self.eps = groups, eps
+        self.norm1 = nn.GroupNorm(groups, cin, eps=eps, affine=True)
+        self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
+        self.time_emb_proj = nn.Linear(temb, cout)
+        self.norm2 = nn.GroupNorm(groups, cout, eps=eps, affine=True)
+        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
+        self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
+
+
+class Attention(nn.Module):
+    def __init__(self, query_dim, heads, dim_head, cross_dim=None):
+        super().__init__()
+        inner = heads * dim_head
+        self.heads = heads
+        self.to_q = nn.Linear(query_dim, inner, bias=False)
+        self.to_k = nn.Linear(cross_dim or query_dim, inner, bias=False)
+        self.to_v = nn.Linear(cross_dim or query_dim, inner, bias=False)
+        self.to_out = nn.ModuleList([nn.Linear(inner, query_dim), nn.Dropout(0.0)])
+
+
+class GEGLU(nn.Module):
+    def __init__(self, dim, inner):
+        super().__init__()
+        self.proj = nn.Linear(dim, inner * 2)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, mult=4):
+        super().__init__()
+        self.net = nn.ModuleList([GEGLU(dim, dim * mult), nn.Dropout(0.0), nn.Linear(dim * mult, dim)])
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, heads, cross_dim):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn1 = Attention(dim, heads, dim // heads)
+        self.norm2 = nn.LayerNorm(dim)
+        self.attn2 = Attention(dim, heads, dim // heads, cross_dim)
+        self.norm3 = nn.LayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+
+class Transformer2DModel(nn.Module):
+    def __init__(self, ch, heads, cross_dim, layers, groups, linear_proj):
+        super().__init__()
+        self.linear_proj = linear_proj
+        self.groups = groups
+        self.norm = nn.GroupNorm(groups, ch, eps=1e-6, affine=True)
+        self.proj_in = nn.Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(ch, heads, cross_dim) for _ in range(layers)])
+        self.proj_out = nn.Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, ch):
+        super().__init__()
+        self.conv = nn.Conv2d(ch, ch, 3, stride=2, padding=1)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, ch):
+        super().__init__()
+        self.conv = nn.Conv2d(ch, ch, 3, padding=1)
+
+
+class _Block(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.attentions = None
+        self.resnets = nn.ModuleList()
+        self.downsamplers = None
+        self.upsamplers = None
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.linear_1 = nn.Linear(cin, cout)
+        self.linear_2 = nn.Linear(cout, cout)
+
+
+class UNet2DConditionModel(nn.Module):
+    def __init__(self, cfg: UNetConfig = SD15):
+        super().__init__()
+        self.config = cfg
+        ch = cfg.block_out_channels
+        g, eps = cfg.norm_num_groups, cfg.norm_eps
+        temb = ch[0] * 4
+        self.conv_in = nn.Conv2d(cfg.in_channels, ch[0], 3, padding=1)
+        self.time_embedding = TimestepEmbedding(ch[0], temb)
+        if cfg.addition_embed_type == "text_time":
+            self.add_embedding = TimestepEmbedding(cfg.projection_class_embeddings_input_dim, temb)
+        else:
+            self.add_embedding = None
+        self.down_blocks = nn.ModuleList()
+        prev = ch[0]
+        for i, t in enumerate(cfg.down_block_types):
+            out = ch[i]
+            blk = _Block()
+            attn = t == "CrossAttnDownBlock2D"
+            if attn:
+                blk.attentions = nn.ModuleList()
+            for j in range(cfg.layers_per_block):
+                blk.resnets.append(ResnetBlock2D(prev if j == 0 else out, out, temb, g, eps))
+                if attn:
+                    blk.attentions.append(Transformer2DModel(out, cfg.heads(i), cfg.cross_attention_dim,
+                                                             cfg.tlayers(i), g, cfg.use_linear_projection))
+            if i < len(ch) - 1:
+                blk.downsamplers = nn.ModuleList([Downsample2D(out)])
+            self.down_blocks.append(blk)
+            prev = out
+        # mid
+        self.mid_block = _Block()
+        self.mid_block.attentions = nn.ModuleList([Transformer2DModel(ch[-1], cfg.heads(len(ch) - 1),
+                                                                      cfg.cross_attention_dim,
+                                                                      cfg.tlayers(len(ch) - 1), g,
+                                                                      cfg.use_linear_projection)])
+        self.mid_block.resnets.append(ResnetBlock2D(ch[-1], ch[-1], temb, g, eps))
+        self.mid_block.resnets.append(ResnetBlock2D(ch[-1], ch[-1], temb, g, eps))
+        # up
+        self.up_blocks = nn.ModuleList()
+        rev = list(reversed(ch))
+        nrev_heads = [cfg.heads(len(ch) - 1 - i) for i in range(len(ch))]
+        nrev_layers = [cfg.tlayers(len(ch) - 1 - i) for i in range(len(ch))]
+        prev = rev[0]
+        for i, t in enumerate(cfg.up_block_types):
+            out = rev[i]
+            inp = rev[min(i + 1, len(ch) - 1)]
+            blk = _Block()
+            attn = t == "CrossAttnUpBlock2D"
+            if attn:
+                blk.attentions = nn.ModuleList()
+            for j in range(cfg.layers_per_block + 1):
+                skip = inp if j == cfg.layers_per_block else out
+                rin = prev if j == 0 else out
+                blk.resnets.append(ResnetBlock2D(rin + skip, out, temb, g, eps))
+                if attn:
+                    blk.attentions.append(Transformer2DModel(out, nrev_heads[i], cfg.cross_attention_dim,
+                                                             nrev_layers[i], g, cfg.use_linear_projection))
+            if i < len(ch) - 1:
+                blk.upsamplers = nn.ModuleList([Upsample2D(out)])
+            self.up_blocks.append(blk)
+            prev = out
+        self.conv_norm_out = nn.GroupNorm(g, ch[0], eps=eps)
+        self.conv_out = nn.Conv2d(ch[0], cfg.out_channels, 3, padding=1)
+
+    # ---------------------------------------------------------------- init
+    @torch.no_grad()
+    def init_synthetic(self, seed=0):
+        """weights N(0, 1/fan_in) (seed 0), biases 0, norm gamma 1 beta 0.
+        Drawn in fp32 on the CPU generator (device independent), stored fp16."""
+        gen = torch.Generator("cpu").manual_seed(seed)
+        for name, p in self.named_parameters():
+            if name.endswith("weight") and p.dim() >= 2:
+                fan_in = p[0].numel()
+                p.copy_((torch.randn(p.shape, generator=gen) / fan_in ** 0.5).to(p.dtype))
+            elif name.endswith("bias"):
+                p.zero_()
+            elif name.endswith("weight"):
+                p.fill_(1.0)
+        return self
+
+    # ---------------------------------------------------------------- NHWC fused forward
+    def forward(self, *a, **k):  # pragma: no cover - the pipeline drives fwd()
+        raise RuntimeError("use UNet2DConditionModel.fwd(x_nhwc, temb_in, ctx_kv) (NHWC fused path)")
+
+    @torch.no_grad()
+    def prepare_context(self, ctx):
+        """Cross-attention K/V of the text context for every attn2: {id(attn2): (k, v)}."""
+        kv = {}
+        B, S, D = ctx.shape
+        c2 = ctx.reshape(B * S, D).contiguous()
+        for m in self.modules():
+            if isinstance(m, BasicTransformerBlock):
+                k = run_linear(m.attn2.to_k, c2).view(B, S, -1)
+                v = run_linear(m.attn2.to_v, c2).view(B, S, -1)
+                kv[id(m.attn2)] = (k, v)
+        return kv
+
+    @torch.no_grad()
+    def fwd(self, x, temb_in, ctx_kv, add_emb_in=None):
+        """x: [2B, H, W, Cp] fp16 NHWC (Cp = in_channels padded to 8); temb_in: [2B, C0] fp16
+        sinusoidal timestep features; returns the noise prediction [2B, H, W, 8] (4 real ch)."""
+        cfg = self.config
+        t = run_linear(self.time_embedding.linear_1, temb_in)
+        t = K.silu(t, out=t)
+        temb = run_linear(self.time_embedding.linear_2, t)
+        if self.add_embedding is not None:
+            if add_emb_in is None:
+                raise ValueError("SDXL UNet needs the text_time additional embedding input")
+            a = run_linear(self.add_embedding.linear_1, add_emb_in)
+            a = K.silu(a, out=a)
+            temb = run_linear(self.add_embedding.linear_2, a, residual=temb)
+        temb_silu = K.silu(temb)
+
+        h = run_conv(self.conv_in, x, c_valid=cfg.in_channels)
+        skips = [h]
+        for blk in self.down_blocks:
+            for i, res in enumerate(blk.resnets):
+                h = resnet_fwd(res, h, temb_silu)
+                if blk.attentions is not None:
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv)
+                skips.append(h)
+            if blk.downsamplers is not None:
+                h = run_conv(blk.downsamplers[0].conv, h)
+                skips.append(h)
+        mb = self.mid_block
+        h = resnet_fwd(mb.resnets[0], h, temb_silu)
+        h = transformer_fwd(mb.attentions[0], h, ctx_kv)
+        h = resnet_fwd(mb.resnets[1], h, temb_silu)
+        for blk in self.up_blocks:
+            for i, res in enumerate(blk.resnets):
+                skip = skips.pop()
+                h = resnet_fwd(res, h, temb_silu, skip=skip)
+                if blk.attentions is not None:
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv)
+            if blk.upsamplers is not None:
+                h = run_conv(blk.upsamplers[0].conv, h, upsample=True)
+        q = conv_qbits(self.conv_out)
+        h = K.groupnorm_nhwc(h, self.conv_norm_out.num_groups, self.conv_norm_out.eps,
+                             _f16(self.conv_norm_out.weight), _f16(self.conv_norm_out.bias), silu=True, q_bits=q)
+        return run_conv(self.conv_out, h, prequant=bool(q), co_pad=8)
+
+
+# ------------------------------------------------------------------ fused layer helpers
+def _f16(t):
+    if t is None:
+        return None
+    if t.dtype != torch.float16 or not t.is_contiguous():
+        raise RuntimeError("UNet parameters must be fp16 contiguous (call .half())")
+    return t
+
+
+def conv_qbits(layer):
+    """Input/output act-quant bits of a conv whose input quant can be fused (per_channel)."""
+    if isinstance(layer, WxAxConv2d) and layer.quantise_act:
+        return layer.n_bits_A if layer.act_quant_name == "per_channel" else -1
+    return 0
+
+
+def _conv_weight(layer, co_pad=None):
+    """[Co(_pad)][kh][kw][Ci_pad] fp16 operand + padded bias, cached on the module."""
+    w = layer.weight
+    ver = (w.data_ptr(), w._version, co_pad)
+    cache = getattr(layer, "_qd_cache", None)
+    if cache is not None and cache[0] == ver:
+        return cache[1], cache[2]
+    ci = w.shape[1]
+    cip = (ci + 7) // 8 * 8
+    wk = K.conv_weight_khwc(w.detach().contiguous(), cip)
+    b = layer.bias.detach() if layer.bias is not None else None
+    if co_pad is not None and co_pad > wk.shape[0]:
+        wpad = torch.zeros(co_pad, *wk.shape[1:], dtype=wk.dtype, device=wk.device)
+        wpad[: wk.shape[0]] = wk
+        wk = wpad
+        if b is not None:
+            bp = torch.zeros(co_pad, dtype=b.dtype, device=b.device)
+            bp[: b.shape[0]] = b
+            b = bp
+    layer._qd_cache = (ver, wk, b)
+    return wk, b
+
+
+def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=False, c_valid=0, co_pad=None):
+    """NHWC conv of an nn.Conv2d or WxAxConv2d with the reference's act fake-quant semantics:
+    q_x = act_quant(x) -> y = conv(q_x) + b -> q_y = act_quant(y) -> [+ residual | + temb]."""
+    if isinstance(layer, WxAxConv2d):
+        layer._check_supported()
+    wk, bias = _conv_weight(layer, co_pad)
+    stride, pad = layer.stride[0], layer.padding[0]
+    ci = layer.weight.shape[1]
+    q = conv_qbits(layer)
+    if q < 0:  # non-per_channel act granularity: run the drop-in NCHW module (same kernels)
+        return _conv_via_module(layer, x, residual, chan_add, upsample, co_pad)
+    if q and not prequant:
+        amax = K.act_absmax(x, "per_channel", K.NHWC)
+        x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
+    if q:
+        n = x.shape[0]
+        amax = torch.empty(n * wk.shape[0], dtype=torch.float32, device=x.device)
+        y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax)
+        return K.fq_finalize(y, amax, q, residual=residual, chan_add=chan_add, out=y)
+    if chan_add is None:
+        return K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, residual=residual)
+    y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias)
+    return K.fq_finalize(y, None, 0, residual=residual, chan_add=chan_add, out=y)
+
+
+def _conv_via_module(layer, x, residual, chan_add, upsample, co_pad):
+    n, h, w, cp = x.shape
+    if upsample:
+        raise NotImplementedError("upsample fusion needs per_channel act quant")
+    xn = K.nhwc_to_nchw(x, layer.in_channels)
+    y = layer(xn)
+    yh = K.nchw_to_nhwc(y.contiguous(), co_pad or y.shape[1])
+    if residual is not None or chan_add is not None:
+        yh = K.fq_finalize(yh, None, 0, residual=residual, chan_add=chan_add, out=yh)
+    return yh
+
+
+def run_linear(layer, x2d, residual=None):
+    """x2d [M, K] -> [M, N] for an nn.Linear or WxAxLinear (fake_quant.py:214-225 semantics)."""
+    hook = getattr(layer, "_qd_hook", None)
+    if hook is not None:  # SmoothQuant calibration (calib.py)
+        hook(x2d)
+    if isinstance(layer, WxAxLinear):
+        xin = layer.act_quant(x2d) if layer.quantize_act else x2d
+        w, fmt, sc, g = layer.gemm_weight()
+        if layer.output_quant_name != "None":
+            y = K.linear(xin, w, fmt, sc, g, bias=layer.bias)
+            y = K.act_fakequant(y, layer.output_quant_name, layer.n_bits_A, out=y)
+            return K.add(y, residual, out=y) if residual is not None else y
+        return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual)
+    return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual)
+
+
+def resnet_fwd(res, x, temb_silu, skip=None):
+    """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1)."""
+    xin = K.concat_c(x, skip) if skip is not None else x
+    q1 = conv_qbits(res.conv1)
+    h = K.groupnorm_nhwc(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
+                         silu=True, q_bits=max(q1, 0))
+    tp = run_linear(res.time_emb_proj, temb_silu)
+    h = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp)
+    q2 = conv_qbits(res.conv2)
+    h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
+                         silu=True, q_bits=max(q2, 0))
+    sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
+    return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc)
+
+
+def transformer_fwd(tm, x, ctx_kv):
+    """diffusers Transformer2DModel (continuous input) + BasicTransformerBlock(s)."""
+    n, hh, ww, c = x.shape
+    if tm.linear_proj:
+        h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
+        t = run_linear(tm.proj_in, h.view(-1, c))
+    else:
+        q = conv_qbits(tm.proj_in)
+        h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias),
+                             q_bits=max(q, 0))
+        t = run_conv(tm.proj_in, h, prequant=q > 0).view(-1, c)
+    for blk in tm.transformer_blocks:
+        t = block_fwd(blk, t, n, hh * ww, ctx_kv)
+    if tm.linear_proj:
+        return run_linear(tm.proj_out, t, residual=x.view(-1, c)).view(n, hh, ww, c)
+    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x)
+
+
+def block_fwd(blk, t, n, s, ctx_kv):
+    """BasicTransformerBlock: self-attn, cross-attn, GEGLU feed-forward, each + residual."""
+    c = t.shape[1]
+    a1 = blk.attn1
+    h = K.layernorm(t, blk.norm1.eps, _f16(blk.norm1.weight), _f16(blk.norm1.bias))
+    q = run_linear(a1.to_q, h).view(n, s, c)
+    k = run_linear(a1.to_k, h).view(n, s, c)
+    v = run_linear(a1.to_v, h).view(n, s, c)
+    o = K.attention(q, k, v, a1.heads)
+    t = run_linear(a1.to_out[0], o.view(-1, c), residual=t)
+    a2 = blk.attn2
+    h = K.layernorm(t, blk.norm2.eps, _f16(blk.norm2.weight), _f16(blk.norm2.bias))
+    q = run_linear(a2.to_q, h).view(n, s, c)
+    k, v = ctx_kv[id(a2)]
+    o = K.attention(q, k, v, a2.heads)
+    t = run_linear(a2.to_out[0], o.view(-1, c), residual=t)
+    h = K.layernorm(t, blk.norm3.eps, _f16(blk.norm3.weight), _f16(blk.norm3.bias))
+    g = K.geglu(run_linear(blk.ff.net[0].proj, h))
+    return run_linear(blk.ff.net[2], g, residual=t)

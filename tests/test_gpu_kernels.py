@@ -1,0 +1,315 @@
+"""HIP kernels vs the golden-pinned oracle (bit-exact for the fake-quant math) and vs fp32 torch
+references for the floating-point kernels (GEMM / conv / attention / norms), with the
+tolerance stated in each test.  Runs on the MI355X (-m gpu)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import fake_quant_np as FQ
+from oracle import fake_quant_torch as FT
+from oracle.unet_ref import ddim_step, timestep_embedding
+
+pytestmark = pytest.mark.gpu
+
+
+def K():
+    from qdiff import kernels
+    return kernels
+
+
+def same_bits(a, b):
+    a = np.ascontiguousarray(a, dtype=np.float16)
+    b = np.ascontiguousarray(b, dtype=np.float16)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint16), b.view(np.uint16))
+
+
+def ulp16(x):
+    """fp16 ulp of |x| (x float32 tensor)."""
+    a = x.abs().clamp(min=6.1e-5)
+    return torch.pow(2.0, torch.floor(torch.log2(a)) - 10)
+
+
+def assert_fp16_close(got, ref, ulps=2.0, atol=1e-3, frac=1.0):
+    """|got - ref| <= ulps * ulp16(ref) + atol for at least `frac` of the elements."""
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    ok = (got - ref).abs() <= ulps * ulp16(ref) + atol
+    assert torch.isfinite(got).all()
+    assert ok.float().mean().item() >= frac, f"{(~ok).sum().item()} / {ok.numel()} outside tolerance; " \
+        f"max err {(got - ref).abs().max().item():.4g}"
+
+
+# ------------------------------------------------------------------ fake-quant: bit-exact
+def test_act_quant_bit_exact(golden, dev):
+    k = K()
+    g = golden["fake_quant_golden"]
+    for bits in (4, 8, 16):
+        x = torch.from_numpy(g[f"atok_b{bits}_in"]).to(dev)
+        assert same_bits(k.act_fakequant(x, "per_token", bits).cpu().numpy(), g[f"atok_b{bits}_out"])
+        x = torch.from_numpy(g[f"achan_b{bits}_in"]).to(dev)
+        assert same_bits(k.act_fakequant(x, "per_channel", bits, layout=k.NCHW).cpu().numpy(), g[f"achan_b{bits}_out"])
+        # NHWC path on the transposed tensor
+        xh = x.permute(0, 2, 3, 1).contiguous()
+        yh = k.act_fakequant(xh, "per_channel", bits, layout=k.NHWC).permute(0, 3, 1, 2).cpu().numpy()
+        assert same_bits(yh, g[f"achan_b{bits}_out"])
+        x = torch.from_numpy(g[f"aten_b{bits}_in"]).to(dev)
+        assert same_bits(k.act_fakequant(x, "per_tensor", bits).cpu().numpy(), g[f"aten_b{bits}_out"])
+        x = torch.from_numpy(g[f"agrp_b{bits}_in"]).to(dev)
+        assert same_bits(k.act_fakequant(x, "per_group", bits, layout=k.NCHW, group=6).cpu().numpy(),
+                         g[f"agrp_b{bits}_out"])
+
+
+def test_public_quant_functions(golden, dev):
+    import qdiff
+    g = golden["fake_quant_golden"]
+    for bits in (4, 8):
+        for kk in (320, 768, 5120):
+            w = torch.from_numpy(g[f"wgroup_b{bits}_k{kk}_in"]).to(dev)
+            assert same_bits(qdiff.quantize_weight_absmax(w, bits, 128).cpu().numpy(), g[f"wgroup_b{bits}_k{kk}_out"])
+        w = torch.from_numpy(g[f"wpc_b{bits}_64x32x3x3_in"]).to(dev)
+        assert same_bits(qdiff.quantize_weight_per_channel_absmax(w, bits).cpu().numpy(), g[f"wpc_b{bits}_64x32x3x3_out"])
+        w = torch.from_numpy(g[f"wpt_b{bits}_in"]).to(dev)
+        assert same_bits(qdiff.quantize_weight_per_tensor_absmax(w, bits).cpu().numpy(), g[f"wpt_b{bits}_out"])
+    x = torch.from_numpy(g["agrp_b8_in"]).to(dev)
+    assert same_bits(qdiff.quantize_activation_per_channel_group_absmax(x, 8, 8).cpu().numpy(), g["agrp_b8_out"])
+
+
+def test_weight_codes(golden, dev):
+    k = K()
+    g = golden["fake_quant_golden"]
+    for bits in (4, 8):
+        w = g[f"wgroup_b{bits}_k2560_in"]
+        codes, scales, wdq = k.weight_quant(torch.from_numpy(w).to(dev), 128, bits)
+        c_ref, s_ref, _ = FQ.quantize_weight_absmax_codes(w, bits, 128)
+        assert np.array_equal(codes.cpu().numpy(), c_ref)
+        assert same_bits(scales.cpu().numpy(), s_ref)
+        assert same_bits(wdq.cpu().numpy(), g[f"wgroup_b{bits}_k2560_out"])
+        if bits == 4:
+            packed = k.pack_int4(codes).cpu().numpy()
+            lo = (packed & 0xF).astype(np.int8)
+            hi = (packed >> 4).astype(np.int8)
+            lo[lo >= 8] -= 16
+            hi[hi >= 8] -= 16
+            assert np.array_equal(np.stack([lo, hi], -1).reshape(c_ref.shape), c_ref)
+
+
+def test_fq_finalize_bit_exact(dev):
+    k = K()
+    rng = np.random.default_rng(3)
+    y = (rng.standard_normal((2, 8, 8, 64)) * 3).astype(np.float16)
+    res = rng.standard_normal((2, 8, 8, 64)).astype(np.float16)
+    yt = torch.from_numpy(y).to(dev)
+    amax = k.act_absmax(yt, "per_channel", k.NHWC)
+    out = k.fq_finalize(yt, amax, 8, residual=torch.from_numpy(res).to(dev)).cpu().numpy()
+    ref = FQ.quantize_activation_per_channel_absmax(y.transpose(0, 3, 1, 2), 8).transpose(0, 2, 3, 1)
+    ref = (ref.astype(np.float32) + res.astype(np.float32)).astype(np.float16)
+    assert same_bits(out, ref)
+    cadd = rng.standard_normal((2, 64)).astype(np.float16)
+    out2 = k.fq_finalize(yt, amax, 8, chan_add=torch.from_numpy(cadd).to(dev)).cpu().numpy()
+    ref2 = FQ.quantize_activation_per_channel_absmax(y.transpose(0, 3, 1, 2), 8).transpose(0, 2, 3, 1)
+    ref2 = (ref2.astype(np.float32) + cadd[:, None, None, :].astype(np.float32)).astype(np.float16)
+    assert same_bits(out2, ref2)
+
+
+def test_smooth_fold_and_hook(golden, dev):
+    k = K()
+    s = golden["smooth_golden"]
+    lnw = torch.from_numpy(s["ln_w_in"]).to(dev)
+    lnb = torch.from_numpy(s["ln_b_in"]).to(dev)
+    fcs = [torch.from_numpy(s[f"fc{i}_w_in"]).to(dev) for i in range(3)]
+    k.smooth_fold(lnw, lnb, fcs, torch.from_numpy(s["act"]).to(dev), 0.8)
+    # powf on device vs the reference's pow: at most a handful of 1-ulp scale differences
+    nbad = int((lnw.cpu().numpy() != s["ln_w_out"]).sum())
+    assert nbad <= 3, nbad
+    x = torch.from_numpy(s["hook_x"].reshape(-1, 320)).to(dev)
+    ws = torch.empty(320, dtype=torch.float32, device=dev)
+    sm = torch.zeros(320, dtype=torch.float32, device=dev)
+    am = torch.empty(320, dtype=torch.float16, device=dev)
+    k.channel_absmax_accum(x, ws, sm, am)
+    k.channel_absmax_accum(x, ws, sm, None)
+    assert same_bits(am.cpu().numpy(), s["hook_amax"])
+    assert torch.equal(sm.cpu(), 2 * torch.from_numpy(s["hook_amax"]).float())
+
+
+# ------------------------------------------------------------------ GEMMs vs fp32 torch
+@pytest.mark.parametrize("M,N,Kd", [(128, 128, 64), (200, 320, 320), (616, 640, 768), (4096, 2560, 320),
+                                    (8, 1280, 1280), (1000, 64, 128)])
+@pytest.mark.parametrize("fmt", ["f16", "i8", "i4"])
+def test_linear_formats(M, N, Kd, fmt, dev):
+    k = K()
+    g = torch.Generator().manual_seed(M + N + Kd)
+    x = torch.randn(M, Kd, generator=g).half()
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half()
+    b = torch.randn(N, generator=g).half()
+    res = torch.randn(M, N, generator=g).half()
+    bits = {"f16": 8, "i8": 8, "i4": 4}[fmt]
+    gs = FQ.shrink_group(Kd, 128)
+    codes, scales, wdq = k.weight_quant(w.to(dev), gs, bits)
+    if fmt == "f16":
+        op, sc, grp = wdq, None, 0
+    elif fmt == "i8":
+        op, sc, grp = codes, scales, gs
+    else:
+        op, sc, grp = k.pack_int4(codes), scales, gs
+    y = k.linear(x.to(dev), op, fmt, sc, grp, bias=b.to(dev), residual=res.to(dev))
+    yf = (x.float() @ wdq.cpu().float().t() + b.float()).half().float() + res.float()
+    # fp32 accumulation order differs -> the fp16 rounding of y may move by 1 ulp (then the
+    # residual add by one more); 2 ulp + 1e-3 everywhere
+    assert_fp16_close(y, yf, ulps=2.0, atol=1e-3)
+
+
+def test_linear_amax_epilogue(dev):
+    k = K()
+    g = torch.Generator().manual_seed(1)
+    M, N, Kd = 4 * 256, 320, 640
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(N, Kd, generator=g) / 25).half().to(dev)
+    amax = torch.empty(4 * N, dtype=torch.float32, device=dev)
+    y = k.linear(x, w, "f16", amax=amax, rows_per_sample=256)
+    ref = y.float().abs().view(4, 256, N).amax(1).reshape(-1)
+    assert torch.equal(amax, ref)
+
+
+@pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups", [(64, 64, 3, 1, 16, False), (64, 128, 3, 2, 16, False),
+                                                        (128, 64, 1, 1, 8, False), (4, 64, 3, 1, 16, False),
+                                                        (64, 64, 3, 1, 8, True), (320, 320, 3, 1, 32, False),
+                                                        (960, 320, 3, 1, 16, False)])
+def test_conv_nhwc(cin, cout, ksz, stride, hw, ups, dev):
+    k = K()
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    n = 2
+    x = torch.randn(n, cin, hw, hw, generator=g).half()
+    w = (torch.randn(cout, cin, ksz, ksz, generator=g) / (cin * ksz * ksz) ** 0.5).half()
+    b = torch.randn(cout, generator=g).half()
+    cip = (cin + 7) // 8 * 8
+    xh = k.nchw_to_nhwc(x.to(dev), cip)
+    wk = k.conv_weight_khwc(w.to(dev), cip)
+    pad = ksz // 2
+    amax = torch.empty(n * cout, dtype=torch.float32, device=dev)
+    y = k.conv2d_nhwc(xh, wk, cin, stride, pad, ups, bias=b.to(dev), amax=amax)
+    xin = F.interpolate(x.float(), scale_factor=2.0, mode="nearest") if ups else x.float()
+    ref = F.conv2d(xin, w.float(), b.float(), stride, pad).half().float()
+    got = k.nhwc_to_nchw(y).cpu().float()
+    assert_fp16_close(got, ref, ulps=2.0, atol=1e-3)
+    assert torch.equal(amax.view(n, cout).cpu(), got.abs().amax(dim=(2, 3)))
+
+
+# ------------------------------------------------------------------ attention
+@pytest.mark.parametrize("b,heads,sq,skv,d", [(2, 8, 256, 256, 40), (2, 8, 64, 77, 80), (1, 8, 128, 77, 160),
+                                              (2, 5, 200, 200, 64), (1, 2, 4096, 4096, 40)])
+def test_attention(b, heads, sq, skv, d, dev):
+    k = K()
+    g = torch.Generator().manual_seed(sq + skv + d)
+    c = heads * d
+    q = torch.randn(b, sq, c, generator=g).half()
+    kk = torch.randn(b, skv, c, generator=g).half()
+    v = torch.randn(b, skv, c, generator=g).half()
+    o = k.attention(q.to(dev), kk.to(dev), v.to(dev), heads).cpu().float()
+    qh = q.float().view(b, sq, heads, d).transpose(1, 2)
+    kh = kk.float().view(b, skv, heads, d).transpose(1, 2)
+    vh = v.float().view(b, skv, heads, d).transpose(1, 2)
+    p = torch.softmax(qh @ kh.transpose(-1, -2) / math.sqrt(d), -1)
+    ref = (p @ vh).transpose(1, 2).reshape(b, sq, c)
+    # P is rounded to fp16 before P.V (flash-style); error ~ 1e-3 relative to |V|
+    assert (o - ref).abs().max().item() < 1e-2
+
+
+# ------------------------------------------------------------------ norms / elementwise
+@pytest.mark.parametrize("c,hw,silu,q", [(320, 64, True, 8), (640, 256, True, 0), (960, 16, True, 8),
+                                         (64, 256, False, 8), (2560, 16, True, 4)])
+def test_groupnorm_fused(c, hw, silu, q, dev):
+    k = K()
+    g = torch.Generator().manual_seed(c + hw)
+    n = 2
+    x = (torch.randn(n, c, hw, generator=g) * 2 + 0.5).half()
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
+    bet = (0.1 * torch.randn(c, generator=g)).half()
+    xh = x.transpose(1, 2).contiguous().to(dev)  # NHWC [n, hw, c]
+    y = k.groupnorm_nhwc(xh, 32, 1e-5, gam.to(dev), bet.to(dev), silu=silu, q_bits=q)
+    ref = F.group_norm(x.view(n, c, hw, 1), 32, gam, bet, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    got = y.cpu().transpose(1, 2).reshape(n, c, hw, 1)
+    if q:
+        ref = FT.per_channel(ref, q)
+        # a 1-ulp GN difference can flip one rounding step of the fake-quant grid
+        step = ref.float().abs().amax(dim=(2, 3), keepdim=True) / (2 ** (q - 1) - 1)
+        err = (got.float() - ref.float()).abs()
+        assert (err <= step * 1.01 + 1e-3).all()
+        assert (err <= 1e-3).float().mean() > 0.995
+    else:
+        assert_fp16_close(got, ref, ulps=2.0, atol=2e-3)
+
+
+def test_groupnorm_two_sources(dev):
+    k = K()
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(2, 64, 640, generator=g).half()
+    b2 = torch.randn(2, 64, 320, generator=g).half()
+    gam = torch.ones(960).half()
+    bet = torch.zeros(960).half()
+    y1 = k.groupnorm_nhwc(a.to(dev), 32, 1e-5, gam.to(dev), bet.to(dev), silu=True, x2=b2.to(dev))
+    y2 = k.groupnorm_nhwc(k.concat_c(a.to(dev), b2.to(dev)), 32, 1e-5, gam.to(dev), bet.to(dev), silu=True)
+    assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize("rows,c", [(77, 320), (4096, 640), (33, 1280), (5, 2048)])
+def test_layernorm(rows, c, dev):
+    k = K()
+    g = torch.Generator().manual_seed(rows + c)
+    x = (torch.randn(rows, c, generator=g) * 3).half()
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
+    bet = (0.1 * torch.randn(c, generator=g)).half()
+    y = k.layernorm(x.to(dev), 1e-5, gam.to(dev), bet.to(dev)).cpu()
+    ref = F.layer_norm(x.float(), (c,), gam.float(), bet.float(), 1e-5)
+    assert_fp16_close(y, ref, ulps=2.0, atol=2e-3)
+
+
+def test_elementwise(dev):
+    k = K()
+    g = torch.Generator().manual_seed(9)
+    h = (torch.randn(300, 2 * 640, generator=g) * 2).half()
+    out = k.geglu(h.to(dev)).cpu()
+    a, gate = h.chunk(2, -1)
+    ref = (a.float() * F.gelu(gate.float()).half().float()).half()
+    assert_fp16_close(out, ref, ulps=1.0, atol=1e-3)
+    x = (torch.randn(1000, generator=g) * 4).half()
+    assert_fp16_close(k.silu(x.to(dev)).cpu(), F.silu(x.float()), ulps=1.0, atol=1e-4)
+    y = torch.randn(1000, generator=g).half()
+    assert torch.equal(k.add(x.to(dev), y.to(dev)).cpu(), (x.float() + y.float()).half())
+    a2 = torch.randn(6, 5, 24, generator=g).half()
+    b2 = torch.randn(6, 5, 40, generator=g).half()
+    assert torch.equal(k.concat_c(a2.to(dev), b2.to(dev)).cpu(), torch.cat([a2, b2], -1))
+    xn = torch.randn(2, 5, 7, 9, generator=g).half()
+    xh = k.nchw_to_nhwc(xn.to(dev), 8)
+    assert torch.equal(xh[..., :5].cpu(), xn.permute(0, 2, 3, 1)) and xh[..., 5:].abs().sum().item() == 0
+    assert torch.equal(k.nhwc_to_nchw(xh, 5).cpu(), xn)
+
+
+def test_timestep_embedding_and_ddim(dev):
+    k = K()
+    from qdiff.scheduler import ddim_tables
+    ts, a_t, a_p = ddim_tables(50)
+    ts_d = ts.float().to(dev)
+    idx = torch.tensor([7], dtype=torch.int32, device=dev)
+    e = k.timestep_embedding(ts_d, idx, 3, 320).cpu()
+    ref = timestep_embedding(torch.full((3,), int(ts[7])), 320).half()
+    assert_fp16_close(e, ref, ulps=1.0, atol=2e-3)
+    # CFG + DDIM step
+    g = torch.Generator().manual_seed(2)
+    B, h, w = 2, 8, 8
+    lat = torch.randn(B, 4, h, w, generator=g).half()
+    eps = torch.randn(2 * B, 4, h, w, generator=g).half()
+    lat_h = k.nchw_to_nhwc(lat.to(dev), 8)
+    eps_h = k.nchw_to_nhwc(eps.to(dev), 8)
+    nxt = torch.zeros(2 * B, h, w, 8, dtype=torch.float16, device=dev)
+    step = torch.tensor([5], dtype=torch.int32, device=dev)
+    k.cfg_ddim_step(lat_h, eps_h, 7.5, a_t.to(dev), a_p.to(dev), step, nxt, c=4)
+    got = k.nhwc_to_nchw(lat_h, 4).cpu()
+    ref = ddim_step(eps, 5, lat, a_t, a_p, 7.5)
+    assert_fp16_close(got, ref, ulps=2.0, atol=1e-3)
+    assert step.item() == 6
+    assert torch.equal(k.nhwc_to_nchw(nxt[:B], 4), k.nhwc_to_nchw(nxt[B:], 4))
