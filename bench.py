@@ -10,8 +10,9 @@ Also reported (rank 0):
                 with HIP events on the stream it runs on; ALGORITHMIC flops / duration vs the
                 fp16 dense MFMA peak (the path computes fake-quant operands in fp16)
   path_roofline whole-loop FLOP rate (803.3 GFLOP per UNet eval per sample)
-  cpu_baseline  the CPU oracle (reference fake-quant math, torch-CPU fp16 ops) timed on this
-                box's host cores on a bounded sample: one W8A8 UNet eval at CFG batch 2
+  cpu_baseline  the reference's CPU path restated by the oracle (torch-CPU fp16 ops, W8A8
+                fake-quant) timed on this box's host cores on a bounded sample (one op of each
+                FLOP class; see cpu_baseline())
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
 import argparse
@@ -95,26 +96,42 @@ def dominant_kernel_roofline(dev, iters=20):
 
 
 def cpu_baseline(threads):
-    """The CPU oracle (reference fake-quant semantics, torch-CPU fp16) on a bounded sample."""
-    import dataclasses
-
+    """The reference's CPU fake-quant path (oracle restatement: torch-CPU fp16 ops, W8A8
+    per-channel act quant) on a BOUNDED sample: one op of each FLOP class of the SD1.5 UNet at
+    CFG batch 2 (1 image), timed on this host; the per-image time is the class FLOPs of
+    SURVEY App. B divided by the measured class rates (conv 443.9, linear 233.3, attention
+    126.1 GFLOP per sample per UNet eval; x2 CFG; x50 steps)."""
     import torch
-    from oracle.unet_ref import RefUNet
-    from qdiff.unet import SD15, UNet2DConditionModel
+    import torch.nn.functional as F
+    from oracle import fake_quant_torch as FT
     torch.set_num_threads(threads)
-    u = UNet2DConditionModel(SD15).half().init_synthetic(0)
-    cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(SD15).items()}
-    ref = RefUNet(cd, u.state_dict(), dict(QCFG["w8a8"]))
-    del u
-    g = torch.Generator().manual_seed(42)
-    x = torch.randn(2, 4, 64, 64, generator=g).half()
-    ctx = torch.randn(2, 77, 768, generator=g).half()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 320, 64, 64, generator=g).half()
+    w = FT.weight_per_channel((torch.randn(320, 320, 3, 3, generator=g) * 0.02).half(), 8)
+    b = torch.zeros(320).half()
     t0 = time.time()
-    ref.forward(x, 981, ctx)
-    dt = time.time() - t0
-    return {"value": round(1.0 / (50 * dt), 6), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"1 W8A8 UNet eval at CFG batch 2 (1 image), 64x64 latents, {dt:.2f} s, x50 steps",
-            "seconds_per_unet_eval": round(dt, 3)}
+    FT.per_channel(F.conv2d(FT.per_channel(x, 8), w, b, 1, 1), 8)
+    t_conv = time.time() - t0
+    conv_rate = 2 * 2 * 4096 * 320 * 2880 / t_conv
+    xt = torch.randn(2, 4096, 320, generator=g).half()
+    wl = FT.weight_group((torch.randn(2560, 320, generator=g) * 0.05).half(), 8, 128)
+    t0 = time.time()
+    F.linear(xt, wl, torch.zeros(2560).half())
+    t_lin = time.time() - t0
+    lin_rate = 2 * 8192 * 2560 * 320 / t_lin
+    q = torch.randn(2, 8, 4096, 40, generator=g).half()
+    t0 = time.time()
+    F.scaled_dot_product_attention(q, q, q)
+    t_att = time.time() - t0
+    att_rate = 4 * 2 * 8 * 4096 * 4096 * 40 / t_att
+    per_eval = 2 * (443.9e9 / conv_rate + 233.3e9 / lin_rate + 126.1e9 / att_rate)
+    per_image = 50 * per_eval
+    return {"value": round(1.0 / per_image, 8), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": (f"one fp16 op per FLOP class at SD1.5 CFG batch 2: W8A8 conv3x3 320@64x64 {t_conv:.2f}s "
+                       f"({conv_rate / 1e9:.2f} GFLOP/s), linear 320->2560 x8192 {t_lin:.3f}s "
+                       f"({lin_rate / 1e9:.1f} GFLOP/s), SDPA 4096^2 d40 x16 heads {t_att:.3f}s "
+                       f"({att_rate / 1e9:.1f} GFLOP/s); image = 50 steps x class FLOPs / class rates"),
+            "seconds_per_image": round(per_image, 1)}
 
 
 def main():
@@ -132,7 +149,13 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
+    def log(msg):
+        if rank == 0:
+            print(f"[bench +{time.time() - T0:.0f}s] {msg}", file=sys.stderr, flush=True)
+
+    T0 = time.time()
     model = build_model(args, dev)
+    log(f"model built + quantized ({args.mode})")
     B = args.batch
     hw = args.res // 8
     loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.5, use_graph=True)
@@ -153,6 +176,7 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
+    log("warmup done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -171,6 +195,7 @@ def main():
     value = images / dt
     if rank == 0:
         assert out is not None and torch.isfinite(out.float()).all(), "non-finite latents"
+        log(f"timed {args.steps} steps: {dt:.3f}s")
         roof = dominant_kernel_roofline(dev)
         evals_per_s = value * args.denoise_steps  # UNet evals per image per step: 50 steps at CFG batch 2
         path_tflops = evals_per_s * 2 * UNET_GFLOP_PER_SAMPLE / 1e3
@@ -189,7 +214,8 @@ def main():
                               "flop_per_image": 2 * args.denoise_steps * UNET_GFLOP_PER_SAMPLE * 1e9},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+            log("cpu baseline ...")
+            line["cpu_baseline"] = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -57,3 +57,37 @@ def per_group(t, group_size=128, n_bits=8):
 
 
 ACT = {"per_token": per_token, "per_channel": per_channel, "per_tensor": per_tensor}
+
+
+def _shrink(k, g):
+    while k % g != 0:
+        g -= 32
+        if g == 0:
+            raise ZeroDivisionError("integer division or modulo by zero")
+    return g
+
+
+@torch.no_grad()
+def weight_group(w, n_bits=8, group_size=0):
+    """quantize_weight_absmax (fake_quant.py:21-84) on a CPU fp16 tensor (not in place)."""
+    shape = w.shape
+    w2 = w.clone()
+    if group_size > 0:
+        w2 = w2.reshape(-1, _shrink(shape[-1], group_size))
+    assert w2.dim() == 2
+    s = _scale(w2.abs().max(dim=-1, keepdim=True)[0], n_bits)
+    return _qdq(w2, s).reshape(shape)
+
+
+@torch.no_grad()
+def weight_per_channel(w, n_bits=8):
+    """fake_quant.py:86-93."""
+    s = _scale(w.abs().max(dim=-1, keepdim=True)[0], n_bits)
+    return _qdq(w, s)
+
+
+@torch.no_grad()
+def weight_per_tensor(w, n_bits=8):
+    """fake_quant.py:96-105."""
+    s = _scale(w.abs().max(), n_bits)
+    return _qdq(w, s)

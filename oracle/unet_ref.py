@@ -24,12 +24,19 @@ F16 = torch.float16
 
 
 # ------------------------------------------------------------------ weight quantization
-def quantize_state_dict(sd, qc):
+def quantize_state_dict(sd, qc, backend="torch"):
     """Return (qsd, flags): fake-quantized fp16 weights and per-layer activation flags.
 
     qc keys (AwqConfig): w_bit, a_bit, q_group_size, weight_quant_type, weight_quant_conv_type,
     act_quant_conv_type, quantize_act.  Linear = 2-D weight, Conv2d = 4-D weight.
+    backend "torch" (fast, CPU fp16 ops) or "numpy"; both are pinned bit-exactly by the goldens.
     """
+    if backend == "numpy":
+        wq = {"group": lambda w, b, g: torch.from_numpy(np.ascontiguousarray(FQ.quantize_weight_absmax(w.numpy(), b, g))),
+              "per_channel": lambda w, b: torch.from_numpy(np.ascontiguousarray(FQ.quantize_weight_per_channel_absmax(w.numpy(), b))),
+              "per_tensor": lambda w, b: torch.from_numpy(np.ascontiguousarray(FQ.quantize_weight_per_tensor_absmax(w.numpy(), b)))}
+    else:
+        wq = {"group": FT.weight_group, "per_channel": FT.weight_per_channel, "per_tensor": FT.weight_per_tensor}
     qsd = dict(sd)
     flags = {}
     for key, w in sd.items():
@@ -37,30 +44,25 @@ def quantize_state_dict(sd, qc):
             continue
         name = key[: -len(".weight")]
         child = name.split(".")[-1]
-        wn = w.to(F16).numpy()
+        w = w.to(F16).contiguous()
         if w.dim() == 2:
             wt = qc.get("weight_quant_type", "group")
             if wt == "group":
-                q = FQ.quantize_weight_absmax(wn, qc["w_bit"], qc.get("q_group_size", 128))
-            elif wt == "per_channel":
-                q = FQ.quantize_weight_per_channel_absmax(wn, qc["w_bit"])
-            elif wt == "per_tensor":
-                q = FQ.quantize_weight_per_tensor_absmax(wn, qc["w_bit"])
+                q = wq["group"](w, qc["w_bit"], qc.get("q_group_size", 128))
+            elif wt in ("per_channel", "per_tensor"):
+                q = wq[wt](w, qc["w_bit"])
             else:
                 raise ValueError(wt)
             qout = "k_proj" in child or "v_proj" in child or "q_proj" in child
             flags[name] = {"kind": "linear", "out_quant": qout, "a_bit": qc["a_bit"]}
         else:
             wt = qc.get("weight_quant_conv_type", "per_channel")
-            if wt == "per_channel":
-                q = FQ.quantize_weight_per_channel_absmax(wn, qc["w_bit"])
-            elif wt == "per_tensor":
-                q = FQ.quantize_weight_per_tensor_absmax(wn, qc["w_bit"])
-            else:
+            if wt not in ("per_channel", "per_tensor"):
                 raise ValueError(wt)
+            q = wq[wt](w, qc["w_bit"])
             flags[name] = {"kind": "conv", "act": qc.get("act_quant_conv_type", "per_channel"),
                            "quant": bool(qc.get("quantize_act", False)), "a_bit": qc["a_bit"]}
-        qsd[key] = torch.from_numpy(np.ascontiguousarray(q))
+        qsd[key] = q.contiguous()
     return qsd, flags
 
 
@@ -77,10 +79,41 @@ def timestep_embedding(t, dim, flip_sin_to_cos=True, shift=0.0, max_period=10000
     return emb
 
 
+class _Fp32Ops:
+    """Each torch op evaluated in fp32 and rounded to fp16 once ("single rounding" variant)."""
+
+    @staticmethod
+    def linear(x, w, b=None):
+        return F.linear(x.float(), w.float(), None if b is None else b.float()).half()
+
+    @staticmethod
+    def conv2d(x, w, b=None, stride=1, padding=0):
+        return F.conv2d(x.float(), w.float(), None if b is None else b.float(), stride, padding).half()
+
+    @staticmethod
+    def group_norm(x, g, w, b, eps):
+        return F.group_norm(x.float(), g, w.float(), b.float(), eps).half()
+
+    @staticmethod
+    def layer_norm(x, shape, w, b, eps):
+        return F.layer_norm(x.float(), shape, w.float(), b.float(), eps).half()
+
+    @staticmethod
+    def scaled_dot_product_attention(q, k, v, **kw):
+        return F.scaled_dot_product_attention(q.float(), k.float(), v.float(), **kw).half()
+
+
 class RefUNet:
-    def __init__(self, cfg, sd, qc=None):
+    """variant "half": torch-CPU Half kernels, the reference's own library calls (default).
+    variant "fp32": every GEMM / conv / norm / attention op computed in fp32 and rounded to fp16
+    once - the same math with a single rounding per op, i.e. what an fp32-accumulating
+    implementation (MFMA) computes.  The spread between the two variants measures how much the
+    fake-quant network amplifies ulp-level differences (tests/test_gpu_unet.py)."""
+
+    def __init__(self, cfg, sd, qc=None, variant="half"):
         """cfg: dict of UNetConfig fields; sd: {key: fp16 cpu tensor}; qc: AwqConfig dict or None."""
         self.cfg = cfg
+        self.ops = _Fp32Ops if variant == "fp32" else F
         sd = {k: v.detach().to("cpu", F16).contiguous() for k, v in sd.items()}
         if qc is not None:
             self.sd, self.flags = quantize_state_dict(sd, qc)
@@ -92,7 +125,7 @@ class RefUNet:
     def lin(self, name, x):
         if self.hooks is not None and name in self.hooks:
             self.hooks[name](x)
-        y = F.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias"))
+        y = self.ops.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias"))
         f = self.flags.get(name)
         if f and f["out_quant"]:
             y = FT.per_token(y, f["a_bit"])
@@ -106,7 +139,7 @@ class RefUNet:
         quant = f is not None and f["quant"]
         if quant:
             x = self._act(f, x)
-        y = F.conv2d(x, w, self.sd.get(name + ".bias"), stride, padding)
+        y = self.ops.conv2d(x, w, self.sd.get(name + ".bias"), stride, padding)
         if quant:
             y = self._act(f, y)
         return y
@@ -117,10 +150,10 @@ class RefUNet:
         return FT.ACT[f["act"]](x, f["a_bit"])
 
     def gn(self, name, x, groups, eps):
-        return F.group_norm(x, groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)
+        return self.ops.group_norm(x, groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)
 
     def ln(self, name, x):
-        return F.layer_norm(x, (x.shape[-1],), self.sd[name + ".weight"], self.sd[name + ".bias"], 1e-5)
+        return self.ops.layer_norm(x, (x.shape[-1],), self.sd[name + ".weight"], self.sd[name + ".bias"], 1e-5)
 
     # ---- blocks
     def resnet(self, p, x, temb):
@@ -144,7 +177,7 @@ class RefUNet:
         q = q.view(b, -1, heads, d).transpose(1, 2)
         k = k.view(b, -1, heads, d).transpose(1, 2)
         v = v.view(b, -1, heads, d).transpose(1, 2)
-        o = F.scaled_dot_product_attention(q, k, v, dropout_p=0.0, is_causal=False)
+        o = self.ops.scaled_dot_product_attention(q, k, v, dropout_p=0.0, is_causal=False)
         o = o.transpose(1, 2).reshape(b, -1, heads * d).to(q.dtype)
         return self.lin(p + ".to_out.0", o)
 

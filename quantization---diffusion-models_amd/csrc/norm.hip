@@ -376,6 +376,10 @@ extern "C" int qd_timestep_embedding(const float* timesteps, const int* step_idx
 //   eps  = u + g * (c - u)                       pipeline_stable_diffusion.py (CFG)
 //   x0   = (x - sqrt(1 - a_t) * eps) / sqrt(a_t) DDIMScheduler.step
 //   prev = sqrt(a_prev) * x0 + sqrt(1 - a_prev) * eps
+// torch-CPU Half semantics, measured (tests/test_gpu_kernels.py pins them against torch):
+//   python-float * half  -> half(float(g) * x)            (scalar kept in fp32)
+//   0-d fp32 tensor * half -> half(float(half(s)) * x)    (scalar first cast to fp16)
+//   half / 0-d fp32 tensor -> half(x / s)                 (scalar kept in fp32)
 // latents / unet_out are NHWC with c_pad channel stride (only c used); next_in = [x; x].
 // ---------------------------------------------------------------------------------------
 __global__ void k_cfg_ddim(f16* __restrict__ lat, const f16* __restrict__ uo, int b, long l, float g,
@@ -394,12 +398,15 @@ __global__ void k_cfg_ddim(f16* __restrict__ lat, const f16* __restrict__ uo, in
     const f16 diff = (f16)(cc - u);
     const f16 gd = (f16)(g * (float)diff);
     const f16 eps = (f16)(u + (float)gd);
-    const float sb = sqrtf(1.0f - a_t), sa = sqrtf(a_t);
+    const float sb = (float)(f16)sqrtf(1.0f - a_t);   // beta_prod_t ** 0.5 (0-d tensor, cast for *)
+    const float sa = sqrtf(a_t);                      // alpha_prod_t ** 0.5 (divisor, fp32)
     const f16 t1 = (f16)(sb * (float)eps);
     const f16 t2 = (f16)((float)lat[e] - (float)t1);
     const f16 x0 = (f16)((float)t2 / sa);
-    const f16 dir = (f16)(sqrtf(1.0f - a_p) * (float)eps);
-    const f16 t3 = (f16)(sqrtf(a_p) * (float)x0);
+    const float sd = (float)(f16)sqrtf(1.0f - a_p);
+    const float sp = (float)(f16)sqrtf(a_p);
+    const f16 dir = (f16)(sd * (float)eps);
+    const f16 t3 = (f16)(sp * (float)x0);
     out = (f16)((float)t3 + (float)dir);
   } else {
     out = (f16)0.f;

@@ -10,6 +10,7 @@ import ctypes
 import torch
 
 from . import _lib
+from .arena import empty as _empty
 
 GRAN = {"per_token": 0, "per_channel": 1, "per_tensor": 2, "per_group": 3}
 NCHW, NHWC = 0, 1
@@ -48,7 +49,7 @@ def act_fakequant(x, gran, n_bits, layout=NCHW, group=0, out=None):
     per_tensor: any shape.
     """
     _chk(x, "x")
-    y = out if out is not None else torch.empty_like(x)
+    y = out if out is not None else _empty(x.shape, x.dtype, x.device)
     g = GRAN[gran]
     if gran == "per_token":
         c = x.shape[-1]
@@ -56,7 +57,7 @@ def act_fakequant(x, gran, n_bits, layout=NCHW, group=0, out=None):
         ws = None
     elif gran == "per_tensor":
         n, c, h, w = 1, x.numel(), 1, 1
-        ws = torch.empty(1, dtype=torch.float32, device=x.device)
+        ws = _empty((1,), torch.float32, x.device)
     else:
         if x.dim() != 4:
             raise ValueError(f"{gran} activation quant needs a 4-D tensor")
@@ -65,9 +66,9 @@ def act_fakequant(x, gran, n_bits, layout=NCHW, group=0, out=None):
         else:
             n, h, w, c = x.shape
         if gran == "per_channel":
-            ws = torch.empty(n * c, dtype=torch.float32, device=x.device)
+            ws = _empty((n * c,), torch.float32, x.device)
         else:
-            ws = torch.empty(n * c * (h // group) * (w // group), dtype=torch.float32, device=x.device)
+            ws = _empty((n * c * (h // group) * (w // group),), torch.float32, x.device)
     _lib.call("qd_act_fakequant", _p(x), _p(y), layout, n, c, h, w, g, group, n_bits, _p(ws), _stream())
     return y
 
@@ -79,7 +80,7 @@ def act_absmax(x, gran, layout=NHWC, group=0):
             n, c, h, w = x.shape
         else:
             n, h, w, c = x.shape
-        out = torch.empty(n * c, dtype=torch.float32, device=x.device)
+        out = _empty((n * c,), torch.float32, x.device)
     else:
         raise ValueError("act_absmax wrapper supports per_channel only")
     _lib.call("qd_act_absmax", _p(x), layout, n, c, h, w, GRAN[gran], group, _p(out), _stream())
@@ -91,7 +92,7 @@ def act_apply_nhwc(x, amax, n_bits, out=None, c_valid=0):
     c_valid > 0: channels >= c_valid are zero padding and are copied unchanged."""
     _chk(x, "x")
     n, h, w, c = x.shape
-    y = out if out is not None else torch.empty_like(x)
+    y = out if out is not None else _empty(x.shape, x.dtype, x.device)
     _lib.call("qd_act_apply", _p(x), _p(y), NHWC, n, c, h, w, GRAN["per_channel"], c_valid, n_bits, _p(amax),
               _stream())
     return y
@@ -138,7 +139,7 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     M, K = x2d.shape
     N = weight.shape[0]
     if out is None:
-        out = torch.empty(M, N, dtype=torch.float16, device=x2d.device)
+        out = _empty((M, N), torch.float16, x2d.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0)
     if residual is not None:
@@ -160,7 +161,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     H, W = (2 * h, 2 * w) if upsample2x else (h, w)
     ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
     if out is None:
-        out = torch.empty(n, ho, wo, co, dtype=torch.float16, device=x.device)
+        out = _empty((n, ho, wo, co), torch.float16, x.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0)
     _lib.call("qd_conv2d_fwd", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad,
@@ -173,7 +174,7 @@ def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
     _chk(y, "y")
     n, c = y.shape[0], y.shape[-1]
     hw = y.numel() // (n * c)
-    o = out if out is not None else torch.empty_like(y)
+    o = out if out is not None else _empty(y.shape, y.dtype, y.device)
     _lib.call("qd_fq_finalize", _p(y), _p(amax), n, hw, c, n_bits, _p(residual), _p(chan_add), _p(o),
               _stream())
     return o
@@ -187,7 +188,7 @@ def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, o
     c = c1 + (x2.shape[-1] if x2 is not None else 0)
     hw = x.numel() // (n * c1)
     if out is None:
-        out = torch.empty(*x.shape[:-1], c, dtype=torch.float16, device=x.device)
+        out = _empty((*x.shape[:-1], c), torch.float16, x.device)
     _lib.call("qd_groupnorm", _p(x), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma), _p(beta),
               1 if silu else 0, q_bits, _p(out), _stream())
     return out
@@ -197,7 +198,7 @@ def layernorm(x, eps, gamma, beta, out=None):
     _chk(x, "x")
     c = x.shape[-1]
     rows = x.numel() // c
-    o = out if out is not None else torch.empty_like(x)
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
     _lib.call("qd_layernorm", _p(x), rows, c, float(eps), _p(gamma), _p(beta), _p(o), _stream())
     return o
 
@@ -206,14 +207,14 @@ def geglu(h, out=None):
     _chk(h, "h")
     inner = h.shape[-1] // 2
     m = h.numel() // h.shape[-1]
-    o = out if out is not None else torch.empty(*h.shape[:-1], inner, dtype=torch.float16, device=h.device)
+    o = out if out is not None else _empty((*h.shape[:-1], inner), torch.float16, h.device)
     _lib.call("qd_geglu", _p(h), m, inner, _p(o), _stream())
     return o
 
 
 def silu(x, out=None):
     _chk(x, "x")
-    o = out if out is not None else torch.empty_like(x)
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
     _lib.call("qd_silu", _p(x), _p(o), x.numel(), _stream())
     return o
 
@@ -221,7 +222,7 @@ def silu(x, out=None):
 def add(a, b, out=None):
     _chk(a, "a")
     _chk(b, "b")
-    o = out if out is not None else torch.empty_like(a)
+    o = out if out is not None else _empty(a.shape, a.dtype, a.device)
     _lib.call("qd_add", _p(a), _p(b), _p(o), a.numel(), _stream())
     return o
 
@@ -231,7 +232,7 @@ def concat_c(a, b, out=None):
     _chk(b, "b")
     c1, c2 = a.shape[-1], b.shape[-1]
     m = a.numel() // c1
-    o = out if out is not None else torch.empty(*a.shape[:-1], c1 + c2, dtype=torch.float16, device=a.device)
+    o = out if out is not None else _empty((*a.shape[:-1], c1 + c2), torch.float16, a.device)
     _lib.call("qd_concat_c", _p(a), c1, _p(b), c2, m, _p(o), _stream())
     return o
 
@@ -253,7 +254,7 @@ def nhwc_to_nchw(x, c=None):
     _chk(x, "x")
     n, h, w, cp = x.shape
     c = c or cp
-    y = torch.empty(n, c, h, w, dtype=torch.float16, device=x.device)
+    y = _empty((n, c, h, w), torch.float16, x.device)
     _lib.call("qd_nhwc_to_nchw", _p(x), n, c, h * w, cp, _p(y), _stream())
     return y
 
@@ -264,7 +265,7 @@ def attention(q, k, v, heads, out=None, b=None):
     skv = k.shape[1]
     d = c // heads
     if out is None:
-        out = torch.empty(B, sq, c, dtype=torch.float16, device=q.device)
+        out = _empty((B, sq, c), torch.float16, q.device)
     for t, nm in ((q, "q"), (k, "k"), (v, "v")):
         if t.dtype != torch.float16 or not t.is_cuda or t.stride(2) != 1:
             raise ValueError(f"{nm} must be fp16 HIP with unit last stride")
@@ -274,7 +275,7 @@ def attention(q, k, v, heads, out=None, b=None):
 
 
 def timestep_embedding(timesteps_f32, step_idx, b, dim, flip_sin_to_cos=True, shift=0.0, out=None):
-    o = out if out is not None else torch.empty(b, dim, dtype=torch.float16, device=timesteps_f32.device)
+    o = out if out is not None else _empty((b, dim), torch.float16, timesteps_f32.device)
     _lib.call("qd_timestep_embedding", _p(timesteps_f32), _p(step_idx), b, dim, 1 if flip_sin_to_cos else 0,
               float(shift), _p(o), _stream())
     return o

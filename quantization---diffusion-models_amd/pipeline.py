@@ -13,6 +13,7 @@ import zlib
 
 import torch
 
+from . import arena as A
 from . import kernels as K
 from .scheduler import DDIMConfig, ddim_tables
 
@@ -60,6 +61,7 @@ class DenoiseLoop:
         self.ctx_kv = None
         self.graph = None
         self.last_out = None
+        self.arena = A.Arena()
 
     # ---------------------------------------------------------------- inputs
     @torch.no_grad()
@@ -85,12 +87,14 @@ class DenoiseLoop:
 
     # ---------------------------------------------------------------- one step
     @torch.no_grad()
-    def step(self):
-        K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
-                             shift=float(self.unet.config.freq_shift), out=self.temb_in)
-        out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
-        K.cfg_ddim_step(self.lat, out, self.guidance, self.a_t, self.a_p, self.step_idx, self.next_in,
-                        c=self.cin)
+    def step(self, frozen=False):
+        """One denoising step; every intermediate comes from the loop's static arena."""
+        with A.using(self.arena, frozen=frozen):
+            K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
+                                 shift=float(self.unet.config.freq_shift), out=self.temb_in)
+            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
+            K.cfg_ddim_step(self.lat, out, self.guidance, self.a_t, self.a_p, self.step_idx, self.next_in,
+                            c=self.cin)
         self.last_out = out
         return out
 
@@ -107,7 +111,7 @@ class DenoiseLoop:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.step()
+            self.step(frozen=True)   # no allocation may happen inside the capture
         self.graph = g
 
     @torch.no_grad()

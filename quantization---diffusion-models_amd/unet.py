@@ -373,7 +373,7 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
     if q:
         n = x.shape[0]
-        amax = torch.empty(n * wk.shape[0], dtype=torch.float32, device=x.device)
+        amax = K._empty((n * wk.shape[0],), torch.float32, x.device)
         y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax)
         return K.fq_finalize(y, amax, q, residual=residual, chan_add=chan_add, out=y)
     if chan_add is None:

@@ -12,6 +12,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
+    config.addinivalue_line("markers", "slow: full-size (SD1.5) parity case, minutes of CPU oracle time")
 
 
 @pytest.fixture(scope="session")

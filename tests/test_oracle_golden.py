@@ -27,6 +27,19 @@ def test_weight_group_np(golden):
         assert same_bits(FQ.quantize_weight_absmax(g[k + "_in"], _bits(k), gs), g[k + "_out"]), k
 
 
+def test_weight_torch_backend(golden):
+    g = golden["fake_quant_golden"]
+    for k in [k[:-3] for k in g.files if k.endswith("_in") and k.startswith(("wgroup", "wpc", "wpt"))]:
+        w = torch.from_numpy(g[k + "_in"])
+        if k.startswith("wgroup"):
+            out = FT.weight_group(w, _bits(k), 0 if k.startswith("wgroup0") else 128)
+        elif k.startswith("wpc"):
+            out = FT.weight_per_channel(w, _bits(k))
+        else:
+            out = FT.weight_per_tensor(w, _bits(k))
+        assert same_bits(out.numpy(), g[k + "_out"]), k
+
+
 def test_weight_per_channel_and_tensor_np(golden):
     g = golden["fake_quant_golden"]
     for k in [k[:-3] for k in g.files if k.endswith("_in") and (k.startswith("wpc") or k.startswith("wpt"))]:
@@ -145,6 +158,9 @@ def test_install_decisions(golden):
                     ("w4a16qa0", dict(w_bit=4, a_bit=16, quantize_act=False))):
         orig = {k.split("|", 1)[1]: torch.from_numpy(g[k]) for k in g.files if k.startswith(tag + "_orig|")}
         qsd, flags = quantize_state_dict(orig, dict(qc, q_group_size=128))
+        qsd_np, _ = quantize_state_dict(orig, dict(qc, q_group_size=128), backend="numpy")
+        for key in qsd:
+            assert same_bits(qsd[key].numpy(), qsd_np[key].numpy()), key
         layers = {row.split("|")[0]: row.split("|") for row in g[tag + "_layers"]}
         assert set(layers) == set(flags)
         for name, (_, kind, oq) in layers.items():
