@@ -73,3 +73,8 @@ __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erf
   } while (0)
 
 extern "C" int qd_set_error(int code, const char* msg);
+
+// Zero an fp32 workspace with a kernel node, never hipMemsetAsync: memset nodes captured into a
+// hipGraph were observed (ROCm 7.x runtime bundled with torch) to race with the following
+// kernel on replay, leaving atomic-max targets unzeroed/zeroed late ("graph capture").
+void qd_zero_f32(float* p, size_t n, hipStream_t st);

@@ -413,7 +413,7 @@ extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "x must be 16-B aligned");
   if (M == 0) return 0;
   if (epi & QD_EPI_AMAX)  // amax is zeroed by the call (stream-ordered, graph-capturable)
-    (void)hipMemsetAsync(amax, 0, sizeof(float) * (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
+    qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
   launch_gemm<AM_LINEAR>(p, wfmt, S(stream));
   QD_CHECK_LAUNCH();
   return 0;
@@ -458,7 +458,7 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "x must be 16-B aligned");
   if (p.M == 0) return 0;
   if (epi & QD_EPI_AMAX)  // amax is zeroed by the call (stream-ordered, graph-capturable)
-    (void)hipMemsetAsync(amax, 0, sizeof(float) * (size_t)n * co, S(stream));
+    qd_zero_f32(amax, (size_t)n * co, S(stream));
   launch_gemm<AM_CONV>(p, QD_WFMT_F16, S(stream));
   QD_CHECK_LAUNCH();
   return 0;

@@ -30,6 +30,16 @@ extern "C" int qd_device_arch(char* buf, int len) {
 }
 
 static inline int qmax_of(int bits) { return (1 << (bits - 1)) - 1; }
+
+__global__ void k_zero_f32(float* __restrict__ p, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = 0.f;
+}
+
+void qd_zero_f32(float* p, size_t n, hipStream_t st) {
+  if (n == 0) return;
+  k_zero_f32<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(p, n);
+}
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------------------------------
@@ -185,7 +195,7 @@ static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, 
                          float* amax, hipStream_t st) {
   const long hw = (long)h * w;
   if (gran == QD_GRAN_PER_CHANNEL) {
-    (void)hipMemsetAsync(amax, 0, sizeof(float) * n * c, st);
+    qd_zero_f32(amax, (size_t)n * c, st);
     if (layout == QD_LAYOUT_NHWC) {
       QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
       const int chunks = c / 8;
@@ -201,7 +211,7 @@ static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, 
     const long rows = (long)n * hw;  // rows of length c (caller passes h = w = 1 normally)
     k_rowmax<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, rows, c, amax);
   } else if (gran == QD_GRAN_PER_TENSOR) {
-    (void)hipMemsetAsync(amax, 0, sizeof(float), st);
+    qd_zero_f32(amax, 1, st);
     const long count = (long)n * c * hw;
     k_tensormax<<<(int)std::min<long>(2048, grid1(count)), 256, 0, st>>>((const f16*)x, count, amax);
   } else if (gran == QD_GRAN_PER_GROUP) {
@@ -332,7 +342,7 @@ extern "C" int qd_weight_quant(const void* w, int rows, int cols, int group, int
     float* ws = nullptr;
     hipError_t e = hipMallocAsync((void**)&ws, sizeof(float), st);
     if (e != hipSuccess) return qd_set_error((int)e, "workspace alloc");
-    (void)hipMemsetAsync(ws, 0, sizeof(float), st);
+    qd_zero_f32(ws, 1, st);
     k_tensormax<<<(int)std::min<long>(2048, grid1(count)), 256, 0, st>>>((const f16*)w, count, ws);
     k_weight_tensor_apply<<<grid1(count), 256, 0, st>>>((const f16*)w, count, qmax_of(n_bits), ws,
                                                         codes, (f16*)scales, (f16*)w_dq);
@@ -497,7 +507,7 @@ extern "C" int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const i
   QD_REQUIRE(ln_w && fc_w && fc_rows && act_mean && wmax_ws && scales_out, "null pointer");
   QD_REQUIRE(nfc > 0 && c > 0, "bad shape");
   hipStream_t st = S(stream);
-  (void)hipMemsetAsync(wmax_ws, 0, sizeof(float) * c, st);
+  qd_zero_f32(wmax_ws, (size_t)c, st);
   for (int i = 0; i < nfc; ++i) {
     QD_REQUIRE(fc_w[i] && fc_rows[i] > 0, "bad fc");
     dim3 grid((c + 255) / 256, (fc_rows[i] + 63) / 64);
