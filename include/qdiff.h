@@ -117,11 +117,14 @@ int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n
 /* ---------------- normalisation / activations (diffusers UNet ops, fp16 I/O) --------- */
 /* GroupNorm(groups, eps, affine) on NHWC [N, HW, C] (+ SiLU) (+ per-(n, c) fake-quant of the
  * result with q_bits, i.e. the input quant of the conv that consumes it, fused because a
- * workgroup owns a whole (n, group) slab).  x may be two tensors concatenated along C:
- * x2 != NULL -> channels [0, c1) from x (row stride c1), [c1, c) from x2 (row stride c - c1). */
+ * per-(n, c) amax is reduced deterministically across the slab's row chunks).  x may be two
+ * tensors concatenated along C: x2 != NULL -> channels [0, c1) from x (row stride c1), [c1, c)
+ * from x2 (row stride c - c1); c1 and c multiples of 8.  ws: qd_groupnorm_workspace() fp32. */
 int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
                  float eps, const void* gamma, const void* beta, int silu, int q_bits,
-                 void* y, void* stream);
+                 void* y, float* ws, void* stream);
+/* fp32 elements of the qd_groupnorm workspace for this shape. */
+int qd_groupnorm_workspace(int n, int hw, int c, int groups);
 /* LayerNorm over the last dim C of [rows, C]. */
 int qd_layernorm(const void* x, int rows, int c, float eps, const void* gamma, const void* beta,
                  void* y, void* stream);

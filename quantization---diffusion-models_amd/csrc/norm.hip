@@ -12,137 +12,186 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 static int grid1(long count, int per_block = 256) { return (int)((count + per_block - 1) / per_block); }
 
 // ---------------------------------------------------------------------------------------
-// GroupNorm on NHWC [N, HW, C] with an optional second source for channels [c1, C).
-// One 256-thread workgroup per (n, group).  Thread t owns channel pair p = t % P (P = cg/2) and
-// visits rows t/P, t/P + R, ... (R = 256 / P), so per-channel amax stays in registers.
-// Passes: mean, variance (two-pass, fp32), then [amax of the final fp16 output], then write.
+// GroupNorm on NHWC [N, HW, C] (+ SiLU) (+ fused per-(n,c) fake-quant of the output), with an
+// optional second source for channels [c1, C) (the UNet's skip concat, never materialised).
+//
+// Four stream-ordered kernels, all deterministic (fixed-order reductions, max is exact):
+//   1. k_gn_stats   grid (n*G, S): slab chunk -> shifted partial sums (s1, s2) per block
+//   2. k_gn_coeff   per (n, c): mean / rstd from the S partials (fixed order) ->
+//                   scale = rstd*gamma, bias = beta - scale*mean  (torch CPU GroupNorm form)
+//   3. k_gn_amax    [q_bits] grid (n*G, S): per-channel max |fq input| over the chunk's rows
+//                   (the input quant of the consuming conv: fake_quant.py:125 reduction)
+//   4. k_gn_apply   elementwise, 8 channels (16 B) per thread: y = fq(silu(half(x*a + b)))
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ const f16* gn_src(const f16* x, const f16* x2, int c1, int c, long row,
                                              int ch) {
   return ch < c1 ? x + row * c1 + ch : x2 + row * (c - c1) + (ch - c1);
 }
 
-__global__ void __launch_bounds__(256) k_groupnorm(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                   int c1, int hw, int c, int groups, float eps,
-                                                   const f16* __restrict__ gamma,
-                                                   const f16* __restrict__ beta, int silu, int qmax,
-                                                   f16* __restrict__ y) {
+static int gn_splits(long slabs, int hw) {
+  int s = 1;
+  while (slabs * s < 2048 && hw / (s * 2) >= 16) s *= 2;
+  return s;
+}
+
+// thread t: channel pair p = t % P of the group, rows r0 = t / P, stride R = 256 / P
+__global__ void __launch_bounds__(256) k_gn_stats(const f16* __restrict__ x, const f16* __restrict__ x2,
+                                                  int c1, int hw, int c, int groups, int S,
+                                                  float* __restrict__ part) {
   __shared__ float red[8];
-  __shared__ float chmax[256];
-  const int n = blockIdx.x / groups;
-  const int g = blockIdx.x % groups;
-  const int cg = c / groups;
-  const int P = cg >> 1;
-  const int R = 256 / P;
+  const int slab = blockIdx.x;  // n * groups + g
+  const int n = slab / groups, g = slab % groups;
+  const int cg = c / groups, P = cg >> 1, R = 256 / P;
   const int t = threadIdx.x;
-  const bool active = t < P * R;
-  const int p = t % P;
-  const int r0 = t / P;
-  const int ch = g * cg + 2 * p;
+  const int rows = (hw + S - 1) / S;
+  const int ra = blockIdx.y * rows, rb = min(hw, ra + rows);
   const long rowbase = (long)n * hw;
-
-  // pass 1: mean
-  float s = 0.f;
-  if (active)
-    for (int r = r0; r < hw; r += R) {
+  const float x0 = (float)*gn_src(x, x2, c1, c, rowbase, g * cg);  // shift (same for all S blocks)
+  float s1 = 0.f, s2 = 0.f;
+  if (t < P * R) {
+    const int ch = g * cg + 2 * (t % P);
+    for (int r = ra + t / P; r < rb; r += R) {
       const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
-      s += (float)__low2float(v) + (float)__high2float(v);
+      const float a = __low2float(v) - x0, b = __high2float(v) - x0;
+      s1 += a + b;
+      s2 += a * a + b * b;
     }
-  s = wave_sum(s);
-  if ((t & 63) == 0) red[t >> 6] = s;
-  __syncthreads();
-  const float cnt = (float)cg * (float)hw;
-  const float mean = (red[0] + red[1] + red[2] + red[3]) / cnt;
-  __syncthreads();
-  // pass 2: variance (population)
-  float v2 = 0.f;
-  if (active)
-    for (int r = r0; r < hw; r += R) {
-      const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
-      const float a = __low2float(v) - mean, b = __high2float(v) - mean;
-      v2 += a * a + b * b;
-    }
-  v2 = wave_sum(v2);
-  if ((t & 63) == 0) red[4 + (t >> 6)] = v2;
-  __syncthreads();
-  const float var = (red[4] + red[5] + red[6] + red[7]) / cnt;
-  const float rstd = 1.0f / sqrtf(var + eps);
-  const float sc0 = rstd * (float)gamma[ch], sc1 = rstd * (float)gamma[ch + 1];
-  const float bi0 = fmaf(-sc0, mean, (float)beta[ch]), bi1 = fmaf(-sc1, mean, (float)beta[ch + 1]);
-
-  auto out_val = [&](float xv, float sc, float bi) -> float {
-    f16 o = (f16)fmaf(xv, sc, bi);
-    if (silu) o = (f16)silu_f((float)o);
-    return (float)o;
-  };
-
-  float s0 = 0.f, s1 = 0.f;
-  if (qmax > 0) {
-    // pass 3: per-channel amax of the rounded output (fake_quant.py:125 reduction)
-    float m0 = 0.f, m1 = 0.f;
-    if (active)
-      for (int r = r0; r < hw; r += R) {
-        const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
-        m0 = fmaxf(m0, fabsf(out_val(__low2float(v), sc0, bi0)));
-        m1 = fmaxf(m1, fabsf(out_val(__high2float(v), sc1, bi1)));
-      }
-    // reduce over the R row-lanes sharing a pair: through LDS
-    chmax[t] = m0;
-    __syncthreads();
-    if (t < P) {
-      float m = 0.f;
-      for (int i = 0; i < R; ++i) m = fmaxf(m, chmax[t + i * P]);
-      chmax[t] = m;  // slot t < P now holds channel 2t's amax
-    }
-    __syncthreads();
-    const float a0 = chmax[p];
-    __syncthreads();
-    chmax[t] = m1;
-    __syncthreads();
-    if (t < P) {
-      float m = 0.f;
-      for (int i = 0; i < R; ++i) m = fmaxf(m, chmax[t + i * P]);
-      chmax[t] = m;
-    }
-    __syncthreads();
-    const float a1 = chmax[p];
-    s0 = fq_scale(a0, qmax);
-    s1 = fq_scale(a1, qmax);
   }
-  // pass 4: write
-  if (active)
-    for (int r = r0; r < hw; r += R) {
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if ((t & 63) == 0) {
+    red[t >> 6] = s1;
+    red[4 + (t >> 6)] = s2;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float* o = part + ((long)slab * S + blockIdx.y) * 3;
+    o[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    o[1] = (red[4] + red[5]) + (red[6] + red[7]);
+    o[2] = x0;
+  }
+}
+
+__global__ void k_gn_coeff(const float* __restrict__ part, int n, int hw, int c, int groups, int S, float eps,
+                           const f16* __restrict__ gamma, const f16* __restrict__ beta,
+                           float2* __restrict__ coef) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * c) return;
+  const int ni = i / c, ch = i % c;
+  const int cg = c / groups, g = ch / cg;
+  const float* p = part + ((long)(ni * groups + g) * S) * 3;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < S; ++k) {
+    s1 += p[3 * k];
+    s2 += p[3 * k + 1];
+  }
+  const float cnt = (float)cg * (float)hw;
+  const float m = s1 / cnt;                          // mean of the shifted values
+  const float var = fmaxf(s2 / cnt - m * m, 0.f);    // population variance
+  const float mean = m + p[2];
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const float sc = rstd * (float)gamma[ch];
+  coef[i] = make_float2(sc, fmaf(-sc, mean, (float)beta[ch]));
+}
+
+__device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
+  f16 o = (f16)fmaf(xv, k.x, k.y);
+  if (silu) o = (f16)silu_f((float)o);
+  return (float)o;
+}
+
+__global__ void __launch_bounds__(256) k_gn_amax(const f16* __restrict__ x, const f16* __restrict__ x2,
+                                                 int c1, int hw, int c, int groups, int S,
+                                                 const float2* __restrict__ coef, int silu,
+                                                 float* __restrict__ amax) {
+  __shared__ float red[2][256];
+  const int slab = blockIdx.x;
+  const int n = slab / groups, g = slab % groups;
+  const int cg = c / groups, P = cg >> 1, R = 256 / P;
+  const int t = threadIdx.x;
+  const int rows = (hw + S - 1) / S;
+  const int ra = blockIdx.y * rows, rb = min(hw, ra + rows);
+  const long rowbase = (long)n * hw;
+  float m0 = 0.f, m1 = 0.f;
+  const int ch = g * cg + 2 * (t % P);
+  if (t < P * R) {
+    const float2 k0 = coef[(long)n * c + ch], k1 = coef[(long)n * c + ch + 1];
+    for (int r = ra + t / P; r < rb; r += R) {
       const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
-      float o0 = out_val(__low2float(v), sc0, bi0);
-      float o1 = out_val(__high2float(v), sc1, bi1);
-      f16 h0, h1;
-      if (qmax > 0) {
-        h0 = fq_apply(o0, s0);
-        h1 = fq_apply(o1, s1);
-      } else {
-        h0 = (f16)o0;
-        h1 = (f16)o1;
-      }
-      f16* dst = y + (rowbase + r) * c + ch;
-      dst[0] = h0;
-      dst[1] = h1;
+      m0 = fmaxf(m0, fabsf(gn_out(__low2float(v), k0, silu)));
+      m1 = fmaxf(m1, fabsf(gn_out(__high2float(v), k1, silu)));
     }
+  }
+  red[0][t] = m0;
+  red[1][t] = m1;
+  __syncthreads();
+  if (t < P) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < R; ++i) {
+      a = fmaxf(a, red[0][t + i * P]);
+      b = fmaxf(b, red[1][t + i * P]);
+    }
+    atomic_max_pos(&amax[(long)n * c + ch], a);
+    atomic_max_pos(&amax[(long)n * c + ch + 1], b);
+  }
+}
+
+// 8 channels per thread; the two sources are both multiples of 8 channels wide (host check).
+__global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, const f16* __restrict__ x2,
+                                                  int c1, long count8, int hw, int c,
+                                                  const float2* __restrict__ coef, int silu, int qmax,
+                                                  const float* __restrict__ amax, f16* __restrict__ y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count8) return;
+  const long e = i * 8;
+  const int ch = (int)(e % c);
+  const long row = e / c;
+  const long n = row / hw;
+  const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, row, ch));
+  const float2* k = coef + n * c + ch;
+  f16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float val = gn_out((float)v[j], k[j], silu);
+    o[j] = qmax > 0 ? fq_apply(val, fq_scale(amax[n * c + ch + j], qmax)) : (f16)val;
+  }
+  *reinterpret_cast<f16x8*>(y + e) = o;
+}
+
+extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
+  const int S = gn_splits((long)n * groups, hw);
+  return n * groups * S * 3 + 1 + 3 * n * c;  // partials, float2 alignment pad, coef, amax
 }
 
 extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
                             float eps, const void* gamma, const void* beta, int silu, int q_bits,
-                            void* y, void* stream) {
-  QD_REQUIRE(x && gamma && beta && y, "null pointer");
+                            void* y, float* ws, void* stream) {
+  QD_REQUIRE(x && gamma && beta && y && ws, "null pointer");
   QD_REQUIRE(groups > 0 && c % groups == 0, "groups must divide C");
   const int cg = c / groups;
   QD_REQUIRE(cg % 2 == 0 && cg <= 512, "channels per group must be even and <= 512");
-  if (x2) QD_REQUIRE(c1 % 2 == 0 && c1 > 0 && c1 < c, "bad concat split");
+  QD_REQUIRE(c % 8 == 0, "GroupNorm needs C % 8 == 0");
+  if (x2) QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c, "bad concat split (must be a multiple of 8)");
   else c1 = c;
   QD_REQUIRE(q_bits == 0 || (q_bits >= 2 && q_bits <= 16), "bad q_bits");
   if ((long)n * hw == 0) return 0;
-  k_groupnorm<<<n * groups, 256, 0, S(stream)>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, eps,
-                                                 (const f16*)gamma, (const f16*)beta, silu,
-                                                 q_bits ? (1 << (q_bits - 1)) - 1 : 0, (f16*)y);
+  hipStream_t st = S(stream);
+  const int S_ = gn_splits((long)n * groups, hw);
+  float* part = ws;
+  float2* coef = reinterpret_cast<float2*>(ws + (long)n * groups * S_ * 3 + ((n * groups * S_ * 3) & 1));
+  float* amax = reinterpret_cast<float*>(coef + (long)n * c);
+  dim3 sg(n * groups, S_);
+  k_gn_stats<<<sg, 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, S_, part);
+  k_gn_coeff<<<grid1((long)n * c), 256, 0, st>>>(part, n, hw, c, groups, S_, eps, (const f16*)gamma,
+                                                 (const f16*)beta, coef);
+  const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
+  if (qmax) {
+    qd_zero_f32(amax, (size_t)n * c, st);
+    k_gn_amax<<<sg, 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, S_, coef, silu, amax);
+  }
+  const long count8 = (long)n * hw * c / 8;
+  k_gn_apply<<<grid1(count8), 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, count8, hw, c, coef, silu, qmax,
+                                            amax, (f16*)y);
   QD_CHECK_LAUNCH();
   return 0;
 }

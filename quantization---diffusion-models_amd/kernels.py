@@ -189,8 +189,10 @@ def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, o
     hw = x.numel() // (n * c1)
     if out is None:
         out = _empty((*x.shape[:-1], c), torch.float16, x.device)
+    wsn = _lib.load().qd_groupnorm_workspace(n, hw, c, groups)
+    ws = _empty((wsn,), torch.float32, x.device)
     _lib.call("qd_groupnorm", _p(x), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma), _p(beta),
-              1 if silu else 0, q_bits, _p(out), _stream())
+              1 if silu else 0, q_bits, _p(out), _p(ws), _stream())
     return out
 
 
