@@ -95,7 +95,12 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
                   const void* wscale, int group, const void* bias, const void* residual,
                   void* y, int N, int ldy, int epi, float* amax, int rows_per_sample,
-                  void* stream);
+                  float* ws, long ws_elems, void* stream);
+
+/* fp32 elements of split-K workspace the GEMM plans for this shape (0: runs unsplit).  Pass
+ * at least that much as (ws, ws_elems) to qd_linear_fwd / qd_conv2d_fwd (conv: M = N*Ho*Wo,
+ * K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo); with less (or NULL) the call runs unsplit. */
+long qd_gemm_workspace(int M, int N, int K, int wfmt, int rows_per_sample, int epi);
 
 /* NHWC implicit-GEMM Conv2d: y[N, Ho, Wo, Co] = conv(x[N, H, W, Ci], W[Co][kh][kw][Ci_pad]).
  * WxAxConv2d.forward's F.conv2d (fake_quant.py:339); groups = dilation = 1.
@@ -105,7 +110,8 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
  * the rounded output into amax[N][Co] (zeroed by the call). */
 int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co,
                   int kh, int kw, int stride, int pad, int upsample2x, const void* bias,
-                  const void* residual, void* y, int epi, float* amax, void* stream);
+                  const void* residual, void* y, int epi, float* amax, float* ws, long ws_elems,
+                  void* stream);
 
 /* Conv output fake-quant + fused adds (the q_y = output_quant(y) of fake_quant.py:340 followed
  * by the diffusers residual / temb add): out = half(fq(y; amax[n][c]) + res) with res either a

@@ -27,11 +27,10 @@ SIGNATURES = {
     "qd_weight_quant": [P, I, I, I, I, P, P, P, P],
     "qd_pack_int4": [P, I, I, P, P],
     "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
-    "qd_linear_fwd": [P, I, I, I, P, I, P, I, P, P, P, I, I, I, P, I, P],
-    "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P],
+    "qd_linear_fwd": [P, I, I, I, P, I, P, I, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
+    "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, P, P],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
-    "qd_groupnorm_workspace": [I, I, I, I],
     "qd_layernorm": [P, I, I, F, P, P, P, P],
     "qd_geglu": [P, I, I, P, P],
     "qd_silu": [P, P, I64, P],
@@ -44,6 +43,12 @@ SIGNATURES = {
     "qd_cfg_ddim_step": [P, P, I, I64, F, P, P, P, P, I, I, P],
     "qd_channel_absmax_accum": [P, I64, I, P, P, P, P],
     "qd_smooth_fold": [P, P, P, P, I, I, P, F, P, P, P],
+}
+
+# size queries (no status code)
+QUERIES = {
+    "qd_gemm_workspace": ([I, I, I, I, I, I], ctypes.c_long),
+    "qd_groupnorm_workspace": ([I, I, I, I], I),
 }
 
 _lib = None
@@ -70,6 +75,10 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = I
+    for name, (argtypes, restype) in QUERIES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
     lib.qd_last_error.argtypes = []
     lib.qd_last_error.restype = ctypes.c_char_p
     _lib = lib
@@ -87,4 +96,4 @@ def call(name, *args):
 
 
 def exported_symbols():
-    return list(SIGNATURES) + ["qd_last_error"]
+    return list(SIGNATURES) + list(QUERIES) + ["qd_last_error"]

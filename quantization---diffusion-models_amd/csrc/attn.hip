@@ -16,156 +16,246 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 
 constexpr int KV_T = 64;
 
-__device__ __forceinline__ int kswz(int row, int chunk, int rowchunks) {
-  // XOR the low 3 bits of the chunk index (rows hold a multiple of 8 chunks)
-  return row * rowchunks * 8 + (((chunk & ~7) | ((chunk & 7) ^ (row & 7))) << 3);
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// V^T fragment through the gfx950 LDS transpose read: each 16-lane group gathers a 4-row x
+// 16-column block of the row-major V tile and lane i receives column i (one head-dim index)
+// of the 4 rows (4 consecutive keys).
+__device__ __forceinline__ f16x4 tr_read(const f16* p) {
+  s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  return __builtin_bit_cast(f16x4, r);
 }
 
-template <int DP, int DV>  // DP: head dim padded to 32 (QK^T K-dim); DV: head dim padded to 16
+// LDS row stride (elements) of the row-major V tile: an odd multiple of 8 dwords, so the
+// 8 consecutive rows one 32-lane half reads with ds_read_b64_tr_b16 hit 8 disjoint bank octets.
+constexpr int v_stride(int dv) { return ((dv / 2 / 8) & 1) ? dv : dv + 16; }
+
+// Swapped-operand flash attention (S^T = K Q^T, O^T = V^T P^T), 16x16x32 f16 MFMA.
+//   * 4 waves x 16 queries; a lane owns ONE query (column lane&15 of every accumulator), so
+//     the softmax row max is 16 in-register maxes + 2 cross-group shuffles and the
+//     online-softmax rescale is one scalar per lane, skipped (wave-uniformly) whenever no
+//     lane's running max grew.
+//   * P^T leaves the S^T accumulator straight into the B operand of the PV MFMA (k order
+//     permuted to the accumulator's: kv = 32s + 16(j>>2) + 4g + (j&3)); V^T comes from the
+//     row-major V tile with ds_read_b64_tr_b16 in that same k order.  P never touches LDS.
+//   * The softmax denominator rides in the PV MFMA: V tile column d (head-dim padding,
+//     DV > d) holds 1.0, so O^T row d accumulates sum(P) with the same fp16 P and the same
+//     rescales as the numerator - no per-element VALU sum.
+//   * K/V tiles register-staged and double-buffered in LDS (tile loop unrolled x2 so every
+//     LDS address is a per-lane base + immediate); the next tile's loads are in flight while
+//     the current one is computed; one barrier per tile.
+template <int DP, int DV, int NB>
 __global__ void __launch_bounds__(256) k_attn(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                               int ldk, const f16* __restrict__ v, int ldv,
                                               f16* __restrict__ o, int ldo, int heads, int sq, int skv,
                                               int d, float scale_log2) {
-  constexpr int KCH = (DP / 8 + 7) / 8 * 8;  // chunks per K row in LDS (multiple of 8)
-  constexpr int TNO = DV / 16;
-  __shared__ f16 ks[KV_T * KCH * 8];
-  __shared__ f16 vt[DV * KV_T];
-  __shared__ f16 ps[4][16 * KV_T];
+  constexpr int KCH = DP / 8;                  // 16-B chunks per K row (QK^T depth DP)
+  constexpr int KCHP = (KCH + 7) / 8 * 8;      // padded so the XOR swizzle stays in the row
+  constexpr int VST = v_stride(DV);
+  constexpr int KSZ = KV_T * KCHP * 8, VSZ = KV_T * VST;
+  constexpr int VCH = DV / 8;
+  constexpr int NKL = (KV_T * KCH + 255) / 256, NVL = (KV_T * VCH + 255) / 256;
+  constexpr int TD = DV / 16;
+  __shared__ __attribute__((aligned(16))) f16 smem[NB * (KSZ + VSZ)];
 
   const int bh = blockIdx.y;
   const int b = bh / heads, h = bh % heads;
   const int q0 = blockIdx.x * 64;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
 
   const f16* qb = q + (long)b * sq * ldq + h * d;
   const f16* kb = k + (long)b * skv * ldk + h * d;
   const f16* vb = v + (long)b * skv * ldv + h * d;
   f16* ob = o + (long)b * sq * ldo + h * d;
+  const int dchunks = d >> 3;
 
-  // Q fragments: row q0 + wid*16 + fr, d = ks*32 + 8*fq .. +8
+  // B operand of S^T: Q[q = q0 + 16*wid + fr][dd = 32s + 8fq .. +8]
   f16x8 qf[DP / 32];
   {
     const int qrow = q0 + wid * 16 + fr;
 #pragma unroll
     for (int s = 0; s < DP / 32; ++s) {
-      const int dd = s * 32 + 8 * fq;
+      const int c = s * 4 + fq;
       f16x8 val = {};
-      if (qrow < sq && dd < d) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + dd);
+      if (qrow < sq && c < dchunks) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + c * 8);
       qf[s] = val;
     }
   }
 
-  f32x4 oacc[TNO];
-#pragma unroll
-  for (int j = 0; j < TNO; ++j) oacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float mrow[4], lrow[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    mrow[r] = -INFINITY;
-    lrow[r] = 0.f;
+  // Padding of both tile buffers, written once: K chunks >= d/8 are zero; V columns >= d are
+  // zero except column d = 1.0 (the denominator row of O^T).  Tile stores never touch them.
+  for (int i = tid; i < NB * KV_T * KCHP; i += 256) {
+    const int bf = i / (KV_T * KCHP), row = (i / KCHP) % KV_T, c = i % KCHP;
+    if (c >= dchunks) *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + ((c ^ (row & 7)) << 3)) = f16x8{};
+  }
+  for (int i = tid; i < NB * KV_T * (VST - d); i += 256) {
+    const int bf = i / (KV_T * (VST - d)), row = (i / (VST - d)) % KV_T, col = d + i % (VST - d);
+    smem[bf * (KSZ + VSZ) + KSZ + row * VST + col] = (f16)(col == d ? 1.0f : 0.0f);
   }
 
-  const int dchunks = d / 8;  // d % 8 == 0
-  for (int kv0 = 0; kv0 < skv; kv0 += KV_T) {
-    __syncthreads();  // previous tile fully consumed
-    // ---- stage K [64][KCH*8] (zero-padded) and V^T [DV][64] ----
-    for (int i = threadIdx.x; i < KV_T * KCH; i += 256) {
-      const int row = i / KCH, c = i % KCH;
-      f16x8 val = {};
-      if (kv0 + row < skv && c < dchunks) val = *reinterpret_cast<const f16x8*>(kb + (long)(kv0 + row) * ldk + c * 8);
-      *reinterpret_cast<f16x8*>(ks + kswz(row, c, KCH)) = val;
-    }
-    for (int i = threadIdx.x; i < KV_T * (DV / 8); i += 256) {
-      const int row = i / (DV / 8), c = i % (DV / 8);  // row = kv, c = d chunk
-      f16x8 val = {};
-      if (kv0 + row < skv && c < dchunks) val = *reinterpret_cast<const f16x8*>(vb + (long)(kv0 + row) * ldv + c * 8);
+  // K/V tile loads: raw buffer loads; rows past skv fall off the end of the buffer and read 0.
+  const unsigned kbytes = (unsigned)(((long)(skv - 1) * ldk + d) * 2);
+  const unsigned vbytes = (unsigned)(((long)(skv - 1) * ldv + d) * 2);
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kb, 0, kbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vb, 0, vbytes, 0x00020000);
+  unsigned koff[NKL], voff[NVL];
+  int kdst[NKL], vdst[NVL];  // LDS element offset within a buffer, -1 = padding chunk (skip)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int dd = c * 8 + e;  // V^T row
-        vt[dd * KV_T + ((((row >> 3) ^ (dd & 7)) << 3) | (row & 7))] = val[e];
-      }
-    }
-    __syncthreads();
+  for (int i = 0; i < NKL; ++i) {
+    const int e = tid + i * 256, row = e / KCH, c = e % KCH;
+    const bool ok = e < KV_T * KCH && c < dchunks;
+    koff[i] = (unsigned)(row * ldk + c * 8) * 2u;
+    kdst[i] = ok ? row * KCHP * 8 + ((c ^ (row & 7)) << 3) : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < NVL; ++i) {
+    const int e = tid + i * 256, row = e / VCH, c = e % VCH;
+    const bool ok = e < KV_T * VCH && c < dchunks;
+    voff[i] = (unsigned)(row * ldv + c * 8) * 2u;
+    vdst[i] = ok ? KSZ + row * VST + c * 8 : -1;
+  }
+  f16x8 kst[NKL], vst[NVL];
+  auto load_tile = [&](int kv0) {
+    const unsigned ks0 = (unsigned)(kv0 * ldk) * 2u, vs0 = (unsigned)(kv0 * ldv) * 2u;
+#pragma unroll
+    for (int i = 0; i < NKL; ++i)
+      kst[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, (int)(koff[i] + ks0), 0, 0));
+#pragma unroll
+    for (int i = 0; i < NVL; ++i)
+      vst[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, (int)(voff[i] + vs0), 0, 0));
+  };
+  auto store_tile = [&](f16* base) {
+#pragma unroll
+    for (int i = 0; i < NKL; ++i)
+      if (kdst[i] >= 0) *reinterpret_cast<f16x8*>(base + kdst[i]) = kst[i];
+#pragma unroll
+    for (int i = 0; i < NVL; ++i)
+      if (vdst[i] >= 0) *reinterpret_cast<f16x8*>(base + vdst[i]) = vst[i];
+  };
 
-    // ---- S = Q K^T (16 x 64 per wave) ----
+  f32x4 oacc[TD];
+#pragma unroll
+  for (int j = 0; j < TD; ++j) oacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float mrow = -INFINITY;  // running max of this lane's query (log2 domain)
+
+  // per-lane LDS read offsets (elements, within a buffer)
+  int kread[4][DP / 32];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < DP / 32; ++s) {
+      const int row = j * 16 + fr, c = s * 4 + fq;
+      kread[j][s] = row * KCHP * 8 + ((c ^ (row & 7)) << 3);
+    }
+  const int vread = KSZ + (fq * 4 + (fr >> 2)) * VST + (fr & 3) * 4;
+
+  const int ntiles = (skv + KV_T - 1) / KV_T;
+  auto tile = [&](const f16* ks, int kv0) {
+    // ---- S^T[kv][q] = K Q^T: tile jt holds kv = 16jt + 4fq + r for query fr ----
     f32x4 sacc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) sacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < DP / 32; ++s) {
+    for (int s = 0; s < DP / 32; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const f16x8 kf = *reinterpret_cast<const f16x8*>(ks + kswz(j * 16 + fr, s * 4 + fq, KCH));
-        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[s], kf, sacc[j], 0, 0, 0);
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(ks + kread[j][s]);
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], sacc[j], 0, 0, 0);
       }
+    if (kv0 + KV_T > skv) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kv0 + j * 16 + fq * 4 + r >= skv) sacc[j][r] = -INFINITY;
     }
-    // ---- online softmax (rows fq*4 + r, cols j*16 + fr) ----
-    float alpha[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bool ok = kv0 + j * 16 + fr < skv;
-        const float sv = ok ? sacc[j][r] * scale_log2 : -INFINITY;
-        sacc[j][r] = sv;
-        mx = fmaxf(mx, sv);
-      }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-      const float mnew = fmaxf(mrow[r], mx);
-      alpha[r] = exp2f(mrow[r] - mnew);
-      mrow[r] = mnew;
-      float sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float pv = exp2f(sacc[j][r] - mnew);
-        sacc[j][r] = pv;
-        sum += pv;
-      }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
-      lrow[r] = lrow[r] * alpha[r] + sum;
-    }
-#pragma unroll
-    for (int j = 0; j < TNO; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) oacc[j][r] *= alpha[r];
-    // ---- P -> LDS (fp16) as [16 q][64 kv], chunk-swizzled ----
-    f16* pw = ps[wid];
+    // ---- online softmax for query fr (log2 domain) ----
+    float mx = sacc[0][0];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = fq * 4 + r, col = j * 16 + fr;
-        pw[row * KV_T + ((((col >> 3) ^ (row & 7)) << 3) | (col & 7))] = (f16)sacc[j][r];
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[j][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(mrow, mx * scale_log2);
+    if (__any(mnew > mrow)) {  // wave-uniform: lanes whose max did not grow get alpha = 1
+      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
+#pragma unroll
+      for (int j = 0; j < TD; ++j) oacc[j] *= alpha;
+      mrow = mnew;
+    }
+    f16x8 pf[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pf[j >> 1][(j & 1) * 4 + r] = (f16)__builtin_amdgcn_exp2f(fmaf(sacc[j][r], scale_log2, -mrow));
+    // ---- O^T[d][q] += V^T P^T ----
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < TD; ++j) {
+        const f16* vp = ks + vread + s * 32 * VST + j * 16;
+        const f16x4 lo = tr_read(vp);
+        const f16x4 hi = tr_read(vp + 16 * VST);
+        const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        oacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[s], oacc[j], 0, 0, 0);
       }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes visible
-    __builtin_amdgcn_wave_barrier();
-    // ---- O += P V ----
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int pc = s * 4 + fq;
-      const f16x8 pf = *reinterpret_cast<const f16x8*>(pw + fr * KV_T + ((pc ^ (fr & 7)) << 3));
-#pragma unroll
-      for (int j = 0; j < TNO; ++j) {
-        const int dd = j * 16 + fr;
-        const f16x8 vf = *reinterpret_cast<const f16x8*>(vt + dd * KV_T + ((pc ^ (dd & 7)) << 3));
-        oacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, vf, oacc[j], 0, 0, 0);
+  };
+
+  load_tile(0);
+  __syncthreads();  // padding writes above
+  store_tile(smem);
+  __syncthreads();
+  if constexpr (NB == 2) {
+    f16* const b0 = smem;
+    f16* const b1 = smem + KSZ + VSZ;
+    for (int t = 0; t < ntiles; t += 2) {
+      if (t + 1 < ntiles) load_tile((t + 1) * KV_T);
+      tile(b0, t * KV_T);
+      if (t + 1 >= ntiles) break;
+      store_tile(b1);
+      __syncthreads();
+      if (t + 2 < ntiles) load_tile((t + 2) * KV_T);
+      tile(b1, (t + 1) * KV_T);
+      if (t + 2 >= ntiles) break;
+      store_tile(b0);
+      __syncthreads();
+    }
+  } else {
+    for (int t = 0; t < ntiles; ++t) {
+      tile(smem, t * KV_T);
+      if (t + 1 < ntiles) {
+        load_tile((t + 1) * KV_T);
+        __syncthreads();
+        store_tile(smem);
+        __syncthreads();
       }
     }
   }
-  // ---- epilogue ----
+  // ---- epilogue: lane holds O^T rows 16j + 4fq + r of query fr; row d holds sum(P) ----
+  const int dj = d >> 4, dg = (d & 15) >> 2, dr = d & 3;  // (tile, lane group, reg) of row d
+  float lsum = 0.f;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qrow = q0 + wid * 16 + fq * 4 + r;
-    if (qrow >= sq) continue;
-    const float inv = 1.0f / lrow[r];
+  for (int j = 0; j < TD; ++j)
 #pragma unroll
-    for (int j = 0; j < TNO; ++j) {
-      const int dd = j * 16 + fr;
-      if (dd < d) ob[(long)qrow * ldo + dd] = (f16)(oacc[j][r] * inv);
+    for (int r = 0; r < 4; ++r)
+      if (j == dj && r == dr) lsum = oacc[j][r];
+  lsum = __shfl(lsum, dg * 16 + fr, 64);
+  const int qrow = q0 + wid * 16 + fr;
+  if (qrow < sq) {
+    const float inv = 1.0f / lsum;
+#pragma unroll
+    for (int j = 0; j < TD; ++j) {
+      const int dd = j * 16 + fq * 4;
+      if (dd < d) {
+        f16x4 w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = (f16)(oacc[j][r] * inv);
+        *reinterpret_cast<f16x4*>(ob + (long)qrow * ldo + dd) = w;
+      }
     }
   }
 }
@@ -174,7 +264,8 @@ template <int DP, int DV>
 static void launch(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, hipStream_t st) {
   dim3 grid((sq + 63) / 64, b * heads);
-  k_attn<DP, DV><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o,
+  constexpr int NB = DP <= 96 ? 2 : 1;
+  k_attn<DP, DV, NB><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o,
                                        ldo, heads, sq, skv, d, scale * 1.4426950408889634f);
 }
 
@@ -183,18 +274,25 @@ extern "C" int qd_attention(const void* q, int ldq, const void* k, int ldk, cons
                             void* stream) {
   QD_REQUIRE(q && k && v && o, "null pointer");
   QD_REQUIRE(d % 8 == 0 && d > 0 && d <= 256, "head_dim must be a multiple of 8 in (0, 256]");
-  QD_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0, "leading dims must be multiples of 8");
+  QD_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
+             "leading dims must be multiples of 8 (q, k, v) and 4 (o)");
   QD_REQUIRE(skv > 0, "empty key sequence");
   if ((long)b * heads * sq == 0) return 0;
   hipStream_t st = S(stream);
-  if (d <= 32) launch<32, 32>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 48) launch<64, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 64) launch<64, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 80) launch<96, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 96) launch<96, 96>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 128) launch<128, 128>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 160) launch<160, 160>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else launch<256, 256>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  // DP: QK^T depth (multiple of 32 >= d); DV: PV rows, a multiple of 16 > d (row d = denominator)
+  if (d <= 32) launch<32, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 40) launch<64, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 56) launch<64, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 64) launch<64, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 72) launch<96, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 88) launch<96, 96>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 96) launch<96, 112>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 120) launch<128, 128>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 128) launch<128, 144>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 152) launch<160, 160>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 160) launch<160, 176>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else if (d <= 248) launch<256, 256>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
+  else launch<256, 272>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -144,9 +144,19 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
           (EPI_AMAX if amax is not None else 0)
     if residual is not None:
         _chk(residual, "residual")
+    ws, wsn = _gemm_ws(M, N, K, WFMT[wfmt], rows_per_sample, epi, x2d.device)
     _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(weight), WFMT[wfmt], _p(scales), group,
-              _p(bias), _p(residual), _p(out), N, out.stride(0), epi, _p(amax), rows_per_sample, _stream())
+              _p(bias), _p(residual), _p(out), N, out.stride(0), epi, _p(amax), rows_per_sample,
+              _p(ws), wsn, _stream())
     return out
+
+
+def _gemm_ws(M, N, K, wfmt, rows_per_sample, epi, device):
+    """Split-K slab workspace the kernel plans for this shape (None if it runs unsplit)."""
+    n = _lib.load().qd_gemm_workspace(M, N, K, wfmt, rows_per_sample, epi)
+    if n <= 0:
+        return None, 0
+    return _empty((n,), torch.float32, device), n
 
 
 def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, residual=None, out=None,
@@ -164,8 +174,10 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
         out = _empty((n, ho, wo, co), torch.float16, x.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0)
+    ws, wsn = (None, 0) if cip % 64 else _gemm_ws(n * ho * wo, co, kh * kw * cip, 0, ho * wo, epi, x.device)
     _lib.call("qd_conv2d_fwd", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad,
-              1 if upsample2x else 0, _p(bias), _p(residual), _p(out), epi, _p(amax), _stream())
+              1 if upsample2x else 0, _p(bias), _p(residual), _p(out), epi, _p(amax), _p(ws), wsn,
+              _stream())
     return out
 
 

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "qdiff.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(qd_\w+)\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long|const char\*)\s+(qd_\w+)\(", src, re.M)))
 
 
 def test_library_exports_all_declared_symbols():
@@ -42,7 +42,7 @@ def test_bad_arguments_fail_before_launch():
                   ctypes.c_void_p(16), None)
     with pytest.raises(RuntimeError, match="K must be"):
         _lib.call("qd_linear_fwd", ctypes.c_void_p(16), 4, 12, 12, ctypes.c_void_p(16), 0, None, 0, None, None,
-                  ctypes.c_void_p(16), 4, 4, 0, None, 0, None)
+                  ctypes.c_void_p(16), 4, 4, 0, None, 0, None, 0, None)
 
 
 def test_sd15_tree_matches_reference_counts():

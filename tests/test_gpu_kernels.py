@@ -136,7 +136,7 @@ def test_smooth_fold_and_hook(golden, dev):
 
 # ------------------------------------------------------------------ GEMMs vs fp32 torch
 @pytest.mark.parametrize("M,N,Kd", [(128, 128, 64), (200, 320, 320), (616, 640, 768), (4096, 2560, 320),
-                                    (8, 1280, 1280), (1000, 64, 128)])
+                                    (8, 1280, 1280), (1000, 64, 128), (256, 1280, 5120), (512, 320, 640)])
 @pytest.mark.parametrize("fmt", ["f16", "i8", "i4"])
 def test_linear_formats(M, N, Kd, fmt, dev):
     k = K()
@@ -178,7 +178,8 @@ def test_linear_amax_epilogue(dev):
 @pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups", [(64, 64, 3, 1, 16, False), (64, 128, 3, 2, 16, False),
                                                         (128, 64, 1, 1, 8, False), (4, 64, 3, 1, 16, False),
                                                         (64, 64, 3, 1, 8, True), (320, 320, 3, 1, 32, False),
-                                                        (960, 320, 3, 1, 16, False)])
+                                                        (960, 320, 3, 1, 16, False), (1280, 1280, 3, 1, 8, False),
+                                                        (640, 640, 3, 1, 16, False)])
 def test_conv_nhwc(cin, cout, ksz, stride, hw, ups, dev):
     k = K()
     g = torch.Generator().manual_seed(cin * 7 + cout)
@@ -197,6 +198,19 @@ def test_conv_nhwc(cin, cout, ksz, stride, hw, ups, dev):
     got = k.nhwc_to_nchw(y).cpu().float()
     assert_fp16_close(got, ref, ulps=2.0, atol=1e-3)
     assert torch.equal(amax.view(n, cout).cpu(), got.abs().amax(dim=(2, 3)))
+    # deterministic (split-K slabs are reduced in a fixed order)
+    y2 = k.conv2d_nhwc(xh, wk, cin, stride, pad, ups, bias=b.to(dev), amax=amax)
+    assert torch.equal(y, y2)
+
+
+def test_gemm_plans_split_k_for_small_m():
+    from qdiff import _lib
+    lib = _lib.load()
+    # SD1.5 8x8 level: M = 8 * 64, N = 1280, K = 9 * 1280 -> too few 128-row tiles, K is split
+    assert lib.qd_gemm_workspace(512, 1280, 11520, 0, 64, 4) > 0
+    assert lib.qd_gemm_workspace(128, 1280, 11520, 0, 64, 4) > 0
+    # the big-M levels run unsplit
+    assert lib.qd_gemm_workspace(32768, 320, 2880, 0, 4096, 4) == 0
 
 
 # ------------------------------------------------------------------ attention
