@@ -32,7 +32,7 @@ __device__ __forceinline__ f16x4 tr_read(const f16* p) {
 constexpr int v_stride(int dv) { return ((dv / 2 / 8) & 1) ? dv : dv + 16; }
 
 // Swapped-operand flash attention (S^T = K Q^T, O^T = V^T P^T), 16x16x32 f16 MFMA.
-//   * 4 waves x 16 queries; a lane owns ONE query (column lane&15 of every accumulator), so
+//   * NW waves x 16 queries; a lane owns ONE query (column lane&15 of every accumulator), so
 //     the softmax row max is 16 in-register maxes + 2 cross-group shuffles and the
 //     online-softmax rescale is one scalar per lane, skipped (wave-uniformly) whenever no
 //     lane's running max grew.
@@ -45,8 +45,8 @@ constexpr int v_stride(int dv) { return ((dv / 2 / 8) & 1) ? dv : dv + 16; }
 //   * K/V tiles register-staged and double-buffered in LDS (tile loop unrolled x2 so every
 //     LDS address is a per-lane base + immediate); the next tile's loads are in flight while
 //     the current one is computed; one barrier per tile.
-template <int DP, int DV, int NB>
-__global__ void __launch_bounds__(256) k_attn(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
+template <int DP, int DV, int NB, int NW>
+__global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                               int ldk, const f16* __restrict__ v, int ldv,
                                               f16* __restrict__ o, int ldo, int heads, int sq, int skv,
                                               int d, float scale_log2) {
@@ -55,13 +55,20 @@ __global__ void __launch_bounds__(256) k_attn(const f16* __restrict__ q, int ldq
   constexpr int VST = v_stride(DV);
   constexpr int KSZ = KV_T * KCHP * 8, VSZ = KV_T * VST;
   constexpr int VCH = DV / 8;
-  constexpr int NKL = (KV_T * KCH + 255) / 256, NVL = (KV_T * VCH + 255) / 256;
+  constexpr int NT = NW * 64;
+  constexpr int NKL = (KV_T * KCH + NT - 1) / NT, NVL = (KV_T * VCH + NT - 1) / NT;
   constexpr int TD = DV / 16;
   __shared__ __attribute__((aligned(16))) f16 smem[NB * (KSZ + VSZ)];
 
-  const int bh = blockIdx.y;
+  // XCD-aware bijective remap: the q-blocks of one (batch, head) run on one XCD (blocks b and
+  // b + 8 share an XCD), so that head's K/V stays in that XCD's L2 while they stream it.
+  const int nqb = (sq + NW * 16 - 1) / (NW * 16);  // q-blocks per (batch, head)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int bh = wg / nqb;
   const int b = bh / heads, h = bh % heads;
-  const int q0 = blockIdx.x * 64;
+  const int q0 = (wg - bh * nqb) * (NW * 16);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
 
@@ -86,11 +93,11 @@ __global__ void __launch_bounds__(256) k_attn(const f16* __restrict__ q, int ldq
 
   // Padding of both tile buffers, written once: K chunks >= d/8 are zero; V columns >= d are
   // zero except column d = 1.0 (the denominator row of O^T).  Tile stores never touch them.
-  for (int i = tid; i < NB * KV_T * KCHP; i += 256) {
+  for (int i = tid; i < NB * KV_T * KCHP; i += NT) {
     const int bf = i / (KV_T * KCHP), row = (i / KCHP) % KV_T, c = i % KCHP;
     if (c >= dchunks) *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + ((c ^ (row & 7)) << 3)) = f16x8{};
   }
-  for (int i = tid; i < NB * KV_T * (VST - d); i += 256) {
+  for (int i = tid; i < NB * KV_T * (VST - d); i += NT) {
     const int bf = i / (KV_T * (VST - d)), row = (i / (VST - d)) % KV_T, col = d + i % (VST - d);
     smem[bf * (KSZ + VSZ) + KSZ + row * VST + col] = (f16)(col == d ? 1.0f : 0.0f);
   }
@@ -104,14 +111,14 @@ __global__ void __launch_bounds__(256) k_attn(const f16* __restrict__ q, int ldq
   int kdst[NKL], vdst[NVL];  // LDS element offset within a buffer, -1 = padding chunk (skip)
 #pragma unroll
   for (int i = 0; i < NKL; ++i) {
-    const int e = tid + i * 256, row = e / KCH, c = e % KCH;
+    const int e = tid + i * NT, row = e / KCH, c = e % KCH;
     const bool ok = e < KV_T * KCH && c < dchunks;
     koff[i] = (unsigned)(row * ldk + c * 8) * 2u;
     kdst[i] = ok ? row * KCHP * 8 + ((c ^ (row & 7)) << 3) : -1;
   }
 #pragma unroll
   for (int i = 0; i < NVL; ++i) {
-    const int e = tid + i * 256, row = e / VCH, c = e % VCH;
+    const int e = tid + i * NT, row = e / VCH, c = e % VCH;
     const bool ok = e < KV_T * VCH && c < dchunks;
     voff[i] = (unsigned)(row * ldv + c * 8) * 2u;
     vdst[i] = ok ? KSZ + row * VST + c * 8 : -1;
@@ -263,10 +270,17 @@ __global__ void __launch_bounds__(256) k_attn(const f16* __restrict__ q, int ldq
 template <int DP, int DV>
 static void launch(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, hipStream_t st) {
-  dim3 grid((sq + 63) / 64, b * heads);
   constexpr int NB = DP <= 96 ? 2 : 1;
-  k_attn<DP, DV, NB><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o,
-                                       ldo, heads, sq, skv, d, scale * 1.4426950408889634f);
+  // 8 waves (128 queries) share each staged K/V tile on long sequences; 4 on short ones
+  if (sq >= 512) {
+    const int grid = ((sq + 127) / 128) * b * heads;
+    k_attn<DP, DV, NB, 8><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                               (f16*)o, ldo, heads, sq, skv, d, scale * 1.4426950408889634f);
+  } else {
+    const int grid = ((sq + 63) / 64) * b * heads;
+    k_attn<DP, DV, NB, 4><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                               (f16*)o, ldo, heads, sq, skv, d, scale * 1.4426950408889634f);
+  }
 }
 
 extern "C" int qd_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
