@@ -34,6 +34,9 @@ extern "C" {
 #define QD_GRAN_PER_CHANNEL 1  /* quantize_activation_per_channel_absmax fake_quant.py:123-131 */
 #define QD_GRAN_PER_TENSOR 2   /* quantize_activation_per_tensor_absmax  fake_quant.py:157-167 */
 #define QD_GRAN_PER_GROUP 3    /* quantize_activation_per_channel_group_absmax :133-153 */
+/* qd_act_absmax only: OR into `gran` when `amax` is known to hold zeros already (a pooled
+ * buffer zeroed once per step with qd_fill_zero); the call then skips its own zero-fill. */
+#define QD_GRAN_ZEROED 0x100
 
 #define QD_LAYOUT_NCHW 0
 #define QD_LAYOUT_NHWC 1
@@ -46,6 +49,8 @@ extern "C" {
 int qd_version(void);
 const char* qd_last_error(void);
 int qd_device_arch(char* buf, int len); /* writes gcnArchName of the current device */
+/* p[0:n) = 0.0f with a kernel (never a memset node: graph-capture safe). */
+int qd_fill_zero(float* p, long n, void* stream);
 
 /* ---------------- activation fake-quant ---------------------------------------------- */
 /* Reduction pass: amax[...] = max |x| over the granularity's reduction set.  `amax` is fp32,
@@ -86,6 +91,8 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 #define QD_EPI_RESIDUAL 2    /* out = half(y + residual[M, N]) */
 #define QD_EPI_AMAX 4        /* per-(sample, col) amax of the rounded y into amax[M/rows_per_sample][N]
                                 (zeroed by the call itself, then atomically max-reduced) */
+#define QD_EPI_AMAX_ZEROED 16 /* with QD_EPI_AMAX: amax already holds zeros (pooled, zeroed once
+                                 per step); the call skips its own zero-fill launch */
 #define QD_EPI_GEGLU 8       /* B holds [hidden; gate] halves (N = 2*I): out[M, I] = h * gelu(g) */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear

@@ -21,6 +21,7 @@ F = ctypes.c_float
 SIGNATURES = {
     "qd_version": [],
     "qd_device_arch": [ctypes.c_char_p, I],
+    "qd_fill_zero": [P, ctypes.c_long, P],
     "qd_act_absmax": [P, I, I, I, I, I, I, I, P, P],
     "qd_act_fakequant": [P, P, I, I, I, I, I, I, I, I, P, P],
     "qd_act_apply": [P, P, I, I, I, I, I, I, I, I, P, P],

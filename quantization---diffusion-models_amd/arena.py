@@ -22,6 +22,48 @@ class Arena:
         self.bufs = []
         self.i = 0
         self.frozen = False
+        # fp32 atomic-max targets that must start each step at zero: recorded individually on the
+        # first step, then carved out of ONE pool that a single kernel zeroes at every step start
+        self.zsizes = []
+        self.zviews = None
+        self.zpool = None
+        self.zi = 0
+
+    def zeroed_f32(self, n, device):
+        """A zero-filled fp32 buffer of n elements for this step -> (tensor, True)."""
+        if self.zviews is not None:
+            if self.zi >= len(self.zviews) or self.zviews[self.zi].numel() != n:
+                raise RuntimeError(f"arena: zeroed buffer #{self.zi} changed size; the step is not shape-static")
+            t = self.zviews[self.zi]
+        else:
+            if self.frozen:
+                raise RuntimeError("arena: zeroed allocation beyond the recorded plan while frozen")
+            self.zsizes.append(n)
+            self.zdevice = device
+            t = torch.zeros(n, dtype=torch.float32, device=device)
+        self.zi += 1
+        return t, True
+
+    def _build_pool(self, device):
+        tot = sum((n + 63) // 64 * 64 for n in self.zsizes)  # 256-B aligned slices
+        self.zpool = torch.zeros(max(tot, 1), dtype=torch.float32, device=device)
+        self.zviews, off = [], 0
+        for n in self.zsizes:
+            self.zviews.append(self.zpool[off:off + n])
+            off += (n + 63) // 64 * 64
+
+    def begin_step(self):
+        """Zero the pool (one launch, captured into the step's graph)."""
+        self.i = 0
+        self.zi = 0
+        if self.zpool is not None:
+            from . import _lib
+            _lib.call("qd_fill_zero", self.zpool.data_ptr(), self.zpool.numel(),
+                      torch.cuda.current_stream(self.zpool.device).cuda_stream)
+
+    def end_step(self):
+        if self.zviews is None and self.zsizes and not self.frozen:
+            self._build_pool(self.zdevice)
 
     def alloc(self, shape, dtype, device):
         shape = torch.Size(shape)
@@ -48,12 +90,13 @@ def using(arena, frozen=False):
     global _active
     prev = _active
     _active = arena
-    arena.i = 0
     arena.frozen = frozen
+    arena.begin_step()
     try:
         yield arena
     finally:
         _active = prev
+        arena.end_step()
         arena.frozen = False
 
 
@@ -61,3 +104,11 @@ def empty(shape, dtype, device):
     if _active is not None:
         return _active.alloc(shape, dtype, device)
     return torch.empty(shape, dtype=dtype, device=device)
+
+
+def zeroed_f32(n, device):
+    """(buffer, zeroed): inside an arena step a pooled zero-filled buffer (the consuming kernel
+    may skip its own zero-fill); otherwise an uninitialised one the kernel must zero itself."""
+    if _active is not None:
+        return _active.zeroed_f32(n, device)
+    return torch.empty(n, dtype=torch.float32, device=device), False

@@ -18,8 +18,9 @@
 //
 // Structure (MI355X): 256 threads = 2 x 2 waves, block tile BM x BN x 64, wave tile
 // (BM/2) x (BN/2).  Each wave computes C^T tiles (MFMA A = weight fragment, B = activation
-// fragment), so a lane ends with 4 consecutive output columns of one row: 8-B stores, bias /
-// residual as 8-B vectors.  All global operand loads are raw buffer loads whose invalid
+// fragment), so a lane ends with 4 consecutive output columns of one row (8-B bias vectors,
+// column amax by 16-lane shuffles); the fp16 tile is then re-read from LDS in 16-B row chunks
+// for fully coalesced residual loads and stores.  All global operand loads are raw buffer loads whose invalid
 // chunks (rows past M/N, halo of the conv, K tail) carry an offset >= 2^31 and read zero:
 // the staging path has no branches and the next K step's loads stay in flight while the
 // current step's MFMAs run (register-staged, LDS double-buffered, one barrier per step).
@@ -379,33 +380,33 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
       }
     }
   } else {
+    // (1) fragments: h = half(acc + bias) -> per-column amax (pre-residual, the conv output the
+    //     reference fake-quantizes) and an fp16 C tile in LDS (the K loop ended on a barrier);
+    // (2) coalesced: 16-B row chunks of the tile (+ residual) -> y.
+    constexpr int LP = BN + 8;  // LDS row pitch (halves)
+    f16* ct = smem;
     const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
     const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn0 + j * 16 + fq * 4;
-      const bool col_ok = n < p.N;  // N % 4 == 0: a lane's 4 columns are all in or all out
+      const int nl = wn0 + j * 16 + fq * 4;
+      const int n = n0 + nl;
+      const bool col_ok = n < p.N;  // N % 8 == 0: a lane's 4 columns are all in or all out
       f16x4 bq = {};
       if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
       float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wm0 + i * 16 + fr;
-        if (m < p.M && col_ok) {
-          f16x4 h;
+        const int ml = wm0 + i * 16 + fr;
+        const bool ok = m0 + ml < p.M && col_ok;
+        f16x4 h;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
-            cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
-          }
-          if (has_res) {
-            const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)m * p.ldy + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
-          }
-          *reinterpret_cast<f16x4*>(p.y + (long)m * p.ldy + n) = h;
+        for (int r = 0; r < 4; ++r) {
+          h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
+          if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
         }
+        *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
       }
       if (do_amax) {
         // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
@@ -417,6 +418,22 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
         }
+      }
+    }
+    __syncthreads();
+    constexpr int CPR = BN / 8;
+#pragma unroll 2
+    for (int e = threadIdx.x; e < BM * CPR; e += 256) {
+      const int row = e / CPR, c = e - row * CPR;
+      const int m = m0 + row, n = n0 + c * 8;
+      if (m < p.M && n < p.N) {
+        f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+        if (has_res) {
+          const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
+        }
+        *reinterpret_cast<f16x8*>(p.y + (long)m * p.ldy + n) = v;
       }
     }
   }
@@ -551,7 +568,7 @@ static int check_common(const GemmArgs& p, int fmt) {
   QD_REQUIRE(p.a && p.b && p.y, "null pointer");
   QD_REQUIRE(p.M >= 0 && p.N > 0 && p.K > 0, "bad GEMM shape");
   QD_REQUIRE(p.K % 8 == 0, "K must be a multiple of 8");
-  QD_REQUIRE(p.N % 4 == 0 && p.ldy % 4 == 0, "N and ldy must be multiples of 4");
+  QD_REQUIRE(p.N % 8 == 0 && p.ldy % 8 == 0, "N and ldy must be multiples of 8");
   QD_REQUIRE(fmt == QD_WFMT_F16 || fmt == QD_WFMT_I8 || fmt == QD_WFMT_I4, "bad weight format");
   if (fmt != QD_WFMT_F16) {
     QD_REQUIRE(p.bscale && p.group > 0 && p.K % p.group == 0, "bad weight scales / group");
@@ -562,9 +579,9 @@ static int check_common(const GemmArgs& p, int fmt) {
   QD_REQUIRE(!(p.epi & QD_EPI_AMAX) || (p.amax && p.rows_per_sample > 0 && p.rows_per_sample % 64 == 0),
              "amax epilogue needs rows_per_sample % 64 == 0");
   QD_REQUIRE(!(p.epi & QD_EPI_GEGLU), "GEGLU epilogue not available in this build");
-  QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 7) == 0, "y must be 8-B aligned");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
-  QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 7) == 0, "residual must be 8-B aligned");
+  QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
   const double wbytes = (double)p.N * p.K * (fmt == QD_WFMT_F16 ? 2 : fmt == QD_WFMT_I8 ? 1 : 0.5);
   QD_REQUIRE(wbytes < 2147483648.0, "weight exceeds the 2 GiB buffer-addressing range");
   return 0;
@@ -603,7 +620,7 @@ extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w
   if (M == 0) return 0;
   p.a_bytes = (unsigned)((long)(M - 1) * lda * 2 + (long)K * 2);
   p.b_bytes = (unsigned)(wfmt == QD_WFMT_F16 ? (long)N * K * 2 : wfmt == QD_WFMT_I8 ? (long)N * K : (long)N * K / 2);
-  if (epi & QD_EPI_AMAX)  // amax is zeroed by the call (stream-ordered, graph-capturable)
+  if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
   run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();
@@ -652,7 +669,7 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
   if (p.M == 0) return 0;
   p.a_bytes = (unsigned)((long)n * h * w * ci_pad * 2);
   p.b_bytes = (unsigned)((long)co * p.K * 2);
-  if (epi & QD_EPI_AMAX)  // amax is zeroed by the call (stream-ordered, graph-capturable)
+  if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)n * co, S(stream));
   if (ci_pad % 64 == 0) run_gemm<AM_CONV>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
   else run_gemm<AM_CONV_ANY>(p, QD_WFMT_F16, ws, ws_elems, S(stream));

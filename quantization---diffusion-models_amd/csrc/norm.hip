@@ -74,9 +74,10 @@ __global__ void __launch_bounds__(256) k_gn_stats(const f16* __restrict__ x, con
 
 __global__ void k_gn_coeff(const float* __restrict__ part, int n, int hw, int c, int groups, int S, float eps,
                            const f16* __restrict__ gamma, const f16* __restrict__ beta,
-                           float2* __restrict__ coef) {
+                           float2* __restrict__ coef, float* __restrict__ amax) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n * c) return;
+  amax[i] = 0.f;  // the amax pass that follows accumulates into it (no separate zero-fill launch)
   const int ni = i / c, ch = i % c;
   const int cg = c / groups, g = ch / cg;
   const float* p = part + ((long)(ni * groups + g) * S) * 3;
@@ -136,26 +137,37 @@ __global__ void __launch_bounds__(256) k_gn_amax(const f16* __restrict__ x, cons
   }
 }
 
-// 8 channels per thread; the two sources are both multiples of 8 channels wide (host check).
+// block (bx, by): thread (tx, ty) owns channel chunk blockIdx.x * bx + tx (8 channels, 16 B) of
+// sample blockIdx.y and rows ty, ty + by, ... of its row range: the per-channel coefficients
+// and fake-quant scales are loaded / computed once per thread, rows stream through.
+// The two sources are both multiples of 8 channels wide (host check).
 __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                  int c1, long count8, int hw, int c,
+                                                  int c1, int hw, int c, int rows_per_block,
                                                   const float2* __restrict__ coef, int silu, int qmax,
                                                   const float* __restrict__ amax, f16* __restrict__ y) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= count8) return;
-  const long e = i * 8;
-  const int ch = (int)(e % c);
-  const long row = e / c;
-  const long n = row / hw;
-  const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, row, ch));
-  const float2* k = coef + n * c + ch;
-  f16x8 o;
+  const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (chunk * 8 >= c) return;
+  const int ch = chunk * 8;
+  const long n = blockIdx.y;
+  const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
+  float2 k[8];
+  float sq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float val = gn_out((float)v[j], k[j], silu);
-    o[j] = qmax > 0 ? fq_apply(val, fq_scale(amax[n * c + ch + j], qmax)) : (f16)val;
+    k[j] = coef[n * c + ch + j];
+    sq[j] = qmax > 0 ? fq_scale(amax[n * c + ch + j], qmax) : 0.f;
   }
-  *reinterpret_cast<f16x8*>(y + e) = o;
+  for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
+    const long row = n * hw + r;
+    const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, row, ch));
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float val = gn_out((float)v[j], k[j], silu);
+      o[j] = qmax > 0 ? fq_apply(val, sq[j]) : (f16)val;
+    }
+    *reinterpret_cast<f16x8*>(y + row * c + ch) = o;
+  }
 }
 
 extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
@@ -183,15 +195,21 @@ extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw
   dim3 sg(n * groups, S_);
   k_gn_stats<<<sg, 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, S_, part);
   k_gn_coeff<<<grid1((long)n * c), 256, 0, st>>>(part, n, hw, c, groups, S_, eps, (const f16*)gamma,
-                                                 (const f16*)beta, coef);
+                                                 (const f16*)beta, coef, amax);
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
   if (qmax) {
-    qd_zero_f32(amax, (size_t)n * c, st);
     k_gn_amax<<<sg, 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, S_, coef, silu, amax);
   }
-  const long count8 = (long)n * hw * c / 8;
-  k_gn_apply<<<grid1(count8), 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, count8, hw, c, coef, silu, qmax,
-                                            amax, (f16*)y);
+  {
+    const int chunks = c / 8;
+    const int bx = std::min(chunks, 256), by = 256 / bx, gx = (chunks + bx - 1) / bx;
+    int rpb = by * 4;  // >= 4 rows per thread, more blocks while the grid is small
+    while (rpb > by && (long)gx * n * ((hw + rpb - 1) / rpb) < 2048) rpb /= 2;
+    while ((long)gx * n * ((hw + rpb - 1) / rpb) > 8192) rpb *= 2;
+    dim3 grid(gx, n, (hw + rpb - 1) / rpb);
+    k_gn_apply<<<grid, dim3(bx, by), 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, rpb, coef, silu, qmax,
+                                              amax, (f16*)y);
+  }
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -40,6 +40,15 @@ void qd_zero_f32(float* p, size_t n, hipStream_t st) {
   if (n == 0) return;
   k_zero_f32<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(p, n);
 }
+
+extern "C" int qd_fill_zero(float* p, long n, void* stream) {
+  QD_REQUIRE(p || n == 0, "null pointer");
+  QD_REQUIRE(n >= 0, "negative size");
+  if (n) qd_zero_f32(p, (size_t)n, reinterpret_cast<hipStream_t>(stream));
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------------------------------
@@ -194,8 +203,10 @@ static int grid1(long count, int per_block = 256) { return (int)((count + per_bl
 static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, int gran, int group,
                          float* amax, hipStream_t st) {
   const long hw = (long)h * w;
+  const bool zeroed = (gran & QD_GRAN_ZEROED) != 0;
+  gran &= ~QD_GRAN_ZEROED;
   if (gran == QD_GRAN_PER_CHANNEL) {
-    qd_zero_f32(amax, (size_t)n * c, st);
+    if (!zeroed) qd_zero_f32(amax, (size_t)n * c, st);
     if (layout == QD_LAYOUT_NHWC) {
       QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
       const int chunks = c / 8;
@@ -211,7 +222,7 @@ static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, 
     const long rows = (long)n * hw;  // rows of length c (caller passes h = w = 1 normally)
     k_rowmax<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, rows, c, amax);
   } else if (gran == QD_GRAN_PER_TENSOR) {
-    qd_zero_f32(amax, 1, st);
+    if (!zeroed) qd_zero_f32(amax, 1, st);
     const long count = (long)n * c * hw;
     k_tensormax<<<(int)std::min<long>(2048, grid1(count)), 256, 0, st>>>((const f16*)x, count, amax);
   } else if (gran == QD_GRAN_PER_GROUP) {

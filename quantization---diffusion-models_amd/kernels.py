@@ -10,12 +10,15 @@ import ctypes
 import torch
 
 from . import _lib
+from . import arena as A
 from .arena import empty as _empty
 
 GRAN = {"per_token": 0, "per_channel": 1, "per_tensor": 2, "per_group": 3}
 NCHW, NHWC = 0, 1
 WFMT = {"f16": 0, "i8": 1, "i4": 2}
 EPI_BIAS, EPI_RESIDUAL, EPI_AMAX = 1, 2, 4
+EPI_AMAX_ZEROED = 16
+GRAN_ZEROED = 0x100
 
 
 def _p(t):
@@ -80,10 +83,11 @@ def act_absmax(x, gran, layout=NHWC, group=0):
             n, c, h, w = x.shape
         else:
             n, h, w, c = x.shape
-        out = _empty((n * c,), torch.float32, x.device)
+        out, zeroed = A.zeroed_f32(n * c, x.device)
     else:
         raise ValueError("act_absmax wrapper supports per_channel only")
-    _lib.call("qd_act_absmax", _p(x), layout, n, c, h, w, GRAN[gran], group, _p(out), _stream())
+    _lib.call("qd_act_absmax", _p(x), layout, n, c, h, w, GRAN[gran] | (GRAN_ZEROED if zeroed else 0), group,
+              _p(out), _stream())
     return out
 
 
@@ -130,7 +134,7 @@ def conv_weight_khwc(w, ci_pad):
 
 # ---------------------------------------------------------------- GEMMs
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
-           amax=None, rows_per_sample=0):
+           amax=None, rows_per_sample=0, amax_zeroed=False):
     """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K)."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
         raise ValueError("x must be an fp16 HIP tensor")
@@ -141,7 +145,7 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     if out is None:
         out = _empty((M, N), torch.float16, x2d.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
-          (EPI_AMAX if amax is not None else 0)
+          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0)
     if residual is not None:
         _chk(residual, "residual")
     ws, wsn = _gemm_ws(M, N, K, WFMT[wfmt], rows_per_sample, epi, x2d.device)
@@ -160,7 +164,7 @@ def _gemm_ws(M, N, K, wfmt, rows_per_sample, epi, device):
 
 
 def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, residual=None, out=None,
-                amax=None):
+                amax=None, amax_zeroed=False):
     """NHWC implicit-GEMM conv; x [N, H, W, Cip], w_khwc [Co, kh, kw, Cip]."""
     _chk(x, "x")
     _chk(w_khwc, "weight")
@@ -173,7 +177,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     if out is None:
         out = _empty((n, ho, wo, co), torch.float16, x.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
-          (EPI_AMAX if amax is not None else 0)
+          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0)
     ws, wsn = (None, 0) if cip % 64 else _gemm_ws(n * ho * wo, co, kh * kw * cip, 0, ho * wo, epi, x.device)
     _lib.call("qd_conv2d_fwd", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad,
               1 if upsample2x else 0, _p(bias), _p(residual), _p(out), epi, _p(amax), _p(ws), wsn,

@@ -27,6 +27,7 @@ from typing import Optional, Sequence, Tuple, Union
 import torch
 from torch import nn
 
+from . import arena as A
 from . import kernels as K
 from .fake_quant import WxAxConv2d, WxAxLinear
 
@@ -373,8 +374,8 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
     if q:
         n = x.shape[0]
-        amax = K._empty((n * wk.shape[0],), torch.float32, x.device)
-        y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax)
+        amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
+        y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)
         return K.fq_finalize(y, amax, q, residual=residual, chan_add=chan_add, out=y)
     if chan_add is None:
         return K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, residual=residual)
