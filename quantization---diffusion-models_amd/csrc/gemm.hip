@@ -388,45 +388,78 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
     const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
     const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
+    const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
+    if (geglu) {
+      // weight rows interleaved in 16-row blocks [hidden 16 | gate 16]: fragment tiles j (hidden)
+      // and j + 1 (gate) hold the same 16 output columns.  diffusers GEGLU: out =
+      // half(h * half(gelu(g))) on the fp16 projection outputs h, g.
+      // (TN is even for every tile the planner allows with GEGLU: BN in {64, 128})
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int nl = wn0 + j * 16 + fq * 4;
-      const int n = n0 + nl;
-      const bool col_ok = n < p.N;  // N % 8 == 0: a lane's 4 columns are all in or all out
-      f16x4 bq = {};
-      if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
-      float cm[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int ml = wm0 + i * 16 + fr;
-        const bool ok = m0 + ml < p.M && col_ok;
-        f16x4 h;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
-          if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+      for (int j = 0; j + 1 < TN; j += 2) {
+        const int nl = wn0 + j * 16 + fq * 4;
+        const int n = n0 + nl;
+        f16x4 bh = {}, bg = {};
+        if (has_bias && n < p.N) {
+          bh = *reinterpret_cast<const f16x4*>(p.bias + n);
+          bg = *reinterpret_cast<const f16x4*>(p.bias + n + 16);
         }
-        *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
+        const int ol = (wn0 >> 1) + j * 8 + fq * 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ml = wm0 + i * 16 + fr;
+          f16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const f16 h = (f16)(acc[i][j][r] + (float)bh[r]);
+            const f16 g = (f16)(acc[i][j + 1][r] + (float)bg[r]);
+            o[r] = (f16)((float)h * (float)(f16)gelu_f((float)g));
+          }
+          *reinterpret_cast<f16x4*>(ct + ml * LP + ol) = o;
+        }
       }
-      if (do_amax) {
-        // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
+    } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
-        const int row0 = m0 + wm0;
-        if (fr == 0 && col_ok && row0 < p.M) {
-          float* a = p.amax + (long)(row0 / p.rows_per_sample) * p.N + n;
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn0 + j * 16 + fq * 4;
+        const int n = n0 + nl;
+        const bool col_ok = n < p.N;  // N % 8 == 0: a lane's 4 columns are all in or all out
+        f16x4 bq = {};
+        if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+        float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
+        for (int i = 0; i < TM; ++i) {
+          const int ml = wm0 + i * 16 + fr;
+          const bool ok = m0 + ml < p.M && col_ok;
+          f16x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
+            if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+          }
+          *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
+        }
+        if (do_amax) {
+          // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
+          const int row0 = m0 + wm0;
+          if (fr == 0 && col_ok && row0 < p.M) {
+            float* a = p.amax + (long)(row0 / p.rows_per_sample) * p.N + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
+          }
         }
       }
     }
     __syncthreads();
-    constexpr int CPR = BN / 8;
+    // output tile: BN columns (BN / 2 with GEGLU) starting at n0 (n0 / 2)
+    const int cpr = geglu ? BN / 16 : BN / 8;
+    const int on0 = geglu ? n0 >> 1 : n0, oN = geglu ? p.N >> 1 : p.N;
 #pragma unroll 2
-    for (int e = threadIdx.x; e < BM * CPR; e += 256) {
-      const int row = e / CPR, c = e - row * CPR;
-      const int m = m0 + row, n = n0 + c * 8;
-      if (m < p.M && n < p.N) {
+    for (int e = threadIdx.x; e < BM * cpr; e += 256) {
+      const int row = e / cpr, c = e - row * cpr;
+      const int m = m0 + row, n = on0 + c * 8;
+      if (m < p.M && n < oN) {
         f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
         if (has_res) {
           const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
@@ -496,7 +529,7 @@ struct Plan {
 // Cost model (seconds): a CU runs ~4 TFLOP/s of this kernel with 2 resident blocks, ~3 with
 // one; tile efficiency eff; a launch takes ceil(blocks / 512) rounds of 2 blocks per CU.
 // Splits add the fp32 slab round trip (~5 TB/s) and one reduction launch.
-static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bool amax) {
+static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bool amax, bool geglu = false) {
   struct T {
     int bm, bn;
     double eff;
@@ -507,9 +540,10 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
     if (t.bn == 160 && N % 160 != 0) continue;  // 160-wide tiles only where they fit N exactly
     if (amax && rows_per_sample % (t.bm / 2) != 0) continue;
     if (quant_w && t.bn == 160) continue;        // int staging maps are built for BN % 64 == 0
+    if (geglu && t.bn == 160) continue;          // GEGLU pairs 16-column fragments: WN % 32 == 0
     const long tiles_mn = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
     for (int s = 1; s <= 16; s *= 2) {
-      if (s > 1 && (K % (64 * s) != 0 || K / s < 512)) break;
+      if (s > 1 && (K % (64 * s) != 0 || K / s < 512 || geglu)) break;
       const long blocks = tiles_mn * s;
       const double blk = 2.0 * t.bm * t.bn * ((double)K / s) / t.eff;  // flop of one block
       double tm = blocks <= 256 ? blk / 3e12 : (double)((blocks + 511) / 512) * 2.0 * blk / 4e12;
@@ -545,7 +579,8 @@ static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 
 
 template <int AMODE>
 static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t st) {
-  Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0);
+  Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
+                      (p.epi & QD_EPI_GEGLU) != 0);
   if (AMODE == AM_CONV_ANY || !ws || ws_elems < split_ws_elems(pl, p.M, p.N)) {
     if (pl.splits > 1) {  // no room for slabs: best unsplit plan
       pl.splits = 1;
@@ -578,7 +613,8 @@ static int check_common(const GemmArgs& p, int fmt) {
   QD_REQUIRE(!(p.epi & QD_EPI_RESIDUAL) || p.res, "residual epilogue without residual");
   QD_REQUIRE(!(p.epi & QD_EPI_AMAX) || (p.amax && p.rows_per_sample > 0 && p.rows_per_sample % 64 == 0),
              "amax epilogue needs rows_per_sample % 64 == 0");
-  QD_REQUIRE(!(p.epi & QD_EPI_GEGLU), "GEGLU epilogue not available in this build");
+  QD_REQUIRE(!(p.epi & QD_EPI_GEGLU) || (!(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL)) && p.N % 32 == 0),
+             "GEGLU epilogue: N % 32 == 0, no residual / amax");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
@@ -588,7 +624,8 @@ static int check_common(const GemmArgs& p, int fmt) {
 }
 
 extern "C" long qd_gemm_workspace(int M, int N, int K, int wfmt, int rows_per_sample, int epi) {
-  const Plan pl = plan_gemm(M, N, K, wfmt != QD_WFMT_F16, rows_per_sample, (epi & QD_EPI_AMAX) != 0);
+  const Plan pl = plan_gemm(M, N, K, wfmt != QD_WFMT_F16, rows_per_sample, (epi & QD_EPI_AMAX) != 0,
+                            (epi & QD_EPI_GEGLU) != 0);
   return split_ws_elems(pl, M, N);
 }
 
@@ -614,7 +651,7 @@ extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w
   p.epi = epi;
   int rc = check_common(p, wfmt);
   if (rc) return rc;
-  QD_REQUIRE(lda >= K && lda % 8 == 0 && ldy >= N, "bad leading dimensions");
+  QD_REQUIRE(lda >= K && lda % 8 == 0 && ldy >= ((epi & QD_EPI_GEGLU) ? N / 2 : N), "bad leading dimensions");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "x must be 16-B aligned");
   QD_REQUIRE((double)M * lda * 2 < 2147483648.0, "activation exceeds the 2 GiB buffer-addressing range");
   if (M == 0) return 0;

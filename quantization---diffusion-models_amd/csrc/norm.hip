@@ -15,84 +15,43 @@ static int grid1(long count, int per_block = 256) { return (int)((count + per_bl
 // GroupNorm on NHWC [N, HW, C] (+ SiLU) (+ fused per-(n,c) fake-quant of the output), with an
 // optional second source for channels [c1, C) (the UNet's skip concat, never materialised).
 //
-// Four stream-ordered kernels, all deterministic (fixed-order reductions, max is exact):
-//   1. k_gn_stats   grid (n*G, S): slab chunk -> shifted partial sums (s1, s2) per block
-//   2. k_gn_coeff   per (n, c): mean / rstd from the S partials (fixed order) ->
-//                   scale = rstd*gamma, bias = beta - scale*mean  (torch CPU GroupNorm form)
-//   3. k_gn_amax    [q_bits] grid (n*G, S): per-channel max |fq input| over the chunk's rows
+// Four stream-ordered kernels, all deterministic (fixed-order reductions, max is exact).  The
+// three streaming passes share one geometry: block (bx, by), thread (tx, ty) owns the 8-channel
+// 16-B chunk blockIdx.x * bx + tx of sample blockIdx.y and rows ty, ty + by, ... of row range
+// blockIdx.z: fully coalesced 16-B accesses, per-channel state in registers.
+//   1. k_gn_stats   per-channel shifted sums (shift = the group's first element) and min / max
+//                   -> LDS reduction over ty -> partial[n][z][c] (s1, s2, min, max)
+//   2. k_gn_coeff   per (n, c): group mean / rstd from the partials in fixed order ->
+//                   scale = rstd*gamma, bias = beta - scale*mean (torch CPU GroupNorm form);
+//                   [q_bits] the exact per-(n,c) amax of the output from the channel's min / max
+//                   (monotonicity argument at k_gn_coeff), flagging the rare channels it cannot
+//   3. k_gn_amax    [q_bits, SiLU] full max |out| pass for the flagged channels only
 //                   (the input quant of the consuming conv: fake_quant.py:125 reduction)
-//   4. k_gn_apply   elementwise, 8 channels (16 B) per thread: y = fq(silu(half(x*a + b)))
+//   4. k_gn_apply   y = fq(silu(half(x*a + b)))
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ const f16* gn_src(const f16* x, const f16* x2, int c1, int c, long row,
                                              int ch) {
   return ch < c1 ? x + row * c1 + ch : x2 + row * (c - c1) + (ch - c1);
 }
 
-static int gn_splits(long slabs, int hw) {
-  int s = 1;
-  while (slabs * s < 2048 && hw / (s * 2) >= 16) s *= 2;
-  return s;
-}
-
-// thread t: channel pair p = t % P of the group, rows r0 = t / P, stride R = 256 / P
-__global__ void __launch_bounds__(256) k_gn_stats(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                  int c1, int hw, int c, int groups, int S,
-                                                  float* __restrict__ part) {
-  __shared__ float red[8];
-  const int slab = blockIdx.x;  // n * groups + g
-  const int n = slab / groups, g = slab % groups;
-  const int cg = c / groups, P = cg >> 1, R = 256 / P;
-  const int t = threadIdx.x;
-  const int rows = (hw + S - 1) / S;
-  const int ra = blockIdx.y * rows, rb = min(hw, ra + rows);
-  const long rowbase = (long)n * hw;
-  const float x0 = (float)*gn_src(x, x2, c1, c, rowbase, g * cg);  // shift (same for all S blocks)
-  float s1 = 0.f, s2 = 0.f;
-  if (t < P * R) {
-    const int ch = g * cg + 2 * (t % P);
-    for (int r = ra + t / P; r < rb; r += R) {
-      const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
-      const float a = __low2float(v) - x0, b = __high2float(v) - x0;
-      s1 += a + b;
-      s2 += a * a + b * b;
-    }
-  }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  if ((t & 63) == 0) {
-    red[t >> 6] = s1;
-    red[4 + (t >> 6)] = s2;
-  }
-  __syncthreads();
-  if (t == 0) {
-    float* o = part + ((long)slab * S + blockIdx.y) * 3;
-    o[0] = (red[0] + red[1]) + (red[2] + red[3]);
-    o[1] = (red[4] + red[5]) + (red[6] + red[7]);
-    o[2] = x0;
-  }
-}
-
-__global__ void k_gn_coeff(const float* __restrict__ part, int n, int hw, int c, int groups, int S, float eps,
-                           const f16* __restrict__ gamma, const f16* __restrict__ beta,
-                           float2* __restrict__ coef, float* __restrict__ amax) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n * c) return;
-  amax[i] = 0.f;  // the amax pass that follows accumulates into it (no separate zero-fill launch)
-  const int ni = i / c, ch = i % c;
-  const int cg = c / groups, g = ch / cg;
-  const float* p = part + ((long)(ni * groups + g) * S) * 3;
-  float s1 = 0.f, s2 = 0.f;
-  for (int k = 0; k < S; ++k) {
-    s1 += p[3 * k];
-    s2 += p[3 * k + 1];
-  }
-  const float cnt = (float)cg * (float)hw;
-  const float m = s1 / cnt;                          // mean of the shifted values
-  const float var = fmaxf(s2 / cnt - m * m, 0.f);    // population variance
-  const float mean = m + p[2];
-  const float rstd = 1.0f / sqrtf(var + eps);
-  const float sc = rstd * (float)gamma[ch];
-  coef[i] = make_float2(sc, fmaf(-sc, mean, (float)beta[ch]));
+struct GnGeom {
+  int bx, by, gx, z, rpb;  // streaming passes
+  int bys, zs, rpbs;       // stats / amax passes: 1024-thread blocks, 4 rows per thread
+};
+static GnGeom gn_geom(int n, int hw, int c) {
+  GnGeom g;
+  const int chunks = c / 8;
+  g.bx = std::min(chunks, 256);
+  g.by = 256 / g.bx;
+  g.gx = (chunks + g.bx - 1) / g.bx;
+  g.rpb = g.by * 4;  // >= 4 rows per thread, more blocks while the grid is small
+  while (g.rpb > g.by && (long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) < 2048) g.rpb /= 2;
+  while ((long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) > 8192) g.rpb *= 2;
+  g.z = (hw + g.rpb - 1) / g.rpb;
+  g.bys = std::max(1, 1024 / g.bx);
+  g.rpbs = g.bys * 4;
+  g.zs = (hw + g.rpbs - 1) / g.rpbs;
+  return g;
 }
 
 __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
@@ -101,39 +60,182 @@ __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
   return (float)o;
 }
 
-__global__ void __launch_bounds__(256) k_gn_amax(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                 int c1, int hw, int c, int groups, int S,
-                                                 const float2* __restrict__ coef, int silu,
-                                                 float* __restrict__ amax) {
-  __shared__ float red[2][256];
-  const int slab = blockIdx.x;
-  const int n = slab / groups, g = slab % groups;
-  const int cg = c / groups, P = cg >> 1, R = 256 / P;
-  const int t = threadIdx.x;
-  const int rows = (hw + S - 1) / S;
-  const int ra = blockIdx.y * rows, rb = min(hw, ra + rows);
-  const long rowbase = (long)n * hw;
-  float m0 = 0.f, m1 = 0.f;
-  const int ch = g * cg + 2 * (t % P);
-  if (t < P * R) {
-    const float2 k0 = coef[(long)n * c + ch], k1 = coef[(long)n * c + ch + 1];
-    for (int r = ra + t / P; r < rb; r += R) {
-      const __half2 v = *reinterpret_cast<const __half2*>(gn_src(x, x2, c1, c, rowbase + r, ch));
-      m0 = fmaxf(m0, fabsf(gn_out(__low2float(v), k0, silu)));
-      m1 = fmaxf(m1, fabsf(gn_out(__high2float(v), k1, silu)));
+__global__ void __launch_bounds__(1024) k_gn_stats(const f16* __restrict__ x, const f16* __restrict__ x2,
+                                                   int c1, int hw, int c, int cg, int rows_per_block,
+                                                   float4* __restrict__ part) {
+  __shared__ float2 red[1024][8];
+  const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
+  const int chunk = blockIdx.x * bx + tx;
+  const bool active = chunk * 8 < c;
+  const int ch = chunk * 8;
+  const long n = blockIdx.y;
+  const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
+  float s1[8], s2[8], sh[8], mn[8], mx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1[j] = s2[j] = 0.f;
+    mn[j] = INFINITY;
+    mx[j] = -INFINITY;
+    sh[j] = active ? (float)*gn_src(x, x2, c1, c, n * hw, (ch + j) / cg * cg) : 0.f;
+  }
+  if (active) {
+    for (int r = r0 + ty; r < r1; r += by) {
+      const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, n * hw + r, ch));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xv = (float)v[j];
+        const float a = xv - sh[j];
+        s1[j] += a;
+        s2[j] = fmaf(a, a, s2[j]);
+        mn[j] = fminf(mn[j], xv);
+        mx[j] = fmaxf(mx[j], xv);
+      }
     }
   }
-  red[0][t] = m0;
-  red[1][t] = m1;
+  const int t = ty * bx + tx;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = make_float2(s1[j], s2[j]);
   __syncthreads();
-  if (t < P) {
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < R; ++i) {
-      a = fmaxf(a, red[0][t + i * P]);
-      b = fmaxf(b, red[1][t + i * P]);
+  if (ty == 0 && active)
+    for (int k = 1; k < by; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float2 o = red[k * bx + tx][j];
+        s1[j] += o.x;
+        s2[j] += o.y;
+      }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = make_float2(mn[j], mx[j]);
+  __syncthreads();
+  if (ty == 0 && active) {
+    for (int k = 1; k < by; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float2 o = red[k * bx + tx][j];
+        mn[j] = fminf(mn[j], o.x);
+        mx[j] = fmaxf(mx[j], o.y);
+      }
+    float4* dst = part + ((n * gridDim.z + blockIdx.z) * c + ch);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j] = make_float4(s1[j], s2[j], mn[j], mx[j]);
+  }
+}
+
+// largest |silu| of any input: silu(-1.2785) = -0.27846; a |half(silu(.))| >= this bound can only
+// come from the positive branch, where the rounded GN+SiLU output is non-decreasing in z
+constexpr float SILU_NEG_BOUND = 0.2786f;
+
+// One block per (n, group): group mean / rstd from the partials (fixed thread -> partial map,
+// fixed reduction tree: deterministic), then per channel the affine coefficients and - when the
+// output is fake-quantized - its exact amax from the channel's min / max input:
+// out = half([silu](half(x * a + b))) is monotone in x on each side of silu's minimum, so
+// max |out| is |out(x_min)| or |out(x_max)| except when SiLU is on and both extremes map below
+// the bound above; those channels are flagged for the (rare) full amax pass.
+__global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, const f16* __restrict__ x,
+                                                  const f16* __restrict__ x2, int c1, int hw, int c, int cg,
+                                                  int Z, float eps, const f16* __restrict__ gamma,
+                                                  const f16* __restrict__ beta, int silu, int quant,
+                                                  float2* __restrict__ coef, float* __restrict__ amax,
+                                                  int* __restrict__ flag) {
+  __shared__ float red[2][4];
+  __shared__ float stat[2];
+  const int groups = c / cg;
+  const int ni = blockIdx.x / groups, g0 = (blockIdx.x % groups) * cg;
+  const int t = threadIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  for (int e = t; e < Z * cg; e += 256) {
+    const int z = e / cg, j = e - z * cg;
+    const float4 v = part[((long)ni * Z + z) * c + g0 + j];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = s1;
+    red[1][t >> 6] = s2;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const float S1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    const float S2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    const float cnt = (float)cg * (float)hw;
+    const float m = S1 / cnt;                        // mean of the shifted values
+    const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
+    stat[0] = m + (float)*gn_src(x, x2, c1, c, (long)ni * hw, g0);
+    stat[1] = 1.0f / sqrtf(var + eps);
+  }
+  __syncthreads();
+  for (int j = t; j < cg; j += 256) {
+    const int ch = g0 + j;
+    const long i = (long)ni * c + ch;
+    const float sc = stat[1] * (float)gamma[ch];
+    const float2 k = make_float2(sc, fmaf(-sc, stat[0], (float)beta[ch]));
+    coef[i] = k;
+    if (!quant) continue;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int z = 0; z < Z; ++z) {
+      const float4 v = part[((long)ni * Z + z) * c + ch];
+      mn = fminf(mn, v.z);
+      mx = fmaxf(mx, v.w);
     }
-    atomic_max_pos(&amax[(long)n * c + ch], a);
-    atomic_max_pos(&amax[(long)n * c + ch + 1], b);
+    const float lo = fabsf(gn_out(mn, k, silu)), hi = fabsf(gn_out(mx, k, silu));
+    const float top = fabsf(gn_out(sc >= 0.f ? mx : mn, k, silu));  // largest z
+    if (!silu) {
+      amax[i] = fmaxf(lo, hi);
+      flag[i] = 0;
+    } else if (top >= SILU_NEG_BOUND) {
+      amax[i] = top;
+      flag[i] = 0;
+    } else {
+      amax[i] = 0.f;  // computed by k_gn_amax
+      flag[i] = 1;
+    }
+  }
+}
+
+// fallback amax pass: only blocks owning a flagged channel stream their rows
+__global__ void __launch_bounds__(1024) k_gn_amax(const f16* __restrict__ x, const f16* __restrict__ x2,
+                                                  int c1, int hw, int c, int rows_per_block,
+                                                  const float2* __restrict__ coef, int silu,
+                                                  const int* __restrict__ flag, float* __restrict__ amax) {
+  __shared__ float red[1024][8];
+  const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
+  const int chunk = blockIdx.x * bx + tx;
+  const bool active = chunk * 8 < c;
+  const int ch = chunk * 8;
+  const long n = blockIdx.y;
+  int any = 0;
+  if (active)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) any |= flag[n * c + ch + j];
+  if (!__syncthreads_or(any)) return;  // block-uniform
+  const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
+  float m[8];
+  float2 k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = 0.f;
+    k[j] = any ? coef[n * c + ch + j] : make_float2(0.f, 0.f);
+  }
+  if (any)
+    for (int r = r0 + ty; r < r1; r += by) {
+      const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, n * hw + r, ch));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf(gn_out((float)v[j], k[j], silu)));
+    }
+  const int t = ty * bx + tx;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = m[j];
+  __syncthreads();
+  if (ty == 0 && any) {
+    for (int q = 1; q < by; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], red[q * bx + tx][j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (flag[n * c + ch + j]) atomic_max_pos(&amax[n * c + ch + j], m[j]);
   }
 }
 
@@ -171,8 +273,8 @@ __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, con
 }
 
 extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
-  const int S = gn_splits((long)n * groups, hw);
-  return n * groups * S * 3 + 1 + 3 * n * c;  // partials, float2 alignment pad, coef, amax
+  const GnGeom g = gn_geom(n, hw, c);
+  return 4 * n * g.zs * c + 2 * n * c + n * c + n * c;  // partials (float4), coef (float2), amax, flags
 }
 
 extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
@@ -180,36 +282,30 @@ extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw
                             void* y, float* ws, void* stream) {
   QD_REQUIRE(x && gamma && beta && y && ws, "null pointer");
   QD_REQUIRE(groups > 0 && c % groups == 0, "groups must divide C");
-  const int cg = c / groups;
-  QD_REQUIRE(cg % 2 == 0 && cg <= 512, "channels per group must be even and <= 512");
   QD_REQUIRE(c % 8 == 0, "GroupNorm needs C % 8 == 0");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "workspace must be 16-B aligned");
   if (x2) QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c, "bad concat split (must be a multiple of 8)");
   else c1 = c;
   QD_REQUIRE(q_bits == 0 || (q_bits >= 2 && q_bits <= 16), "bad q_bits");
   if ((long)n * hw == 0) return 0;
   hipStream_t st = S(stream);
-  const int S_ = gn_splits((long)n * groups, hw);
-  float* part = ws;
-  float2* coef = reinterpret_cast<float2*>(ws + (long)n * groups * S_ * 3 + ((n * groups * S_ * 3) & 1));
+  const int cg = c / groups;
+  const GnGeom g = gn_geom(n, hw, c);
+  float4* part = reinterpret_cast<float4*>(ws);
+  float2* coef = reinterpret_cast<float2*>(part + (long)n * g.zs * c);
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
-  dim3 sg(n * groups, S_);
-  k_gn_stats<<<sg, 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, S_, part);
-  k_gn_coeff<<<grid1((long)n * c), 256, 0, st>>>(part, n, hw, c, groups, S_, eps, (const f16*)gamma,
-                                                 (const f16*)beta, coef, amax);
+  int* flag = reinterpret_cast<int*>(amax + (long)n * c);
+  const dim3 grid(g.gx, n, g.z), block(g.bx, g.by);
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
-  if (qmax) {
-    k_gn_amax<<<sg, 256, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, groups, S_, coef, silu, amax);
-  }
-  {
-    const int chunks = c / 8;
-    const int bx = std::min(chunks, 256), by = 256 / bx, gx = (chunks + bx - 1) / bx;
-    int rpb = by * 4;  // >= 4 rows per thread, more blocks while the grid is small
-    while (rpb > by && (long)gx * n * ((hw + rpb - 1) / rpb) < 2048) rpb /= 2;
-    while ((long)gx * n * ((hw + rpb - 1) / rpb) > 8192) rpb *= 2;
-    dim3 grid(gx, n, (hw + rpb - 1) / rpb);
-    k_gn_apply<<<grid, dim3(bx, by), 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, rpb, coef, silu, qmax,
-                                              amax, (f16*)y);
-  }
+  k_gn_stats<<<dim3(g.gx, n, g.zs), dim3(g.bx, g.bys), 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, cg, g.rpbs,
+                                                                 part);
+  k_gn_coeff<<<n * groups, 256, 0, st>>>(part, (const f16*)x, (const f16*)x2, c1, hw, c, cg, g.zs, eps,
+                                         (const f16*)gamma, (const f16*)beta, silu, qmax > 0, coef, amax, flag);
+  if (qmax && silu)  // only channels whose extremes cannot bound the SiLU output stream here
+    k_gn_amax<<<dim3(g.gx, n, g.zs), dim3(g.bx, g.bys), 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, g.rpbs,
+                                                                  coef, silu, flag, amax);
+  k_gn_apply<<<grid, block, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, g.rpb, coef, silu, qmax, amax,
+                                     (f16*)y);
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -18,6 +18,7 @@ NCHW, NHWC = 0, 1
 WFMT = {"f16": 0, "i8": 1, "i4": 2}
 EPI_BIAS, EPI_RESIDUAL, EPI_AMAX = 1, 2, 4
 EPI_AMAX_ZEROED = 16
+EPI_GEGLU = 8
 GRAN_ZEROED = 0x100
 
 
@@ -134,8 +135,10 @@ def conv_weight_khwc(w, ci_pad):
 
 # ---------------------------------------------------------------- GEMMs
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
-           amax=None, rows_per_sample=0, amax_zeroed=False):
-    """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K)."""
+           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False):
+    """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K).
+    geglu: W rows (and bias) interleaved in 16-row [hidden | gate] blocks (geglu_interleave);
+    returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue)."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
         raise ValueError("x must be an fp16 HIP tensor")
     if x2d.dim() != 2 or x2d.stride(1) != 1:
@@ -143,9 +146,10 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     M, K = x2d.shape
     N = weight.shape[0]
     if out is None:
-        out = _empty((M, N), torch.float16, x2d.device)
+        out = _empty((M, N // 2 if geglu else N), torch.float16, x2d.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
-          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0)
+          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
+          (EPI_GEGLU if geglu else 0)
     if residual is not None:
         _chk(residual, "residual")
     ws, wsn = _gemm_ws(M, N, K, WFMT[wfmt], rows_per_sample, epi, x2d.device)
@@ -153,6 +157,15 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
               _p(bias), _p(residual), _p(out), N, out.stride(0), epi, _p(amax), rows_per_sample,
               _p(ws), wsn, _stream())
     return out
+
+
+def geglu_interleave_rows(n2, device):
+    """Row permutation for the fused GEGLU epilogue: 16-row blocks [hidden b | gate b]."""
+    half = n2 // 2
+    if half % 16:
+        raise ValueError("GEGLU fusion needs the hidden width to be a multiple of 16")
+    idx = torch.arange(half, device=device).view(-1, 16)
+    return torch.stack([idx, idx + half], 1).reshape(-1)
 
 
 def _gemm_ws(M, N, K, wfmt, rows_per_sample, epi, device):

@@ -411,6 +411,38 @@ def run_linear(layer, x2d, residual=None):
     return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual)
 
 
+def _geglu_operand(layer):
+    """(weight, fmt, scales, group, bias) of ff.net[0].proj with rows interleaved for the fused
+    GEGLU epilogue; cached on the module, rebuilt when the underlying buffers change."""
+    if isinstance(layer, WxAxLinear):
+        w, fmt, sc, g = layer.gemm_weight()
+    else:
+        w, fmt, sc, g = _f16(layer.weight), "f16", None, 0
+    b = layer.bias
+    ver = (w.data_ptr(), w._version, None if sc is None else (sc.data_ptr(), sc._version),
+           None if b is None else (b.data_ptr(), b._version))
+    cache = getattr(layer, "_qd_geglu", None)
+    if cache is not None and cache[0] == ver:
+        return cache[1]
+    perm = K.geglu_interleave_rows(w.shape[0], w.device)
+    op = (w[perm].contiguous(), fmt, None if sc is None else sc[perm].contiguous(), g,
+          None if b is None else b.detach()[perm].contiguous())
+    layer._qd_geglu = (ver, op)
+    return op
+
+
+def ff_geglu(layer, x2d):
+    """diffusers GEGLU(proj) = h * gelu(g) with (h, g) = proj(x).chunk(2): one GEMM, fused epilogue."""
+    if isinstance(layer, WxAxLinear) and layer.output_quant_name != "None":
+        return K.geglu(run_linear(layer, x2d))  # output fake-quant sits between proj and GEGLU
+    hook = getattr(layer, "_qd_hook", None)
+    if hook is not None:  # SmoothQuant calibration observes the projection input
+        hook(x2d)
+    xin = layer.act_quant(x2d) if isinstance(layer, WxAxLinear) and layer.quantize_act else x2d
+    w, fmt, sc, g, b = _geglu_operand(layer)
+    return K.linear(xin, w, fmt, sc, g, bias=b, geglu=True)
+
+
 def resnet_fwd(res, x, temb_silu, skip=None):
     """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1)."""
     xin = K.concat_c(x, skip) if skip is not None else x
@@ -461,5 +493,5 @@ def block_fwd(blk, t, n, s, ctx_kv):
     o = K.attention(q, k, v, a2.heads)
     t = run_linear(a2.to_out[0], o.view(-1, c), residual=t)
     h = K.layernorm(t, blk.norm3.eps, _f16(blk.norm3.weight), _f16(blk.norm3.bias))
-    g = K.geglu(run_linear(blk.ff.net[0].proj, h))
+    g = ff_geglu(blk.ff.net[0].proj, h)
     return run_linear(blk.ff.net[2], g, residual=t)

@@ -163,6 +163,36 @@ def test_linear_formats(M, N, Kd, fmt, dev):
     assert ((y - yf).abs() <= tol).all(), (y - yf).abs().max().item()
 
 
+@pytest.mark.parametrize("M,I,Kd,fmt", [(256, 1280, 320, "f16"), (1000, 640, 640, "i8"), (64, 2560, 1280, "i4")])
+def test_linear_geglu_epilogue(M, I, Kd, fmt, dev):
+    k = K()
+    g = torch.Generator().manual_seed(M + I)
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(2 * I, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+    b = torch.randn(2 * I, generator=g).half().to(dev)
+    gs = FQ.shrink_group(Kd, 128)
+    codes, scales, wdq = k.weight_quant(w, gs, 4 if fmt == "i4" else 8)
+    if fmt == "f16":
+        op, sc, grp = wdq, None, 0
+    elif fmt == "i8":
+        op, sc, grp = codes, scales, gs
+    else:
+        op, sc, grp = k.pack_int4(codes), scales, gs
+    perm = k.geglu_interleave_rows(2 * I, dev)
+    fused = k.linear(x, op[perm].contiguous(), fmt, None if sc is None else sc[perm].contiguous(), grp,
+                     bias=b[perm].contiguous(), geglu=True).cpu().float()
+    y = k.linear(x, op, fmt, sc, grp, bias=b)
+    unfused = k.geglu(y).cpu().float()
+    pre = (x.float().cpu() @ wdq.cpu().float().t() + b.float().cpu()).half().float()
+    h, gt = pre.chunk(2, -1)
+    ref = (h * F.gelu(gt).half().float()).half().float()
+    # same accumulation -> identical up to the planner's tile choice (1-ulp of the projection)
+    # a 1-ulp move of h or g propagates as ulp(h)*|gelu(g)| + |h|*ulp(g)*|gelu'(g)| (gelu' <= 1.13)
+    tol = 2 * ulp16(ref) + 2 * ulp16(h) * gt.abs() + 2.5 * h.abs() * ulp16(gt) + 1e-3
+    assert ((fused - ref).abs() <= tol).all(), (fused - ref).abs().max().item()
+    assert ((fused - unfused).abs() <= tol).all()
+
+
 def test_linear_amax_epilogue(dev):
     k = K()
     g = torch.Generator().manual_seed(1)
