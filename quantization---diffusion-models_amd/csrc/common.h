@@ -37,6 +37,18 @@ __device__ __forceinline__ f16 fq_apply(float x, float s) {
   return (f16)(q * s);
 }
 
+// fq_apply with the division replaced by a product with rs = 1.0 / (double)s (computed once per
+// channel).  Exact: x and s are fp16 values, so x / s either terminates within 11 significant
+// bits (then the f64 product, off by <= 2^-52 relative, rounds to it exactly) or lies >= ~2^-36
+// (relative) away from every f32 rounding midpoint, far outside the f64 product's error; the f32
+// rounding - and hence the fp16 one - equals that of the IEEE f32 quotient.  s == 0 (16-bit
+// quant of an all-zero channel) gives rs = inf and the same inf / NaN as the division.
+__device__ __forceinline__ f16 fq_apply_r(float x, float s, double rs) {
+  f16 t = (f16)(float)((double)x * rs);
+  float q = __builtin_rintf((float)t);
+  return (f16)(q * s);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -254,10 +254,12 @@ __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, con
   const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
   float2 k[8];
   float sq[8];
+  double rq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     k[j] = coef[n * c + ch + j];
     sq[j] = qmax > 0 ? fq_scale(amax[n * c + ch + j], qmax) : 0.f;
+    rq[j] = qmax > 0 ? 1.0 / (double)sq[j] : 0.0;
   }
   for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
     const long row = n * hw + r;
@@ -266,7 +268,7 @@ __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, con
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float val = gn_out((float)v[j], k[j], silu);
-      o[j] = qmax > 0 ? fq_apply(val, sq[j]) : (f16)val;
+      o[j] = qmax > 0 ? fq_apply_r(val, sq[j], rq[j]) : (f16)val;
     }
     *reinterpret_cast<f16x8*>(y + row * c + ch) = o;
   }

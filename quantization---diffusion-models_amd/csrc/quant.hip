@@ -143,20 +143,48 @@ __global__ void k_patchmax(const f16* __restrict__ x, int nc, int h, int w, int 
 // ---------------------------------------------------------------------------------------
 
 // NHWC per-channel apply: 8 channels per thread (c % 8 == 0).
+// channel-chunk x rows geometry (as the GroupNorm passes): thread (tx, ty) owns the 8-channel
+// chunk blockIdx.x * bx + tx of sample blockIdx.y, rows ty, ty + by, ... of row range blockIdx.z;
+// the per-channel fake-quant scales (and their f64 reciprocals) are computed once per thread.
+struct CrGeom {
+  int bx, by, gx, z, rpb;
+};
+static CrGeom cr_geom(int n, long hw, int c) {
+  CrGeom g;
+  const int chunks = c / 8;
+  g.bx = chunks < 256 ? chunks : 256;
+  g.by = 256 / g.bx;
+  g.gx = (chunks + g.bx - 1) / g.bx;
+  g.rpb = g.by * 4;
+  while (g.rpb > g.by && (long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) < 2048) g.rpb /= 2;
+  while ((long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) > 8192) g.rpb *= 2;
+  g.z = (int)((hw + g.rpb - 1) / g.rpb);
+  return g;
+}
+
 __global__ void __launch_bounds__(256) k_apply_nhwc(const f16* __restrict__ x, f16* __restrict__ y,
-                                                    long count8, int hw, int c, int c_valid, int qmax,
+                                                    int hw, int c, int c_valid, int qmax, int rows_per_block,
                                                     const float* __restrict__ amax) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= count8) return;
-  const long e = i * 8;
-  const int ch = (int)(e % c);
-  const long n = e / ((long)hw * c);
-  f16x8 v = *reinterpret_cast<const f16x8*>(x + e);
-  const float* a = amax + n * c + ch;
-  f16x8 o;
+  const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (chunk * 8 >= c) return;
+  const int ch = chunk * 8;
+  const long n = blockIdx.y;
+  const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
+  float sc[8];
+  double rs[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = ch + j < c_valid ? fq_apply((float)v[j], fq_scale(a[j], qmax)) : v[j];
-  *reinterpret_cast<f16x8*>(y + e) = o;
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = fq_scale(amax[n * c + ch + j], qmax);
+    rs[j] = 1.0 / (double)sc[j];
+  }
+  for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
+    const long e = (n * hw + r) * c + ch;
+    const f16x8 v = *reinterpret_cast<const f16x8*>(x + e);
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = ch + j < c_valid ? fq_apply_r((float)v[j], sc[j], rs[j]) : v[j];
+    *reinterpret_cast<f16x8*>(y + e) = o;
+  }
 }
 
 // generic apply with a scale index computed per element:
@@ -247,7 +275,9 @@ static int launch_apply(const void* x, void* y, int layout, int n, int c, int h,
   if (gran == QD_GRAN_PER_CHANNEL && layout == QD_LAYOUT_NHWC) {
     QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
     const int c_valid = group > 0 ? std::min(group, c) : c;
-    k_apply_nhwc<<<grid1(count / 8), 256, 0, st>>>((const f16*)x, (f16*)y, count / 8, (int)hw, c, c_valid, qm, amax);
+    const CrGeom g = cr_geom(n, hw, c);
+    k_apply_nhwc<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>((const f16*)x, (f16*)y, (int)hw, c, c_valid, qm,
+                                                                   g.rpb, amax);
   } else if (gran == QD_GRAN_PER_CHANNEL) {
     k_apply_generic<<<grid1(count), 256, 0, st>>>((const f16*)x, (f16*)y, count, 0, hw, h, w, 1, qm, amax);
   } else if (gran == QD_GRAN_PER_TOKEN) {
@@ -414,33 +444,43 @@ extern "C" int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw
 // conv-output finalize: out = half(fq(y) + residual | + chan_add[n][c])
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, const float* __restrict__ amax,
-                                                  long count8, int hw, int c, int qmax,
+                                                  int hw, int c, int qmax, int rows_per_block,
                                                   const f16* __restrict__ res,
                                                   const f16* __restrict__ cadd, f16* __restrict__ out) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= count8) return;
-  const long e = i * 8;
-  const int ch = (int)(e % c);
-  const long n = e / ((long)hw * c);
-  f16x8 v = *reinterpret_cast<const f16x8*>(y + e);
-  f16x8 o;
-  if (qmax > 0) {
-    const float* a = amax + n * c + ch;
+  const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (chunk * 8 >= c) return;
+  const int ch = chunk * 8;
+  const long n = blockIdx.y;
+  const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
+  float sc[8];
+  double rs[8];
+  f16x8 ca = {};
+  if (cadd && !res) ca = *reinterpret_cast<const f16x8*>(cadd + n * c + ch);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = fq_apply((float)v[j], fq_scale(a[j], qmax));
-  } else {
-    o = v;
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = qmax > 0 ? fq_scale(amax[n * c + ch + j], qmax) : 0.f;
+    rs[j] = qmax > 0 ? 1.0 / (double)sc[j] : 0.0;
   }
-  if (res) {
-    f16x8 r = *reinterpret_cast<const f16x8*>(res + e);
+  for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
+    const long e = (n * hw + r) * c + ch;
+    const f16x8 v = *reinterpret_cast<const f16x8*>(y + e);
+    f16x8 o;
+    if (qmax > 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)r[j]);
-  } else if (cadd) {
-    f16x8 r = *reinterpret_cast<const f16x8*>(cadd + n * c + ch);
+      for (int j = 0; j < 8; ++j) o[j] = fq_apply_r((float)v[j], sc[j], rs[j]);
+    } else {
+      o = v;
+    }
+    if (res) {
+      const f16x8 rr = *reinterpret_cast<const f16x8*>(res + e);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)r[j]);
+      for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)rr[j]);
+    } else if (cadd) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)ca[j]);
+    }
+    *reinterpret_cast<f16x8*>(out + e) = o;
   }
-  *reinterpret_cast<f16x8*>(out + e) = o;
 }
 
 extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
@@ -448,11 +488,12 @@ extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, i
   QD_REQUIRE(y && out, "null pointer");
   QD_REQUIRE(c % 8 == 0, "finalize needs C % 8 == 0");
   QD_REQUIRE(n_bits == 0 || (amax && n_bits >= 2 && n_bits <= 16), "bad n_bits / amax");
-  const long count8 = (long)n * hw * c / 8;
-  if (count8 == 0) return 0;
-  k_finalize<<<grid1(count8), 256, 0, S(stream)>>>((const f16*)y, amax, count8, hw, c,
-                                                   n_bits ? qmax_of(n_bits) : 0, (const f16*)residual,
-                                                   (const f16*)chan_add, (f16*)out);
+  if ((long)n * hw * c == 0) return 0;
+  const CrGeom g = cr_geom(n, hw, c);
+  k_finalize<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, S(stream)>>>((const f16*)y, amax, hw, c,
+                                                                      n_bits ? qmax_of(n_bits) : 0, g.rpb,
+                                                                      (const f16*)residual, (const f16*)chan_add,
+                                                                      (f16*)out);
   QD_CHECK_LAUNCH();
   return 0;
 }
