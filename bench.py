@@ -92,8 +92,18 @@ def dominant_kernel_roofline(dev, iters=20):
     return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": (pmc_traffic() or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": pmc_traffic(),
-            "kernel": "k_gemm<AM_CONV,F16> conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880)",
+            "kernel": "conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880) implicit GEMM",
+            "kernel_choice": _conv_choice(),
             "avg_us": round(ms * 1e3, 2)}
+
+
+def _conv_choice():
+    """GEMM family chosen for the dominant conv ((weight op, qd_gemm_force id); >= 100 = LDS-DMA)."""
+    from qdiff import kernels as K
+    for key, c in K.gemm_choices().items():
+        if key[:8] == ("conv", 8, 64, 64, 320, 320, 3, 3):
+            return {"variant": c[1], "family": "k_gemm_dma" if c[1] >= 100 else "k_gemm"} if c else None
+    return None
 
 
 def pmc_traffic():

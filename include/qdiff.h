@@ -104,6 +104,12 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
                   void* y, int N, int ldy, int epi, float* amax, int rows_per_sample,
                   float* ws, long ws_elems, void* stream);
 
+/* Tuning / test knob (process-global, not thread-safe): force the GEMM kernel family of every
+ * following qd_linear_fwd / qd_conv2d_fwd.  -1 = planner's choice (default); 0..3 = the
+ * register-staged tiles 128x160, 128x128, 128x64, 64x64; 100 + i = LDS-DMA variant i (F16
+ * weights only; quantized formats keep the planner's register-staged choice). */
+int qd_gemm_force(int variant);
+
 /* fp32 elements of split-K workspace the GEMM plans for this shape (0: runs unsplit).  Pass
  * at least that much as (ws, ws_elems) to qd_linear_fwd / qd_conv2d_fwd (conv: M = N*Ho*Wo,
  * K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo); with less (or NULL) the call runs unsplit. */

@@ -44,6 +44,7 @@ SIGNATURES = {
     "qd_cfg_ddim_step": [P, P, I, I64, F, P, P, P, P, I, I, P],
     "qd_channel_absmax_accum": [P, I64, I, P, P, P, P],
     "qd_smooth_fold": [P, P, P, P, I, I, P, F, P, P, P],
+    "qd_gemm_force": [I],
 }
 
 # size queries (no status code)

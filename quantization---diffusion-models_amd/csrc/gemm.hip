@@ -292,80 +292,13 @@ __device__ __forceinline__ float rowgroup_max(float v) {
   return v;
 }
 
-// ---- kernel -----------------------------------------------------------------------------
-template <int BM, int BN, int AMODE, int BFMT, bool SPLIT>
-__global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ASZ = BM * BK, BSZ = BN * BK;
-  __shared__ __attribute__((aligned(16))) f16 smem[2 * (ASZ + BSZ)];
-
-  // XCD-aware bijective remap of the linear block id (MI355X_MICROARCH: blocks b, b+8 share an XCD)
-  const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
-  const int ntile = nbm * nbn;
-  const int nwg = ntile * p.splits;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
-  const int m0 = bm * BM, n0 = bn * BN;
-  const int kbeg = split * p.kps;
-  const int kend = min(p.K, kbeg + p.kps);
-
+// ---- shared epilogue ----------------------------------------------------------------------
+// acc[i][j]: C^T fragment (rows n = n0 + wn0 + 16j + 4fq + r, column m = m0 + wm0 + 16i + fr).
+template <int BM, int BN, int NT, int TM, int TN, bool SPLIT>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM][TN], f16* smem, int m0, int n0,
+                                              int wm0, int wn0, int split) {
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
   const int fr = lane & 15, fq = lane >> 4;
-
-  ALoader<BM, AMODE> al;
-  BLoader<BN, BFMT> bl;
-  al.init(p, m0, kbeg);
-  bl.init(p, n0);
-
-  // acc[i][j]: C^T tile (rows n = n0 + wn0 + 16j + 4fq + r, column m = m0 + wm0 + 16i + fr)
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (kend - kbeg + BK - 1) / BK;
-  al.load(p, kbeg);
-  bl.load(p, kbeg);
-  al.store(smem);
-  bl.store(smem + ASZ);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      al.load(p, kbeg + (kt + 1) * BK);
-      bl.load(p, kbeg + (kt + 1) * BK);
-    }
-    const f16* As = smem + cur * (ASZ + BSZ);
-    const f16* Bs = As + ASZ;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      f16x8 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz(wm0 + i * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz(wn0 + j * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) {
-      f16* nx = smem + (cur ^ 1) * (ASZ + BSZ);
-      al.store(nx);
-      bl.store(nx + ASZ);
-    }
-    __syncthreads();
-  }
-
   if constexpr (SPLIT) {
     // fp32 partial slab [split][M][N]
     float* part = p.part + (long)split * p.M * p.N;
@@ -456,7 +389,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
     const int cpr = geglu ? BN / 16 : BN / 8;
     const int on0 = geglu ? n0 >> 1 : n0, oN = geglu ? p.N >> 1 : p.N;
 #pragma unroll 2
-    for (int e = threadIdx.x; e < BM * cpr; e += 256) {
+    for (int e = threadIdx.x; e < BM * cpr; e += NT) {
       const int row = e / cpr, c = e - row * cpr;
       const int m = m0 + row, n = on0 + c * 8;
       if (m < p.M && n < oN) {
@@ -470,6 +403,354 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
       }
     }
   }
+}
+
+// ---- kernel -----------------------------------------------------------------------------
+template <int BM, int BN, int AMODE, int BFMT, bool SPLIT>
+__global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ASZ = BM * BK, BSZ = BN * BK;
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * (ASZ + BSZ)];
+
+  // XCD-aware bijective remap of the linear block id (MI355X_MICROARCH: blocks b, b+8 share an XCD)
+  const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int nwg = ntile * p.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = wg / p.splits, split = wg - tile * p.splits;
+  const int bm = tile / nbn, bn = tile - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int kbeg = split * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  ALoader<BM, AMODE> al;
+  BLoader<BN, BFMT> bl;
+  al.init(p, m0, kbeg);
+  bl.init(p, n0);
+
+  // acc[i][j]: C^T tile (rows n = n0 + wn0 + 16j + 4fq + r, column m = m0 + wm0 + 16i + fr)
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  al.load(p, kbeg);
+  bl.load(p, kbeg);
+  al.store(smem);
+  bl.store(smem + ASZ);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      al.load(p, kbeg + (kt + 1) * BK);
+      bl.load(p, kbeg + (kt + 1) * BK);
+    }
+    const f16* As = smem + cur * (ASZ + BSZ);
+    const f16* Bs = As + ASZ;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz(wm0 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz(wn0 + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      f16* nx = smem + (cur ^ 1) * (ASZ + BSZ);
+      al.store(nx);
+      bl.store(nx + ASZ);
+    }
+    __syncthreads();
+  }
+
+  gemm_epilogue<BM, BN, 256, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
+}
+
+// ---- LDS-DMA variant ----------------------------------------------------------------------
+// Operands go HBM/L2 -> LDS directly (buffer_load_dwordx4 ... lds): no staging registers, no
+// ds_write, and the loads of the next ST-1 K steps stay in flight across the per-step barrier
+// (counted vmcnt + raw s_barrier; __syncthreads would drain them).  A wave-instruction writes
+// 64 x 16 B lane-linearly = 8 LDS rows of 128 B; the XOR swizzle is applied on the SOURCE side
+// (lane l of the row group loads K chunk (l & 7) ^ (row & 7)), so fragments are read with the
+// same swz() as the register-staged kernel.  OOB chunks (rows past M/N, conv halo, K tail)
+// carry offsets >= 2^31 and land as zeros.  F16 B operand only (the reference's dequantized
+// buffer); quantized codes use the register-staged kernel, which dequantizes while staging.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, f16* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, (int)voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// thread (wave w, lane l), load slot j: wave-instruction g = j * NW + w covers rows 8g..8g+7;
+// lane l -> row 8g + (l >> 3), LDS chunk l & 7 holding K chunk (l & 7) ^ (l >> 3).
+template <int BM, int NT, int AMODE>
+struct ADma {
+  static constexpr int NW = NT / 64;
+  static constexpr int L = BM * 8 / NT;
+  static_assert(BM * 8 % NT == 0, "A tile rows must split evenly over the wave-instructions");
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned rowoff[L];
+  int pix[L], ih0[L], iw0[L];
+  int ky, kx, ci0, gc;
+
+  __device__ void init(const GemmArgs& p, int m0, int kbeg, int wid) {
+    rs = rsrc(p.a, p.a_bytes);
+    const int lane = threadIdx.x & 63;
+    gc = ((lane & 7) ^ (lane >> 3)) * 8;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int m = m0 + (j * NW + wid) * 8 + (lane >> 3);
+      const bool ok = m < p.M;
+      if (AMODE == AM_LINEAR) {
+        rowoff[j] = ok ? (unsigned)m * (unsigned)p.lda * 2u : OOB;
+      } else {
+        const int mm = ok ? m : 0;
+        const int ow = mm % p.Wo, oh = (mm / p.Wo) % p.Ho, n = mm / (p.Wo * p.Ho);
+        pix[j] = ok ? n * p.Hs * p.Ws : -1;
+        ih0[j] = oh * p.stride - p.pad;
+        iw0[j] = ow * p.stride - p.pad;
+      }
+    }
+    if (AMODE == AM_CONV) {
+      const int kpos = kbeg / p.Cip;
+      ci0 = kbeg - kpos * p.Cip;
+      ky = kpos / p.kw;
+      kx = kpos - ky * p.kw;
+    }
+  }
+  __device__ __forceinline__ unsigned conv_off(const GemmArgs& p, int j, int kyy, int kxx, int ci) const {
+    const int ih = ih0[j] + kyy, iw = iw0[j] + kxx;
+    const bool ok = pix[j] >= 0 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    const int sh = p.ups ? ih >> 1 : ih, sw = p.ups ? iw >> 1 : iw;
+    return ok ? (unsigned)((pix[j] + sh * p.Ws + sw) * p.Cip + ci) * 2u : OOB;
+  }
+  __device__ void issue(const GemmArgs& p, int k0, f16* sa, int wid) {
+    if (AMODE == AM_LINEAR) {
+      const unsigned ko = k0 + gc < p.K ? (unsigned)(k0 + gc) * 2u : OOB;
+#pragma unroll
+      for (int j = 0; j < L; ++j) glds16(rs, sa + (j * NW + wid) * 8 * BK, rowoff[j] + ko);
+    } else if (AMODE == AM_CONV) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) glds16(rs, sa + (j * NW + wid) * 8 * BK, conv_off(p, j, ky, kx, ci0 + gc));
+      ci0 += BK;
+      if (ci0 == p.Cip) {
+        ci0 = 0;
+        if (++kx == p.kw) {
+          kx = 0;
+          ++ky;
+        }
+      }
+    } else {
+      const int k = k0 + gc;
+      const int kpos = k / p.Cip, ci = k - kpos * p.Cip;
+      const int kyy = kpos / p.kw, kxx = kpos - kyy * p.kw;
+#pragma unroll
+      for (int j = 0; j < L; ++j)
+        glds16(rs, sa + (j * NW + wid) * 8 * BK, k < p.K ? conv_off(p, j, kyy, kxx, ci) : OOB);
+    }
+  }
+};
+
+template <int BN, int NT>
+struct BDma {
+  // BN / 8 row groups over NW waves; when they do not split evenly the first (BN / 8) % NW
+  // waves issue one wave-instruction more (wave-uniform guard; the per-wave count feeds vmcnt)
+  static constexpr int NW = NT / 64;
+  static constexpr int G = BN / 8;
+  static constexpr int L = (G + NW - 1) / NW;
+  static_assert(BN % 8 == 0, "B tile rows in groups of 8");
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned rowoff[L];
+  int gc;
+  __device__ static int count(int wid) { return G / NW + (wid < G % NW ? 1 : 0); }
+  __device__ void init(const GemmArgs& p, int n0, int wid) {
+    rs = rsrc(p.b, p.b_bytes);
+    const int lane = threadIdx.x & 63;
+    gc = ((lane & 7) ^ (lane >> 3)) * 8;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int n = n0 + (j * NW + wid) * 8 + (lane >> 3);
+      rowoff[j] = n < p.N ? (unsigned)n * (unsigned)p.K * 2u : OOB;
+    }
+  }
+  __device__ void issue(const GemmArgs& p, int k0, f16* sb, int wid) {
+    const unsigned ko = k0 + gc < p.K ? (unsigned)(k0 + gc) * 2u : OOB;
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (G % NW == 0 || j * NW + wid < G) glds16(rs, sb + (j * NW + wid) * 8 * BK, rowoff[j] + ko);
+  }
+};
+
+#define QD_VM_CASE(n) \
+  case n:             \
+    wait_vm<n>();     \
+    break;
+// vmcnt with a wave-uniform runtime count (immediate operand: one case per value)
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+    QD_VM_CASE(0) QD_VM_CASE(1) QD_VM_CASE(2) QD_VM_CASE(3) QD_VM_CASE(4) QD_VM_CASE(5) QD_VM_CASE(6)
+    QD_VM_CASE(7) QD_VM_CASE(8) QD_VM_CASE(9) QD_VM_CASE(10) QD_VM_CASE(11) QD_VM_CASE(12)
+    QD_VM_CASE(13) QD_VM_CASE(14) QD_VM_CASE(15) QD_VM_CASE(16) QD_VM_CASE(17) QD_VM_CASE(18)
+    QD_VM_CASE(19) QD_VM_CASE(20) QD_VM_CASE(21) QD_VM_CASE(22) QD_VM_CASE(23) QD_VM_CASE(24)
+    default: wait_vm<0>(); break;
+  }
+}
+#undef QD_VM_CASE
+
+// PIPE 0: per K step  wait(own loads of tile k) -> barrier -> issue tile k+ST-1 -> read + MFMA.
+// PIPE 1 (ST >= 3): the barrier sits between the two K=32 halves of a step, and the fragments
+//   of the next half are read while the current half's MFMAs run:
+//     MFMA(k, half 0) | read(k, half 1)  -> wait(tile k+1) -> barrier -> issue tile k+2 ->
+//     MFMA(k, half 1) | read(k+1, half 0)
+//   (the stage written after the barrier held tile k-1, whose last reads precede it).
+constexpr int dma_lds_halves(int bm, int bn, int st) {
+  return st * (bm + bn) * BK > bm * (bn + 8) ? st * (bm + bn) * BK : bm * (bn + 8);
+}
+// minimum waves per SIMD for __launch_bounds__: (blocks that fit the 160 KB LDS) x waves / 4
+constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt) {
+  return (163840 / (2 * dma_lds_halves(bm, bn, st))) * nt / 256 > 0 ? (163840 / (2 * dma_lds_halves(bm, bn, st))) * nt / 256 : 1;
+}
+
+template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int AMODE, bool SPLIT>
+__global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN))
+    k_gemm_dma(GemmArgs p) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ASZ = BM * BK, SSZ = (BM + BN) * BK;
+  constexpr int LDSZ = dma_lds_halves(BM, BN, ST);
+  static_assert(PIPE == 0 || ST >= 3, "split-phase pipeline needs >= 3 stages");
+  using AL = ADma<BM, NT, AMODE>;
+  using BL = BDma<BN, NT>;
+  __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
+
+  const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int nwg = ntile * p.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = wg / p.splits, split = wg - tile * p.splits;
+  const int bm = tile / nbn, bn = tile - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int kbeg = split * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int per = AL::L + BL::count(wid);  // this wave's loads per K step
+
+  AL al;
+  BL bl;
+  al.init(p, m0, kbeg, wid);
+  bl.init(p, n0, wid);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s) {
+    if (s < nk) {
+      al.issue(p, kbeg + s * BK, smem + s * SSZ, wid);
+      bl.issue(p, kbeg + s * BK, smem + s * SSZ + ASZ, wid);
+    }
+  }
+  auto read_frags = [&](const f16* As, int ks, f16x8 (&af)[TM], f16x8 (&bf)[TN]) {
+    const f16* Bs = As + ASZ;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz(wm0 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz(wn0 + j * 16 + fr, ks * 4 + fq));
+  };
+  auto mfmas = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+  };
+  auto sync = [&](int ahead) {  // own loads of the awaited tile landed, `ahead` later tiles in flight
+    wait_vm_rt(ahead * per);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if constexpr (PIPE == 0) {
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      sync(min(ST - 2, nk - 1 - kt));
+      if (kt + ST - 1 < nk) {
+        int nx = cur + ST - 1;
+        if (nx >= ST) nx -= ST;
+        al.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ, wid);
+        bl.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ + ASZ, wid);
+      }
+      f16x8 af[TM], bf[TN];
+      read_frags(smem + cur * SSZ, 0, af, bf);
+      mfmas(af, bf);
+      read_frags(smem + cur * SSZ, 1, af, bf);
+      mfmas(af, bf);
+      if (++cur == ST) cur = 0;
+    }
+  } else {
+    f16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+    if (nk > 0) {
+      sync(min(ST - 2, nk - 1));
+      read_frags(smem, 0, a0, b0);
+    }
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      int nxt = cur + 1;
+      if (nxt == ST) nxt = 0;
+      read_frags(smem + cur * SSZ, 1, a1, b1);
+      mfmas(a0, b0);
+      if (kt + 1 < nk) {
+        sync(min(ST - 3, nk - 2 - kt));  // tile kt+1 landed everywhere; tile kt-1 fully read
+        if (kt + ST - 1 < nk) {
+          int nx = cur + ST - 1;
+          if (nx >= ST) nx -= ST;
+          al.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ, wid);
+          bl.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ + ASZ, wid);
+        }
+        read_frags(smem + nxt * SSZ, 0, a0, b0);
+      }
+      mfmas(a1, b1);
+      cur = nxt;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  gemm_epilogue<BM, BN, NT, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // split-K reduction + epilogue: block = 64 rows x 256 columns (64 column quads x 4 row groups
@@ -522,9 +803,36 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
 }
 
 // ---- tile / split selection (host) ----------------------------------------------------------
+// kind 0: register-staged k_gemm (any weight format); kind 1: LDS-DMA k_gemm_dma (F16 weights)
 struct Plan {
-  int bm, bn, splits, kps;
+  int kind, bm, bn, var, splits, kps;
 };
+
+// LDS-DMA variants: tile, wave grid, LDS stages
+struct DmaVar {
+  int bm, bn, wgm, wgn, st, pipe;
+  double eff;
+};
+static constexpr DmaVar kDmaC[] = {
+    {128, 160, 2, 2, 2, 0, 1.00},  // 0: 2 blocks / CU
+    {128, 320, 2, 4, 2, 0, 1.00},  // 1
+    {256, 128, 4, 2, 3, 0, 1.00},  // 2
+    {256, 256, 2, 4, 2, 0, 1.00},  // 3
+    {128, 128, 2, 2, 2, 0, 0.95},  // 4: 2 blocks / CU
+    {128, 64, 2, 2, 3, 0, 0.80},   // 5
+    {256, 160, 4, 2, 3, 1, 1.00},  // 6: split-phase
+    {256, 128, 4, 2, 3, 1, 1.00},  // 7: split-phase
+    {128, 160, 2, 2, 3, 1, 1.00},  // 8: split-phase, 1 block / CU
+    {256, 160, 4, 2, 3, 0, 1.00},  // 9
+};
+static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
+
+extern "C" int qd_gemm_force(int variant) {
+  QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) || (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))),
+             "qd_gemm_force: -1, 0..3 or 100 + DMA variant");
+  g_force = variant;
+  return 0;
+}
 
 // Cost model (seconds): a CU runs ~4 TFLOP/s of this kernel with 2 resident blocks, ~3 with
 // one; tile efficiency eff; a launch takes ceil(blocks / 512) rounds of 2 blocks per CU.
@@ -534,9 +842,11 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
     int bm, bn;
     double eff;
   } tiles[] = {{128, 160, 1.00}, {128, 128, 0.97}, {128, 64, 0.80}, {64, 64, 0.60}};
-  Plan best{64, 64, 1, K};
+  Plan best{0, 64, 64, 0, 1, K};
   double best_t = 1e300;
-  for (const T& t : tiles) {
+  for (int ti = 0; ti < 4; ++ti) {
+    const T& t = tiles[ti];
+    if (g_force >= 0 && g_force != ti) continue;
     if (t.bn == 160 && N % 160 != 0) continue;  // 160-wide tiles only where they fit N exactly
     if (amax && rows_per_sample % (t.bm / 2) != 0) continue;
     if (quant_w && t.bn == 160) continue;        // int staging maps are built for BN % 64 == 0
@@ -550,7 +860,21 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       if (s > 1) tm += 8.0 * M * N * s / 5e12 + 3e-6;
       if (tm < best_t * 0.98) {
         best_t = tm;
-        best = {t.bm, t.bn, s, K / s};
+        best = {0, t.bm, t.bn, 0, s, K / s};
+      }
+    }
+  }
+  if (g_force >= 100 && !quant_w) {
+    const DmaVar& d = kDmaC[g_force - 100];
+    const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || (d.bn / d.wgn) % 32 == 0);
+    if (ok) {
+      best = {1, d.bm, d.bn, g_force - 100, 1, K};
+      // same split rule as the register tiles: split only while blocks stay under one round
+      const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
+      for (int sp = 2; sp <= 16 && !geglu; sp *= 2) {
+        if (K % (64 * sp) != 0 || K / sp < 512 || tiles_mn * sp > 256) break;
+        best.splits = sp;
+        best.kps = K / sp;
       }
     }
   }
@@ -567,9 +891,33 @@ static void launch_fmt(const GemmArgs& p, int fmt, hipStream_t st) {
   }
 }
 
+template <int V, int AMODE, bool SPLIT>
+static void launch_dma_v(const GemmArgs& p, hipStream_t st) {
+  constexpr DmaVar d = kDmaC[V];
+  const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
+  k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, AMODE, SPLIT><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+}
+
+template <int AMODE, bool SPLIT>
+static void launch_dma(const GemmArgs& p, int var, hipStream_t st) {
+  switch (var) {
+    case 0: launch_dma_v<0, AMODE, SPLIT>(p, st); break;
+    case 1: launch_dma_v<1, AMODE, SPLIT>(p, st); break;
+    case 2: launch_dma_v<2, AMODE, SPLIT>(p, st); break;
+    case 3: launch_dma_v<3, AMODE, SPLIT>(p, st); break;
+    case 4: launch_dma_v<4, AMODE, SPLIT>(p, st); break;
+    case 5: launch_dma_v<5, AMODE, SPLIT>(p, st); break;
+    case 6: launch_dma_v<6, AMODE, SPLIT>(p, st); break;
+    case 7: launch_dma_v<7, AMODE, SPLIT>(p, st); break;
+    case 8: launch_dma_v<8, AMODE, SPLIT>(p, st); break;
+    default: launch_dma_v<9, AMODE, SPLIT>(p, st); break;
+  }
+}
+
 template <int AMODE, bool SPLIT>
 static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t st) {
-  if (pl.bm == 128 && pl.bn == 160) launch_fmt<128, 160, AMODE, SPLIT>(p, fmt, st);
+  if (pl.kind == 1) launch_dma<AMODE, SPLIT>(p, pl.var, st);
+  else if (pl.bm == 128 && pl.bn == 160) launch_fmt<128, 160, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128 && pl.bn == 128) launch_fmt<128, 128, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128) launch_fmt<128, 64, AMODE, SPLIT>(p, fmt, st);
   else launch_fmt<64, 64, AMODE, SPLIT>(p, fmt, st);

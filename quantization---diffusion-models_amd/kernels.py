@@ -6,6 +6,7 @@ the host and raises ``ValueError`` before anything is launched, mirroring the re
 argument errors; kernel failures surface as ``RuntimeError`` from ``_lib.call``.
 """
 import ctypes
+import os
 
 import torch
 
@@ -134,11 +135,77 @@ def conv_weight_khwc(w, ci_pad):
 
 
 # ---------------------------------------------------------------- GEMMs
+# Kernel-family selection.  libqdiff has two GEMM families: the register-staged k_gemm (any
+# weight format: fp16, or int8 / packed-int4 codes dequantized while staging) and the LDS-DMA
+# k_gemm_dma (fp16 B operand: the dequantized buffer the reference itself stores).  Which tile /
+# family is fastest depends on the shape (SD1.5 spans M = 8..32768, N = 320..10240, K up to
+# 23040) and on the device, so the first eager call of each GEMM shape times the candidates
+# (HIP events, scratch outputs, real operands) and caches the winner; graph capture and replays
+# reuse it.  Every unsplit candidate accumulates each output over K in the same order (one
+# 16x16x32 MFMA chain per 32-deep slice), so the choice does not change results; split-K
+# candidates reduce fixed-order fp32 slabs (deterministic for a given choice).
+# QD_GEMM_TUNE=0 disables the search (library planner only).
+REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
+DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109)  # LDS-DMA variants (fp16 weights)
+_TUNE = {}
+_TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
+
+
+def gemm_choices():
+    """{shape key: (weight format, qd_gemm_force id)} chosen so far."""
+    return dict(_TUNE)
+
+
+def _force(v):
+    _lib.call("qd_gemm_force", v)
+
+
+def _choose(key, cands, run):
+    """Pick the fastest candidate for `key` (eager calls only); run(cand) launches one scratch
+    GEMM.  Returns the cached choice, or None (library planner) while capturing / disabled."""
+    if key in _TUNE:
+        return _TUNE[key]
+    if not _TUNE_ON or torch.cuda.is_current_stream_capturing() or len(cands) == 1:
+        return cands[0] if len(cands) == 1 else None
+    st = torch.cuda.current_stream()
+    best, best_t = None, float("inf")
+    for c in cands:
+        try:
+            run(c)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(3):
+                run(c)
+            e1.record(st)
+            e1.synchronize()
+            t = e0.elapsed_time(e1)
+        except RuntimeError:  # a candidate the library rejects for this shape
+            continue
+        finally:
+            _force(-1)
+        if t < best_t * 0.98:
+            best, best_t = c, t
+    _TUNE[key] = best
+    return best
+
+
+def _cands(ops):
+    """(op index, variant) candidates: register tiles for every format, DMA for fp16."""
+    out = []
+    for i, op in enumerate(ops):
+        out += [(i, v) for v in REG_VARIANTS]
+        if op[1] == "f16":
+            out += [(i, v) for v in DMA_VARIANTS]
+    return out
+
+
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
-           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False):
+           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None):
     """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K).
     geglu: W rows (and bias) interleaved in 16-row [hidden | gate] blocks (geglu_interleave);
-    returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue)."""
+    returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue).
+    weight_f16: the same weight's fp16 dequantized buffer (bit-identical to dequantizing the
+    codes); when given, the kernel search also considers the fp16 LDS-DMA family."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
         raise ValueError("x must be an fp16 HIP tensor")
     if x2d.dim() != 2 or x2d.stride(1) != 1:
@@ -152,10 +219,33 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
           (EPI_GEGLU if geglu else 0)
     if residual is not None:
         _chk(residual, "residual")
-    ws, wsn = _gemm_ws(M, N, K, WFMT[wfmt], rows_per_sample, epi, x2d.device)
-    _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(weight), WFMT[wfmt], _p(scales), group,
-              _p(bias), _p(residual), _p(out), N, out.stride(0), epi, _p(amax), rows_per_sample,
-              _p(ws), wsn, _stream())
+    ops = [(weight, wfmt, scales, group)]
+    if weight_f16 is not None and wfmt != "f16":
+        ops.append((weight_f16, "f16", None, 0))
+
+    def launch(c, y, am, ep, scratch):
+        w, fmt, sc, gr = ops[c[0]]
+        _force(c[1])
+        try:
+            if scratch:
+                n = _lib.load().qd_gemm_workspace(M, N, K, WFMT[fmt], rows_per_sample, ep)
+                ws, wsn = (torch.empty(n, dtype=torch.float32, device=x2d.device), n) if n > 0 else (None, 0)
+            else:
+                ws, wsn = _gemm_ws(M, N, K, WFMT[fmt], rows_per_sample, ep, x2d.device)
+            _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(w), WFMT[fmt], _p(sc), gr,
+                      _p(bias), _p(residual), _p(y), N, y.stride(0), ep, _p(am), rows_per_sample,
+                      _p(ws), wsn, _stream())
+        finally:
+            _force(-1)
+
+    key = ("linear", M, N, K, x2d.stride(0), epi & ~EPI_AMAX_ZEROED, rows_per_sample, tuple(o[1] for o in ops))
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        ta = torch.empty_like(amax) if amax is not None else None
+        c = _choose(key, _cands(ops), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else (0, -1), out, amax, epi, False)
     return out
 
 
@@ -191,10 +281,32 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
         out = _empty((n, ho, wo, co), torch.float16, x.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0)
-    ws, wsn = (None, 0) if cip % 64 else _gemm_ws(n * ho * wo, co, kh * kw * cip, 0, ho * wo, epi, x.device)
-    _lib.call("qd_conv2d_fwd", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad,
-              1 if upsample2x else 0, _p(bias), _p(residual), _p(out), epi, _p(amax), _p(ws), wsn,
-              _stream())
+    M, Kd = n * ho * wo, kh * kw * cip
+
+    def launch(c, y, am, ep, scratch):
+        _force(c[1])
+        try:
+            if cip % 64:
+                ws, wsn = None, 0
+            elif scratch:
+                m_ = _lib.load().qd_gemm_workspace(M, co, Kd, 0, ho * wo, ep)
+                ws, wsn = (torch.empty(m_, dtype=torch.float32, device=x.device), m_) if m_ > 0 else (None, 0)
+            else:
+                ws, wsn = _gemm_ws(M, co, Kd, 0, ho * wo, ep, x.device)
+            _lib.call("qd_conv2d_fwd", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad,
+                      1 if upsample2x else 0, _p(bias), _p(residual), _p(y), ep, _p(am), _p(ws), wsn,
+                      _stream())
+        finally:
+            _force(-1)
+
+    key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        ta = torch.empty_like(amax) if amax is not None else None
+        c = _choose(key, _cands([(w_khwc, "f16", None, 0)]), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else (0, -1), out, amax, epi, False)
     return out
 
 

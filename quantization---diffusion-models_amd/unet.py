@@ -403,11 +403,12 @@ def run_linear(layer, x2d, residual=None):
     if isinstance(layer, WxAxLinear):
         xin = layer.act_quant(x2d) if layer.quantize_act else x2d
         w, fmt, sc, g = layer.gemm_weight()
+        wf = layer.weight if fmt != "f16" else None  # the same weight's fp16 dequantized buffer
         if layer.output_quant_name != "None":
-            y = K.linear(xin, w, fmt, sc, g, bias=layer.bias)
+            y = K.linear(xin, w, fmt, sc, g, bias=layer.bias, weight_f16=wf)
             y = K.act_fakequant(y, layer.output_quant_name, layer.n_bits_A, out=y)
             return K.add(y, residual, out=y) if residual is not None else y
-        return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual)
+        return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual, weight_f16=wf)
     return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual)
 
 
@@ -426,7 +427,8 @@ def _geglu_operand(layer):
         return cache[1]
     perm = K.geglu_interleave_rows(w.shape[0], w.device)
     op = (w[perm].contiguous(), fmt, None if sc is None else sc[perm].contiguous(), g,
-          None if b is None else b.detach()[perm].contiguous())
+          None if b is None else b.detach()[perm].contiguous(),
+          layer.weight.detach()[perm].contiguous() if fmt != "f16" else None)
     layer._qd_geglu = (ver, op)
     return op
 
@@ -439,8 +441,8 @@ def ff_geglu(layer, x2d):
     if hook is not None:  # SmoothQuant calibration observes the projection input
         hook(x2d)
     xin = layer.act_quant(x2d) if isinstance(layer, WxAxLinear) and layer.quantize_act else x2d
-    w, fmt, sc, g, b = _geglu_operand(layer)
-    return K.linear(xin, w, fmt, sc, g, bias=b, geglu=True)
+    w, fmt, sc, g, b, wf = _geglu_operand(layer)
+    return K.linear(xin, w, fmt, sc, g, bias=b, geglu=True, weight_f16=wf)
 
 
 def resnet_fwd(res, x, temb_silu, skip=None):

@@ -78,6 +78,41 @@ def bench_linear():
         print(f"linear M={m:6d} K={kk:5d} N={nn:6d}: {us:8.1f} us  {fl / us / 1e6:7.1f} TFLOP/s", flush=True)
 
 
+
+
+def bench_sweep():
+    """Every GEMM kernel family / tile (qd_gemm_force) on the SD1.5 conv and linear shapes."""
+    from qdiff import _lib
+    variants = [-1, 0, 100, 101, 103, 104, 106, 107, 108, 109]
+    convs = [(8, 64, 320, 320, 3), (8, 32, 640, 640, 3), (8, 16, 1280, 1280, 3), (8, 8, 1280, 1280, 3),
+             (8, 64, 640, 320, 3), (8, 32, 1920, 640, 3), (8, 16, 2560, 1280, 3), (8, 64, 320, 320, 1)]
+    for n, h, ci, co, k in convs:
+        x = rnd(n, h, h, ci)
+        wt = rnd(co, k, k, ci, scale=0.02)
+        bias = rnd(co)
+        amax = torch.empty(n * co, dtype=torch.float32, device=dev)
+        fl = 2.0 * n * h * h * co * ci * k * k
+        row = []
+        for v in variants:
+            _lib.call("qd_gemm_force", v)
+            us = timeit(lambda: K.conv2d_nhwc(x, wt, ci, 1, k // 2, bias=bias, amax=amax))
+            row.append(f"{v}:{fl / us / 1e6:6.0f}")
+        print(f"conv {h}x{h} {ci}->{co} k{k}: " + " ".join(row), flush=True)
+    for m, kk, nn in [(32768, 320, 320), (32768, 320, 2560), (32768, 1280, 320), (8192, 640, 640),
+                      (8192, 640, 5120), (8192, 2560, 640), (2048, 1280, 1280), (2048, 1280, 10240),
+                      (2048, 5120, 1280)]:
+        x = rnd(m, kk)
+        w = rnd(nn, kk, scale=0.02)
+        fl = 2.0 * m * kk * nn
+        row = []
+        for v in variants:
+            _lib.call("qd_gemm_force", v)
+            us = timeit(lambda: K.linear(x, w))
+            row.append(f"{v}:{fl / us / 1e6:6.0f}")
+        print(f"linear {m}x{kk}x{nn}: " + " ".join(row), flush=True)
+    _lib.call("qd_gemm_force", -1)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["attn", "gn", "conv", "linear"]
     for w in which:

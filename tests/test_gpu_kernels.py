@@ -359,3 +359,60 @@ def test_timestep_embedding_and_ddim(dev):
     assert_fp16_close(got, ref, ulps=2.0, atol=1e-3)
     assert step.item() == 6
     assert torch.equal(k.nhwc_to_nchw(nxt[:B], 4), k.nhwc_to_nchw(nxt[B:], 4))
+
+
+# ------------------------------------------------------------------ GEMM kernel families
+@pytest.fixture
+def forced_gemm():
+    from qdiff import _lib
+
+    def force(v):
+        _lib.call("qd_gemm_force", v)
+    yield force
+    _lib.call("qd_gemm_force", -1)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 110)))
+def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
+    """Every kernel family / tile (register-staged and LDS-DMA) on ragged shapes: rows past M,
+    conv halo, stride 2, fused 2x upsample, the 4-channel conv_in (any-Ci decode), K tails,
+    split-K, residual, amax and GEGLU epilogues."""
+    k = K()
+    forced_gemm(variant)
+    g = torch.Generator().manual_seed(variant + 5)
+    for cin, cout, ksz, stride, hw, ups, n in ((64, 320, 3, 1, 16, False, 2), (128, 128, 3, 2, 16, False, 1),
+                                               (4, 64, 3, 1, 8, False, 2), (64, 64, 3, 1, 8, True, 1),
+                                               (320, 640, 1, 1, 8, False, 3), (1280, 320, 3, 1, 8, False, 2)):
+        x = torch.randn(n, cin, hw, hw, generator=g).half()
+        w = (torch.randn(cout, cin, ksz, ksz, generator=g) / (cin * ksz * ksz) ** 0.5).half()
+        b = torch.randn(cout, generator=g).half()
+        cip = (cin + 7) // 8 * 8
+        xh = k.nchw_to_nhwc(x.to(dev), cip)
+        wk = k.conv_weight_khwc(w.to(dev), cip)
+        amax = torch.empty(n * cout, dtype=torch.float32, device=dev)
+        y = k.conv2d_nhwc(xh, wk, cin, stride, ksz // 2, ups, bias=b.to(dev), amax=amax)
+        xin = F.interpolate(x.float(), scale_factor=2.0, mode="nearest") if ups else x.float()
+        ref = F.conv2d(xin, w.float(), b.float(), stride, ksz // 2).half().float()
+        got = k.nhwc_to_nchw(y).cpu().float()
+        assert_fp16_close(got, ref, ulps=2.0, atol=1e-3)
+        assert torch.equal(amax.view(n, cout).cpu(), got.abs().amax(dim=(2, 3))), (variant, cin, cout)
+    for M, N, Kd in ((200, 320, 320), (616, 640, 776), (4096, 1280, 5120), (77, 256, 1280)):
+        x = torch.randn(M, Kd, generator=g).half()
+        w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half()
+        b = torch.randn(N, generator=g).half()
+        res = torch.randn(M, N, generator=g).half()
+        y = k.linear(x.to(dev), w.to(dev), "f16", bias=b.to(dev), residual=res.to(dev)).cpu().float()
+        pre = (x.float() @ w.float().t() + b.float()).half().float()
+        yf = (pre + res.float()).half().float()
+        assert ((y - yf).abs() <= ulp16(pre) + ulp16(yf) + 1e-3).all(), (variant, M, N, Kd)
+    M, I, Kd = 300, 640, 320
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(2 * I, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+    b = torch.randn(2 * I, generator=g).half().to(dev)
+    perm = k.geglu_interleave_rows(2 * I, dev)
+    fused = k.linear(x, w[perm].contiguous(), "f16", bias=b[perm].contiguous(), geglu=True).cpu().float()
+    pre = (x.float().cpu() @ w.cpu().float().t() + b.float().cpu()).half().float()
+    h, gt = pre.chunk(2, -1)
+    ref = (h * F.gelu(gt).half().float()).half().float()
+    tol = 2 * ulp16(ref) + 2 * ulp16(h) * gt.abs() + 2.5 * h.abs() * ulp16(gt) + 1e-3
+    assert ((fused - ref).abs() <= tol).all(), (variant, (fused - ref).abs().max().item())
