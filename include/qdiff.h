@@ -128,10 +128,12 @@ int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const 
 
 /* Conv output fake-quant + fused adds (the q_y = output_quant(y) of fake_quant.py:340 followed
  * by the diffusers residual / temb add): out = half(fq(y; amax[n][c]) + res) with res either a
- * full [N, HW, C] tensor (`residual`), or a per-(n, c) vector (`chan_add`, the time embedding
- * projection), or none.  n_bits == 0 disables the quantization. */
+ * full [N, HW, C] tensor (`residual`), or a per-(n, c) vector (`chan_add` [N][chan_add_ld], the
+ * time embedding projection; chan_add_ld <= 0 means C), or none.  n_bits == 0 disables the
+ * quantization. */
 int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
-                   const void* residual, const void* chan_add, void* out, void* stream);
+                   const void* residual, const void* chan_add, int chan_add_ld, void* out,
+                   void* stream);
 
 /* ---------------- normalisation / activations (diffusers UNet ops, fp16 I/O) --------- */
 /* GroupNorm(groups, eps, affine) on NHWC [N, HW, C] (+ SiLU) (+ per-(n, c) fake-quant of the

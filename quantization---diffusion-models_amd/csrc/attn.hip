@@ -45,7 +45,10 @@ constexpr int v_stride(int dv) { return ((dv / 2 / 8) & 1) ? dv : dv + 16; }
 //   * K/V tiles register-staged and double-buffered in LDS (tile loop unrolled x2 so every
 //     LDS address is a per-lane base + immediate); the next tile's loads are in flight while
 //     the current one is computed; one barrier per tile.
-template <int DP, int DV, int NB, int NW>
+//   * NQ query groups of 16 per wave: every K / V^T fragment read from LDS feeds NQ MFMAs, and
+//     every staged K/V tile serves NW * 16 * NQ queries (LDS-read and L2->CU traffic per FLOP
+//     both / NQ; at head_dim 40 both bound the NQ = 1 loop).
+template <int DP, int DV, int NB, int NW, int NQ>
 __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                               int ldk, const f16* __restrict__ v, int ldv,
                                               f16* __restrict__ o, int ldo, int heads, int sq, int skv,
@@ -62,13 +65,14 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
 
   // XCD-aware bijective remap: the q-blocks of one (batch, head) run on one XCD (blocks b and
   // b + 8 share an XCD), so that head's K/V stays in that XCD's L2 while they stream it.
-  const int nqb = (sq + NW * 16 - 1) / (NW * 16);  // q-blocks per (batch, head)
+  constexpr int QB = NW * 16 * NQ;                  // queries per block
+  const int nqb = (sq + QB - 1) / QB;                // q-blocks per (batch, head)
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int bh = wg / nqb;
   const int b = bh / heads, h = bh % heads;
-  const int q0 = (wg - bh * nqb) * (NW * 16);
+  const int q0 = (wg - bh * nqb) * QB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
 
@@ -78,16 +82,17 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   f16* ob = o + (long)b * sq * ldo + h * d;
   const int dchunks = d >> 3;
 
-  // B operand of S^T: Q[q = q0 + 16*wid + fr][dd = 32s + 8fq .. +8]
-  f16x8 qf[DP / 32];
-  {
-    const int qrow = q0 + wid * 16 + fr;
+  // B operand of S^T: Q[q = q0 + 16*(NQ*wid + g) + fr][dd = 32s + 8fq .. +8]
+  f16x8 qf[NQ][DP / 32];
+#pragma unroll
+  for (int g = 0; g < NQ; ++g) {
+    const int qrow = q0 + (wid * NQ + g) * 16 + fr;
 #pragma unroll
     for (int s = 0; s < DP / 32; ++s) {
       const int c = s * 4 + fq;
       f16x8 val = {};
       if (qrow < sq && c < dchunks) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + c * 8);
-      qf[s] = val;
+      qf[g][s] = val;
     }
   }
 
@@ -142,10 +147,14 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
       if (vdst[i] >= 0) *reinterpret_cast<f16x8*>(base + vdst[i]) = vst[i];
   };
 
-  f32x4 oacc[TD];
+  f32x4 oacc[NQ][TD];
+  float mrow[NQ];  // running max of this lane's queries (log2 domain)
 #pragma unroll
-  for (int j = 0; j < TD; ++j) oacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float mrow = -INFINITY;  // running max of this lane's query (log2 domain)
+  for (int g = 0; g < NQ; ++g) {
+#pragma unroll
+    for (int j = 0; j < TD; ++j) oacc[g][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    mrow[g] = -INFINITY;
+  }
 
   // per-lane LDS read offsets (elements, within a buffer)
   int kread[4][DP / 32];
@@ -161,44 +170,53 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   const int ntiles = (skv + KV_T - 1) / KV_T;
   auto tile = [&](const f16* ks, int kv0) {
     // ---- S^T[kv][q] = K Q^T: tile jt holds kv = 16jt + 4fq + r for query fr ----
-    f32x4 sacc[4];
+    f32x4 sacc[NQ][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < NQ; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sacc[g][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DP / 32; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f16x8 kf = *reinterpret_cast<const f16x8*>(ks + kread[j][s]);
-        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], sacc[j], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < NQ; ++g)
+          sacc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[g][s], sacc[g][j], 0, 0, 0);
       }
     if (kv0 + KV_T > skv) {
+#pragma unroll
+      for (int g = 0; g < NQ; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kv0 + j * 16 + fq * 4 + r >= skv) sacc[g][j][r] = -INFINITY;
+    }
+    // ---- online softmax per query group (log2 domain) ----
+    f16x8 pf[NQ][2];
+#pragma unroll
+    for (int g = 0; g < NQ; ++g) {
+      float mx = sacc[g][0][0];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[g][j][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrow[g], mx * scale_log2);
+      if (__any(mnew > mrow[g])) {  // wave-uniform: lanes whose max did not grow get alpha = 1
+        const float alpha = __builtin_amdgcn_exp2f(mrow[g] - mnew);
+#pragma unroll
+        for (int j = 0; j < TD; ++j) oacc[g][j] *= alpha;
+        mrow[g] = mnew;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (kv0 + j * 16 + fq * 4 + r >= skv) sacc[j][r] = -INFINITY;
+          pf[g][j >> 1][(j & 1) * 4 + r] = (f16)__builtin_amdgcn_exp2f(fmaf(sacc[g][j][r], scale_log2, -mrow[g]));
     }
-    // ---- online softmax for query fr (log2 domain) ----
-    float mx = sacc[0][0];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[j][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(mrow, mx * scale_log2);
-    if (__any(mnew > mrow)) {  // wave-uniform: lanes whose max did not grow get alpha = 1
-      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
-#pragma unroll
-      for (int j = 0; j < TD; ++j) oacc[j] *= alpha;
-      mrow = mnew;
-    }
-    f16x8 pf[2];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        pf[j >> 1][(j & 1) * 4 + r] = (f16)__builtin_amdgcn_exp2f(fmaf(sacc[j][r], scale_log2, -mrow));
     // ---- O^T[d][q] += V^T P^T ----
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -208,7 +226,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
         const f16x4 lo = tr_read(vp);
         const f16x4 hi = tr_read(vp + 16 * VST);
         const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        oacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[s], oacc[j], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < NQ; ++g) oacc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[g][s], oacc[g][j], 0, 0, 0);
       }
   };
 
@@ -244,24 +263,27 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   }
   // ---- epilogue: lane holds O^T rows 16j + 4fq + r of query fr; row d holds sum(P) ----
   const int dj = d >> 4, dg = (d & 15) >> 2, dr = d & 3;  // (tile, lane group, reg) of row d
-  float lsum = 0.f;
 #pragma unroll
-  for (int j = 0; j < TD; ++j)
+  for (int g = 0; g < NQ; ++g) {
+    float lsum = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (j == dj && r == dr) lsum = oacc[j][r];
-  lsum = __shfl(lsum, dg * 16 + fr, 64);
-  const int qrow = q0 + wid * 16 + fr;
-  if (qrow < sq) {
-    const float inv = 1.0f / lsum;
+    for (int j = 0; j < TD; ++j)
 #pragma unroll
-    for (int j = 0; j < TD; ++j) {
-      const int dd = j * 16 + fq * 4;
-      if (dd < d) {
-        f16x4 w;
+      for (int r = 0; r < 4; ++r)
+        if (j == dj && r == dr) lsum = oacc[g][j][r];
+    lsum = __shfl(lsum, dg * 16 + fr, 64);
+    const int qrow = q0 + (wid * NQ + g) * 16 + fr;
+    if (qrow < sq) {
+      const float inv = 1.0f / lsum;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) w[r] = (f16)(oacc[j][r] * inv);
-        *reinterpret_cast<f16x4*>(ob + (long)qrow * ldo + dd) = w;
+      for (int j = 0; j < TD; ++j) {
+        const int dd = j * 16 + fq * 4;
+        if (dd < d) {
+          f16x4 w;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) w[r] = (f16)(oacc[g][j][r] * inv);
+          *reinterpret_cast<f16x4*>(ob + (long)qrow * ldo + dd) = w;
+        }
       }
     }
   }
@@ -271,15 +293,21 @@ template <int DP, int DV>
 static void launch(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, hipStream_t st) {
   constexpr int NB = DP <= 96 ? 2 : 1;
-  // 8 waves (128 queries) share each staged K/V tile on long sequences; 4 on short ones
-  if (sq >= 512) {
+  const float sl2 = scale * 1.4426950408889634f;
+  // long sequences: 8 waves x 2 query groups (256 queries) share each staged K/V tile while the
+  // grid still holds >= 2 blocks per CU; then 8 x 1 (128 queries); 4 x 1 on short ones
+  if (sq >= 512 && DP <= 96 && (long)((sq + 255) / 256) * b * heads >= 512) {
+    const int grid = ((sq + 255) / 256) * b * heads;
+    k_attn<DP, DV, NB, 8, 2><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+  } else if (sq >= 512) {
     const int grid = ((sq + 127) / 128) * b * heads;
-    k_attn<DP, DV, NB, 8><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                               (f16*)o, ldo, heads, sq, skv, d, scale * 1.4426950408889634f);
+    k_attn<DP, DV, NB, 8, 1><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
   } else {
     const int grid = ((sq + 63) / 64) * b * heads;
-    k_attn<DP, DV, NB, 4><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                               (f16*)o, ldo, heads, sq, skv, d, scale * 1.4426950408889634f);
+    k_attn<DP, DV, NB, 4, 1><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
   }
 }
 

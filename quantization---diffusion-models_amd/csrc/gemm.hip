@@ -29,6 +29,8 @@
 // workspace + a fixed-order reduction kernel that runs the same epilogue: deterministic).
 #include "common.h"
 
+#include <algorithm>
+
 using namespace qd;
 
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -322,35 +324,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
     const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
-    if (geglu) {
-      // weight rows interleaved in 16-row blocks [hidden 16 | gate 16]: fragment tiles j (hidden)
-      // and j + 1 (gate) hold the same 16 output columns.  diffusers GEGLU: out =
-      // half(h * half(gelu(g))) on the fp16 projection outputs h, g.
-      // (TN is even for every tile the planner allows with GEGLU: BN in {64, 128})
-#pragma unroll
-      for (int j = 0; j + 1 < TN; j += 2) {
-        const int nl = wn0 + j * 16 + fq * 4;
-        const int n = n0 + nl;
-        f16x4 bh = {}, bg = {};
-        if (has_bias && n < p.N) {
-          bh = *reinterpret_cast<const f16x4*>(p.bias + n);
-          bg = *reinterpret_cast<const f16x4*>(p.bias + n + 16);
-        }
-        const int ol = (wn0 >> 1) + j * 8 + fq * 4;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int ml = wm0 + i * 16 + fr;
-          f16x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const f16 h = (f16)(acc[i][j][r] + (float)bh[r]);
-            const f16 g = (f16)(acc[i][j + 1][r] + (float)bg[r]);
-            o[r] = (f16)((float)h * (float)(f16)gelu_f((float)g));
-          }
-          *reinterpret_cast<f16x4*>(ct + ml * LP + ol) = o;
-        }
-      }
-    } else {
+    {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int nl = wn0 + j * 16 + fq * 4;
@@ -371,7 +345,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           }
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
         }
-        if (do_amax) {
+        if (do_amax && !geglu) {
           // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
 #pragma unroll
           for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
@@ -385,7 +359,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
       }
     }
     __syncthreads();
-    // output tile: BN columns (BN / 2 with GEGLU) starting at n0 (n0 / 2)
+    // output tile: BN columns (BN / 2 with GEGLU) starting at n0 (n0 / 2).  GEGLU: weight rows
+    // are interleaved in 16-row blocks [hidden 16 | gate 16] (BN % 32 == 0), so output columns
+    // 16b + j of the tile read h = tile[32b + j], g = tile[32b + 16 + j]; diffusers GEGLU on the
+    // fp16 projection outputs: out = half(h * half(gelu(g))).
+    static_assert(BN % 32 == 0 || BN % 16 == 0, "tile width");
     const int cpr = geglu ? BN / 16 : BN / 8;
     const int on0 = geglu ? n0 >> 1 : n0, oN = geglu ? p.N >> 1 : p.N;
 #pragma unroll 2
@@ -393,7 +371,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
       const int row = e / cpr, c = e - row * cpr;
       const int m = m0 + row, n = on0 + c * 8;
       if (m < p.M && n < oN) {
-        f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+        f16x8 v;
+        if (geglu) {
+          const int tc = (c >> 1) * 32 + (c & 1) * 8;
+          const f16x8 hv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc);
+          const f16x8 gv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc + 16);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)hv[r] * (float)(f16)gelu_f((float)gv[r]));
+        } else {
+          v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+        }
         if (has_res) {
           const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
 #pragma unroll
@@ -850,10 +837,10 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
     if (t.bn == 160 && N % 160 != 0) continue;  // 160-wide tiles only where they fit N exactly
     if (amax && rows_per_sample % (t.bm / 2) != 0) continue;
     if (quant_w && t.bn == 160) continue;        // int staging maps are built for BN % 64 == 0
-    if (geglu && t.bn == 160) continue;          // GEGLU pairs 16-column fragments: WN % 32 == 0
     const long tiles_mn = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
-    for (int s = 1; s <= 16; s *= 2) {
-      if (s > 1 && (K % (64 * s) != 0 || K / s < 512 || geglu)) break;
+    for (int s = 1; s <= 32; ++s) {
+      // split K into s equal runs of whole 64-deep steps, each >= 8 steps
+      if (s > 1 && (K % 64 != 0 || (K / 64) % s != 0 || K / s < 512 || geglu)) continue;
       const long blocks = tiles_mn * s;
       const double blk = 2.0 * t.bm * t.bn * ((double)K / s) / t.eff;  // flop of one block
       double tm = blocks <= 256 ? blk / 3e12 : (double)((blocks + 511) / 512) * 2.0 * blk / 4e12;
@@ -866,13 +853,16 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
   }
   if (g_force >= 100 && !quant_w) {
     const DmaVar& d = kDmaC[g_force - 100];
-    const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || (d.bn / d.wgn) % 32 == 0);
+    const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
     if (ok) {
       best = {1, d.bm, d.bn, g_force - 100, 1, K};
-      // same split rule as the register tiles: split only while blocks stay under one round
+      // split K (whole 64-deep steps, >= 8 per split) while the blocks fit one resident round
       const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
-      for (int sp = 2; sp <= 16 && !geglu; sp *= 2) {
-        if (K % (64 * sp) != 0 || K / sp < 512 || tiles_mn * sp > 256) break;
+      const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st)), by_waves = 2048 / (64 * d.wgm * d.wgn);
+      const int per_cu = std::max(1, std::min(by_lds, by_waves));
+      for (int sp = 2; sp <= 32 && !geglu && K % 64 == 0; ++sp) {
+        if ((K / 64) % sp != 0 || K / sp < 512) continue;
+        if (tiles_mn * sp > 256L * per_cu) break;
         best.splits = sp;
         best.kps = K / sp;
       }
@@ -1056,8 +1046,15 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
   p.b_bytes = (unsigned)((long)co * p.K * 2);
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)n * co, S(stream));
-  if (ci_pad % 64 == 0) run_gemm<AM_CONV>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
-  else run_gemm<AM_CONV_ANY>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
+  if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && !upsample2x) {
+    // a pointwise conv IS a GEMM over the NHWC pixel rows (x [N*H*W][Ci_pad]): no tap decode
+    p.lda = ci_pad;
+    run_gemm<AM_LINEAR>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
+  } else if (ci_pad % 64 == 0) {
+    run_gemm<AM_CONV>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
+  } else {
+    run_gemm<AM_CONV_ANY>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
+  }
   QD_CHECK_LAUNCH();
   return 0;
 }

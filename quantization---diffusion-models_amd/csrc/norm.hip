@@ -313,69 +313,90 @@ extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw
 }
 
 // ---------------------------------------------------------------------------------------
-// LayerNorm over the last dim: one wave per row, row held in registers (C <= 4096).
+// LayerNorm over the last dim (diffusers BasicTransformerBlock norm1/2/3, torch CPU Half
+// semantics: fp32 mean / biased variance, y = half((x - mean) * rstd * gamma + beta)).
+// One wave per row, R rows per wave with every row's 16-B loads issued before any reduction
+// (enough bytes in flight per CU to stream at HBM rate even for C = 320 rows of 640 B); lane l
+// owns the 8-channel chunks l, l + 64, ... of the row.
 // ---------------------------------------------------------------------------------------
-template <int PER>  // half2 pairs per lane
+template <int PER, int R>  // 8-channel chunks per lane, rows per wave
 __global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, long rows, int c, float eps,
                                                    const f16* __restrict__ gamma,
                                                    const f16* __restrict__ beta, f16* __restrict__ y) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  const int pairs = c >> 1;
-  const __half2* p = reinterpret_cast<const __half2*>(x + row * c);
-  float v[2 * PER];
-  float s = 0.f;
+  const int chunks = c >> 3;
+  f16x8 v[R][PER];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int j = lane + i * 64;
-    if (j < pairs) {
-      const __half2 h = p[j];
-      v[2 * i] = __low2float(h);
-      v[2 * i + 1] = __high2float(h);
-    } else {
-      v[2 * i] = v[2 * i + 1] = 0.f;
-    }
-    s += v[2 * i] + v[2 * i + 1];
-  }
-  const float mean = wave_sum(s) / (float)c;
-  float q = 0.f;
+  for (int r = 0; r < R; ++r)
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int j = lane + i * 64;
-    if (j < pairs) {
-      const float a = v[2 * i] - mean, b = v[2 * i + 1] - mean;
-      q += a * a + b * b;
+    for (int i = 0; i < PER; ++i) {
+      const int j = lane + i * 64;
+      v[r][i] = (row0 + r < rows && j < chunks) ? *reinterpret_cast<const f16x8*>(x + (row0 + r) * c + j * 8)
+                                                : (f16x8){};
     }
-  }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)c + eps);
-  __half2* o = reinterpret_cast<__half2*>(y + row * c);
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int j = lane + i * 64;
-    if (j < pairs) {
-      const int ch = 2 * j;
-      const float a = fmaf((v[2 * i] - mean) * rstd, (float)gamma[ch], (float)beta[ch]);
-      const float b = fmaf((v[2 * i + 1] - mean) * rstd, (float)gamma[ch + 1], (float)beta[ch + 1]);
-      o[j] = __floats2half2_rn(a, b);
+  for (int r = 0; r < R; ++r) {
+    if (row0 + r >= rows) break;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)v[r][i][e];
+    const float mean = wave_sum(s) / (float)c;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (lane + i * 64 < chunks) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = (float)v[r][i][e] - mean;
+          q = fmaf(a, a, q);
+        }
+      }
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)c + eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = lane + i * 64;
+      if (j < chunks) {
+        const f16x8 g = *reinterpret_cast<const f16x8*>(gamma + j * 8);
+        const f16x8 b = *reinterpret_cast<const f16x8*>(beta + j * 8);
+        f16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (f16)fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[e], (float)b[e]);
+        *reinterpret_cast<f16x8*>(y + (row0 + r) * c + j * 8) = o;
+      }
     }
   }
+}
+
+template <int PER>
+static void launch_ln(const f16* x, long rows, int c, float eps, const f16* g, const f16* b, f16* y, hipStream_t st) {
+  // rows per wave: ~2 KB of loads in flight per wave, while the grid still fills the chip
+  int r = std::max(1, 2048 / (c * 2));
+  while (r > 1 && (rows + 4L * r - 1) / (4L * r) < 1024) r >>= 1;
+  if (r >= 4) k_layernorm<PER, 4><<<(int)((rows + 15) / 16), 256, 0, st>>>(x, rows, c, eps, g, b, y);
+  else if (r >= 2) k_layernorm<PER, 2><<<(int)((rows + 7) / 8), 256, 0, st>>>(x, rows, c, eps, g, b, y);
+  else k_layernorm<PER, 1><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, eps, g, b, y);
 }
 
 extern "C" int qd_layernorm(const void* x, int rows, int c, float eps, const void* gamma,
                             const void* beta, void* y, void* stream) {
   QD_REQUIRE(x && gamma && beta && y, "null pointer");
-  QD_REQUIRE(c % 2 == 0 && c <= 8192, "LayerNorm needs even C <= 8192");
+  QD_REQUIRE(c % 8 == 0 && c <= 4096, "LayerNorm needs C % 8 == 0, C <= 4096");
+  QD_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(gamma) |
+               reinterpret_cast<uintptr_t>(beta)) & 15) == 0, "LayerNorm operands must be 16-B aligned");
   if (rows == 0) return 0;
-  const int pairs = c / 2;
-  const int per = (pairs + 63) / 64;
-  dim3 grid(grid1(rows, 4));
+  const int per = (c / 8 + 63) / 64;
   hipStream_t st = S(stream);
-  if (per <= 4) k_layernorm<4><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
-  else if (per <= 8) k_layernorm<8><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
-  else if (per <= 16) k_layernorm<16><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
-  else if (per <= 32) k_layernorm<32><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
-  else k_layernorm<64><<<grid, 256, 0, st>>>((const f16*)x, rows, c, eps, (const f16*)gamma, (const f16*)beta, (f16*)y);
+  const f16 *xp = (const f16*)x, *g = (const f16*)gamma, *b = (const f16*)beta;
+  f16* yp = (f16*)y;
+  if (per <= 1) launch_ln<1>(xp, rows, c, eps, g, b, yp, st);
+  else if (per <= 2) launch_ln<2>(xp, rows, c, eps, g, b, yp, st);
+  else if (per <= 3) launch_ln<3>(xp, rows, c, eps, g, b, yp, st);
+  else if (per <= 4) launch_ln<4>(xp, rows, c, eps, g, b, yp, st);
+  else launch_ln<8>(xp, rows, c, eps, g, b, yp, st);
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -446,7 +446,8 @@ extern "C" int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw
 __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, const float* __restrict__ amax,
                                                   int hw, int c, int qmax, int rows_per_block,
                                                   const f16* __restrict__ res,
-                                                  const f16* __restrict__ cadd, f16* __restrict__ out) {
+                                                  const f16* __restrict__ cadd, int cadd_ld,
+                                                  f16* __restrict__ out) {
   const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
   if (chunk * 8 >= c) return;
   const int ch = chunk * 8;
@@ -455,7 +456,7 @@ __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, con
   float sc[8];
   double rs[8];
   f16x8 ca = {};
-  if (cadd && !res) ca = *reinterpret_cast<const f16x8*>(cadd + n * c + ch);
+  if (cadd && !res) ca = *reinterpret_cast<const f16x8*>(cadd + n * cadd_ld + ch);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sc[j] = qmax > 0 ? fq_scale(amax[n * c + ch + j], qmax) : 0.f;
@@ -484,8 +485,12 @@ __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, con
 }
 
 extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
-                              const void* residual, const void* chan_add, void* out, void* stream) {
+                              const void* residual, const void* chan_add, int chan_add_ld, void* out,
+                              void* stream) {
   QD_REQUIRE(y && out, "null pointer");
+  if (chan_add_ld <= 0) chan_add_ld = c;
+  QD_REQUIRE(!chan_add || (chan_add_ld >= c && chan_add_ld % 8 == 0 && (reinterpret_cast<uintptr_t>(chan_add) & 15) == 0),
+             "chan_add: 16-B aligned rows, ld >= c, ld % 8 == 0");
   QD_REQUIRE(c % 8 == 0, "finalize needs C % 8 == 0");
   QD_REQUIRE(n_bits == 0 || (amax && n_bits >= 2 && n_bits <= 16), "bad n_bits / amax");
   if ((long)n * hw * c == 0) return 0;
@@ -493,7 +498,7 @@ extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, i
   k_finalize<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, S(stream)>>>((const f16*)y, amax, hw, c,
                                                                       n_bits ? qmax_of(n_bits) : 0, g.rpb,
                                                                       (const f16*)residual, (const f16*)chan_add,
-                                                                      (f16*)out);
+                                                                      chan_add_ld, (f16*)out);
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -311,12 +311,18 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 
 
 def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
-    """out = half(fq(y) + residual | + chan_add[n, c]); y NHWC [N, H, W, C] (or [N, HW, C])."""
+    """out = half(fq(y) + residual | + chan_add[n, c]); y NHWC [N, H, W, C] (or [N, HW, C]).
+    chan_add may be a row-strided [N, C] view (e.g. a column slice of a stacked projection)."""
     _chk(y, "y")
     n, c = y.shape[0], y.shape[-1]
     hw = y.numel() // (n * c)
     o = out if out is not None else _empty(y.shape, y.dtype, y.device)
-    _lib.call("qd_fq_finalize", _p(y), _p(amax), n, hw, c, n_bits, _p(residual), _p(chan_add), _p(o),
+    ld = 0
+    if chan_add is not None:
+        if chan_add.dim() != 2 or chan_add.stride(1) != 1 or chan_add.dtype != torch.float16:
+            raise ValueError("chan_add must be an fp16 [N, C] tensor with unit column stride")
+        ld = chan_add.stride(0)
+    _lib.call("qd_fq_finalize", _p(y), _p(amax), n, hw, c, n_bits, _p(residual), _p(chan_add), ld, _p(o),
               _stream())
     return o
 

@@ -257,6 +257,54 @@ class UNet2DConditionModel(nn.Module):
                 p.fill_(1.0)
         return self
 
+    # ---------------------------------------------------------------- time-embedding projections
+    def _resnets(self):
+        for blk in self.down_blocks:
+            yield from blk.resnets
+        yield from self.mid_block.resnets
+        for blk in self.up_blocks:
+            yield from blk.resnets
+
+    def _temb_operand(self):
+        """Every ResnetBlock2D.time_emb_proj stacked along N (they all read the same
+        silu(temb)): (weight, fmt, scales, group, bias, fp16 weight, [(id(res), off, cout)]) or
+        None when they cannot share one GEMM (hooks, act/output quant, differing formats)."""
+        layers = [(res, res.time_emb_proj) for res in self._resnets()]
+        for _, l in layers:
+            if getattr(l, "_qd_hook", None) is not None or l.bias is None:
+                return None
+            if isinstance(l, WxAxLinear) and (l.quantize_act or l.output_quant_name != "None"):
+                return None
+        ops = [l.gemm_weight() if isinstance(l, WxAxLinear) else (_f16(l.weight), "f16", None, 0) for _, l in layers]
+        if len({(o[1], o[3]) for o in ops}) != 1 or any(l.out_features % 8 for _, l in layers):
+            return None
+        ver = tuple((o[0].data_ptr(), o[0]._version, l.weight._version, l.bias._version) for o, (_, l) in zip(ops, layers))
+        cache = getattr(self, "_qd_temb", None)
+        if cache is not None and cache[0] == ver:
+            return cache[1]
+        fmt, g = ops[0][1], ops[0][3]
+        w = torch.cat([o[0] for o in ops]).contiguous()
+        sc = torch.cat([o[2] for o in ops]).contiguous() if fmt != "f16" else None
+        wf = torch.cat([l.weight.detach() for _, l in layers]).contiguous() if fmt != "f16" else None
+        b = torch.cat([l.bias.detach() for _, l in layers]).contiguous()
+        slots, off = [], 0
+        for res, l in layers:
+            slots.append((id(res), off, l.out_features))
+            off += l.out_features
+        op = (w, fmt, sc, g, b, wf, slots)
+        self._qd_temb = (ver, op)
+        return op
+
+    def temb_projections(self, temb_silu):
+        """{id(resnet): time_emb_proj(silu(temb)) [2B, Cout] view}: ONE GEMM for all resnets
+        (each column slice is exactly that resnet's F.linear output)."""
+        op = self._temb_operand()
+        if op is None:
+            return {}
+        w, fmt, sc, g, b, wf, slots = op
+        y = K.linear(temb_silu, w, fmt, sc, g, bias=b, weight_f16=wf)
+        return {rid: y[:, off:off + co] for rid, off, co in slots}
+
     # ---------------------------------------------------------------- NHWC fused forward
     def forward(self, *a, **k):  # pragma: no cover - the pipeline drives fwd()
         raise RuntimeError("use UNet2DConditionModel.fwd(x_nhwc, temb_in, ctx_kv) (NHWC fused path)")
@@ -289,12 +337,13 @@ class UNet2DConditionModel(nn.Module):
             a = K.silu(a, out=a)
             temb = run_linear(self.add_embedding.linear_2, a, residual=temb)
         temb_silu = K.silu(temb)
+        tps = self.temb_projections(temb_silu)
 
         h = run_conv(self.conv_in, x, c_valid=cfg.in_channels)
         skips = [h]
         for blk in self.down_blocks:
             for i, res in enumerate(blk.resnets):
-                h = resnet_fwd(res, h, temb_silu)
+                h = resnet_fwd(res, h, temb_silu, tp=tps.get(id(res)))
                 if blk.attentions is not None:
                     h = transformer_fwd(blk.attentions[i], h, ctx_kv)
                 skips.append(h)
@@ -302,13 +351,13 @@ class UNet2DConditionModel(nn.Module):
                 h = run_conv(blk.downsamplers[0].conv, h)
                 skips.append(h)
         mb = self.mid_block
-        h = resnet_fwd(mb.resnets[0], h, temb_silu)
+        h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])))
         h = transformer_fwd(mb.attentions[0], h, ctx_kv)
-        h = resnet_fwd(mb.resnets[1], h, temb_silu)
+        h = resnet_fwd(mb.resnets[1], h, temb_silu, tp=tps.get(id(mb.resnets[1])))
         for blk in self.up_blocks:
             for i, res in enumerate(blk.resnets):
                 skip = skips.pop()
-                h = resnet_fwd(res, h, temb_silu, skip=skip)
+                h = resnet_fwd(res, h, temb_silu, skip=skip, tp=tps.get(id(res)))
                 if blk.attentions is not None:
                     h = transformer_fwd(blk.attentions[i], h, ctx_kv)
             if blk.upsamplers is not None:
@@ -445,13 +494,15 @@ def ff_geglu(layer, x2d):
     return K.linear(xin, w, fmt, sc, g, bias=b, geglu=True, weight_f16=wf)
 
 
-def resnet_fwd(res, x, temb_silu, skip=None):
-    """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1)."""
+def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
+    """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1).
+    tp: this block's time_emb_proj(silu(temb)) when precomputed by temb_projections()."""
     xin = K.concat_c(x, skip) if skip is not None else x
     q1 = conv_qbits(res.conv1)
     h = K.groupnorm_nhwc(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
                          silu=True, q_bits=max(q1, 0))
-    tp = run_linear(res.time_emb_proj, temb_silu)
+    if tp is None:
+        tp = run_linear(res.time_emb_proj, temb_silu)
     h = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp)
     q2 = conv_qbits(res.conv2)
     h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
@@ -478,14 +529,50 @@ def transformer_fwd(tm, x, ctx_kv):
     return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x)
 
 
+def _qkv_operand(attn):
+    """(weight [3C, C], fmt, scales, group, fp16 weight) of to_q | to_k | to_v stacked along N, or
+    None when the three projections cannot share one GEMM (calibration hooks, input act-quant,
+    output quant, biases, or differing code formats).  Cached; rebuilt when a buffer changes."""
+    layers = (attn.to_q, attn.to_k, attn.to_v)
+    for l in layers:
+        if getattr(l, "_qd_hook", None) is not None or l.bias is not None:
+            return None
+        if isinstance(l, WxAxLinear) and (l.quantize_act or l.output_quant_name != "None"):
+            return None
+    ops = [l.gemm_weight() if isinstance(l, WxAxLinear) else (_f16(l.weight), "f16", None, 0) for l in layers]
+    if len({(o[1], o[3]) for o in ops}) != 1:
+        return None
+    ver = tuple((o[0].data_ptr(), o[0]._version, l.weight.data_ptr(), l.weight._version) for o, l in zip(ops, layers))
+    cache = getattr(attn, "_qd_qkv", None)
+    if cache is not None and cache[0] == ver:
+        return cache[1]
+    fmt, g = ops[0][1], ops[0][3]
+    w = torch.cat([o[0] for o in ops]).contiguous()
+    sc = torch.cat([o[2] for o in ops]).contiguous() if fmt != "f16" else None
+    wf = torch.cat([l.weight.detach() for l in layers]).contiguous() if fmt != "f16" else None
+    op = (w, fmt, sc, g, wf)
+    attn._qd_qkv = (ver, op)
+    return op
+
+
+def self_attn_qkv(attn, h, n, s):
+    """q, k, v [n, s, C] views of ONE projection GEMM with the three weights stacked (same
+    input, same per-row math as three F.linear calls)."""
+    c = h.shape[1]
+    op = _qkv_operand(attn)
+    if op is None:
+        return tuple(run_linear(l, h).view(n, s, c) for l in (attn.to_q, attn.to_k, attn.to_v))
+    w, fmt, sc, g, wf = op
+    y = K.linear(h, w, fmt, sc, g, weight_f16=wf).view(n, s, 3 * c)
+    return y[:, :, :c], y[:, :, c:2 * c], y[:, :, 2 * c:]
+
+
 def block_fwd(blk, t, n, s, ctx_kv):
     """BasicTransformerBlock: self-attn, cross-attn, GEGLU feed-forward, each + residual."""
     c = t.shape[1]
     a1 = blk.attn1
     h = K.layernorm(t, blk.norm1.eps, _f16(blk.norm1.weight), _f16(blk.norm1.bias))
-    q = run_linear(a1.to_q, h).view(n, s, c)
-    k = run_linear(a1.to_k, h).view(n, s, c)
-    v = run_linear(a1.to_v, h).view(n, s, c)
+    q, k, v = self_attn_qkv(a1, h, n, s)
     o = K.attention(q, k, v, a1.heads)
     t = run_linear(a1.to_out[0], o.view(-1, c), residual=t)
     a2 = blk.attn2

@@ -245,7 +245,8 @@ def test_gemm_plans_split_k_for_small_m():
 
 # ------------------------------------------------------------------ attention
 @pytest.mark.parametrize("b,heads,sq,skv,d", [(2, 8, 256, 256, 40), (2, 8, 64, 77, 80), (1, 8, 128, 77, 160),
-                                              (2, 5, 200, 200, 64), (1, 2, 4096, 4096, 40)])
+                                              (2, 5, 200, 200, 64), (1, 2, 4096, 4096, 40), (4, 8, 4000, 333, 40),
+                                              (4, 8, 4096, 1024, 80)])
 def test_attention(b, heads, sq, skv, d, dev):
     k = K()
     g = torch.Generator().manual_seed(sq + skv + d)
@@ -302,7 +303,7 @@ def test_groupnorm_two_sources(dev):
     assert torch.equal(y1, y2)
 
 
-@pytest.mark.parametrize("rows,c", [(77, 320), (4096, 640), (33, 1280), (5, 2048)])
+@pytest.mark.parametrize("rows,c", [(77, 320), (4096, 640), (33, 1280), (5, 2048), (8195, 320), (20001, 160), (3, 3072)])
 def test_layernorm(rows, c, dev):
     k = K()
     g = torch.Generator().manual_seed(rows + c)
