@@ -144,6 +144,14 @@ int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n
 int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
                  float eps, const void* gamma, const void* beta, int silu, int q_bits,
                  void* y, float* ws, void* stream);
+/* qd_groupnorm on the finalized output of the conv that feeds it, recomputed on the fly from
+ * the raw conv output y_raw [N, HW, C]: x = half(fq(y_raw; in_amax[n][c], in_bits) + cadd[n][c])
+ * (in_bits 0: no quantization; cadd [N][cadd_ld] may be NULL) - the q_y = output_quant(y) of
+ * fake_quant.py:340 and the diffusers time-embedding add of ResnetBlock2D, without writing
+ * that tensor (qd_fq_finalize semantics). */
+int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int in_bits, const void* cadd, int cadd_ld,
+                       int n, int hw, int c, int groups, float eps, const void* gamma, const void* beta,
+                       int silu, int q_bits, void* y, float* ws, void* stream);
 /* fp32 elements of the qd_groupnorm workspace for this shape. */
 int qd_groupnorm_workspace(int n, int hw, int c, int groups);
 /* LayerNorm over the last dim C of [rows, C]. */

@@ -32,6 +32,7 @@ SIGNATURES = {
     "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, I, P, P],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
+    "qd_groupnorm_fq_in": [P, P, I, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_layernorm": [P, I, I, F, P, P, P, P],
     "qd_geglu": [P, I, I, P, P],
     "qd_silu": [P, P, I64, P],

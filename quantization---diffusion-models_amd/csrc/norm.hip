@@ -12,11 +12,16 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 static int grid1(long count, int per_block = 256) { return (int)((count + per_block - 1) / per_block); }
 
 // ---------------------------------------------------------------------------------------
-// GroupNorm on NHWC [N, HW, C] (+ SiLU) (+ fused per-(n,c) fake-quant of the output), with an
-// optional second source for channels [c1, C) (the UNet's skip concat, never materialised).
+// GroupNorm on NHWC [N, HW, C] (+ SiLU) (+ fused per-(n,c) fake-quant of the output).
 //
-// Four stream-ordered kernels, all deterministic (fixed-order reductions, max is exact).  The
-// three streaming passes share one geometry: block (bx, by), thread (tx, ty) owns the 8-channel
+// The input is "virtual" (GnIn): either x itself, or x | x2 concatenated along C (the UNet's
+// skip concat, never materialised), or the finalized output of the conv that feeds it,
+// x = half(fq(y; amax[n][c]) + cadd[n][c]) (fake_quant.py:340 output quant + the diffusers
+// time-embedding add), recomputed on the fly from the raw conv output so the finalize pass and
+// its tensor never exist (ResnetBlock2D conv1 -> norm2).
+//
+// Three stream-ordered kernels, all deterministic (fixed-order reductions, max is exact).  The
+// two streaming passes share one geometry: block (bx, by), thread (tx, ty) owns the 8-channel
 // 16-B chunk blockIdx.x * bx + tx of sample blockIdx.y and rows ty, ty + by, ... of row range
 // blockIdx.z: fully coalesced 16-B accesses, per-channel state in registers.
 //   1. k_gn_stats   per-channel shifted sums (shift = the group's first element) and min / max
@@ -24,19 +29,65 @@ static int grid1(long count, int per_block = 256) { return (int)((count + per_bl
 //   2. k_gn_coeff   per (n, c): group mean / rstd from the partials in fixed order ->
 //                   scale = rstd*gamma, bias = beta - scale*mean (torch CPU GroupNorm form);
 //                   [q_bits] the exact per-(n,c) amax of the output from the channel's min / max
-//                   (monotonicity argument at k_gn_coeff), flagging the rare channels it cannot
-//   3. k_gn_amax    [q_bits, SiLU] full max |out| pass for the flagged channels only
-//                   (the input quant of the consuming conv: fake_quant.py:125 reduction)
-//   4. k_gn_apply   y = fq(silu(half(x*a + b)))
+//                   (monotonicity argument below); the rare channels it cannot bound are
+//                   scanned by the same block (the input quant of the consuming conv:
+//                   fake_quant.py:125 reduction)
+//   3. k_gn_apply   y = fq(silu(half(x*a + b)))
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ const f16* gn_src(const f16* x, const f16* x2, int c1, int c, long row,
-                                             int ch) {
-  return ch < c1 ? x + row * c1 + ch : x2 + row * (c - c1) + (ch - c1);
+struct GnIn {
+  const f16* x;
+  const f16* x2;     // channels [c1, c) (row stride c - c1) or null
+  int c1;
+  const float* amax; // virtual input: per-(n, c) amax of the raw conv output (null: none)
+  int qmax;          // ... and its fake-quant qmax (0: no quantization)
+  const f16* cadd;   // ... + cadd[n * cadd_ld + c] (null: none)
+  int cadd_ld;
+};
+
+// per-channel input transform state of one 8-channel chunk of sample n
+struct GnXf {
+  float s[8];
+  double rs[8];
+  float ca[8];
+};
+
+__device__ __forceinline__ void gn_xf_init(const GnIn& in, int c, long n, int ch, GnXf& t) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    t.s[j] = in.qmax > 0 ? fq_scale(in.amax[n * c + ch + j], in.qmax) : 0.f;
+    t.rs[j] = in.qmax > 0 ? 1.0 / (double)t.s[j] : 0.0;
+    t.ca[j] = in.cadd ? (float)in.cadd[n * in.cadd_ld + ch + j] : 0.f;
+  }
+}
+
+__device__ __forceinline__ f16x8 gn_load8(const GnIn& in, int c, long row, int ch, const GnXf& t) {
+  const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
+  f16x8 v = *reinterpret_cast<const f16x8*>(p);
+  if (in.qmax > 0 || in.cadd) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f16 q = in.qmax > 0 ? fq_apply_r((float)v[j], t.s[j], t.rs[j]) : v[j];
+      v[j] = in.cadd ? (f16)((float)q + t.ca[j]) : q;
+    }
+  }
+  return v;
+}
+
+// single element (coefficient kernel: shifts and the fallback scan)
+__device__ __forceinline__ float gn_load1(const GnIn& in, int c, long n, long row, int ch) {
+  const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
+  f16 v = *p;
+  if (in.qmax > 0) {
+    const float s = fq_scale(in.amax[n * c + ch], in.qmax);
+    v = fq_apply_r((float)v, s, 1.0 / (double)s);
+  }
+  if (in.cadd) v = (f16)((float)v + (float)in.cadd[n * in.cadd_ld + ch]);
+  return (float)v;
 }
 
 struct GnGeom {
-  int bx, by, gx, z, rpb;  // streaming passes
-  int bys, zs, rpbs;       // stats / amax passes: 1024-thread blocks, 4 rows per thread
+  int bx, by, gx, z, rpb;  // apply pass
+  int bys, zs, rpbs;       // stats pass: 1024-thread blocks, 4 rows per thread
 };
 static GnGeom gn_geom(int n, int hw, int c) {
   GnGeom g;
@@ -60,8 +111,7 @@ __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
   return (float)o;
 }
 
-__global__ void __launch_bounds__(1024) k_gn_stats(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                   int c1, int hw, int c, int cg, int rows_per_block,
+__global__ void __launch_bounds__(1024) k_gn_stats(GnIn in, int hw, int c, int cg, int rows_per_block,
                                                    float4* __restrict__ part) {
   __shared__ float2 red[1024][8];
   const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
@@ -71,16 +121,18 @@ __global__ void __launch_bounds__(1024) k_gn_stats(const f16* __restrict__ x, co
   const long n = blockIdx.y;
   const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
   float s1[8], s2[8], sh[8], mn[8], mx[8];
+  GnXf xf;
+  if (active) gn_xf_init(in, c, n, ch, xf);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     s1[j] = s2[j] = 0.f;
     mn[j] = INFINITY;
     mx[j] = -INFINITY;
-    sh[j] = active ? (float)*gn_src(x, x2, c1, c, n * hw, (ch + j) / cg * cg) : 0.f;
+    sh[j] = active ? gn_load1(in, c, n, n * hw, (ch + j) / cg * cg) : 0.f;
   }
   if (active) {
     for (int r = r0 + ty; r < r1; r += by) {
-      const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, n * hw + r, ch));
+      const f16x8 v = gn_load8(in, c, n * hw + r, ch, xf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xv = (float)v[j];
@@ -131,18 +183,20 @@ constexpr float SILU_NEG_BOUND = 0.2786f;
 // output is fake-quantized - its exact amax from the channel's min / max input:
 // out = half([silu](half(x * a + b))) is monotone in x on each side of silu's minimum, so
 // max |out| is |out(x_min)| or |out(x_max)| except when SiLU is on and both extremes map below
-// the bound above; those channels are flagged for the (rare) full amax pass.
-__global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, const f16* __restrict__ x,
-                                                  const f16* __restrict__ x2, int c1, int hw, int c, int cg,
+// the bound above; the block then scans those (rare) channels' rows itself.
+__global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, GnIn in, int hw, int c, int cg,
                                                   int Z, float eps, const f16* __restrict__ gamma,
                                                   const f16* __restrict__ beta, int silu, int quant,
-                                                  float2* __restrict__ coef, float* __restrict__ amax,
-                                                  int* __restrict__ flag) {
+                                                  float2* __restrict__ coef, float* __restrict__ amax) {
   __shared__ float red[2][4];
   __shared__ float stat[2];
+  __shared__ int nflag;
+  __shared__ int flagged[1024];
+  __shared__ float fmx[4];
   const int groups = c / cg;
   const int ni = blockIdx.x / groups, g0 = (blockIdx.x % groups) * cg;
   const int t = threadIdx.x;
+  if (t == 0) nflag = 0;
   float s1 = 0.f, s2 = 0.f;
   for (int e = t; e < Z * cg; e += 256) {
     const int z = e / cg, j = e - z * cg;
@@ -163,7 +217,7 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const float cnt = (float)cg * (float)hw;
     const float m = S1 / cnt;                        // mean of the shifted values
     const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
-    stat[0] = m + (float)*gn_src(x, x2, c1, c, (long)ni * hw, g0);
+    stat[0] = m + gn_load1(in, c, ni, (long)ni * hw, g0);
     stat[1] = 1.0f / sqrtf(var + eps);
   }
   __syncthreads();
@@ -184,58 +238,26 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const float top = fabsf(gn_out(sc >= 0.f ? mx : mn, k, silu));  // largest z
     if (!silu) {
       amax[i] = fmaxf(lo, hi);
-      flag[i] = 0;
     } else if (top >= SILU_NEG_BOUND) {
       amax[i] = top;
-      flag[i] = 0;
     } else {
-      amax[i] = 0.f;  // computed by k_gn_amax
-      flag[i] = 1;
+      flagged[atomicAdd(&nflag, 1)] = j;
     }
   }
-}
-
-// fallback amax pass: only blocks owning a flagged channel stream their rows
-__global__ void __launch_bounds__(1024) k_gn_amax(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                  int c1, int hw, int c, int rows_per_block,
-                                                  const float2* __restrict__ coef, int silu,
-                                                  const int* __restrict__ flag, float* __restrict__ amax) {
-  __shared__ float red[1024][8];
-  const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
-  const int chunk = blockIdx.x * bx + tx;
-  const bool active = chunk * 8 < c;
-  const int ch = chunk * 8;
-  const long n = blockIdx.y;
-  int any = 0;
-  if (active)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) any |= flag[n * c + ch + j];
-  if (!__syncthreads_or(any)) return;  // block-uniform
-  const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
-  float m[8];
-  float2 k[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    m[j] = 0.f;
-    k[j] = any ? coef[n * c + ch + j] : make_float2(0.f, 0.f);
-  }
-  if (any)
-    for (int r = r0 + ty; r < r1; r += by) {
-      const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, n * hw + r, ch));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf(gn_out((float)v[j], k[j], silu)));
-    }
-  const int t = ty * bx + tx;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[t][j] = m[j];
   __syncthreads();
-  if (ty == 0 && any) {
-    for (int q = 1; q < by; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], red[q * bx + tx][j]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (flag[n * c + ch + j]) atomic_max_pos(&amax[n * c + ch + j], m[j]);
+  // fallback: a full max |out| scan of each flagged channel by the whole block (fixed order of
+  // channels is irrelevant: max is exact)
+  for (int f = 0; f < nflag; ++f) {
+    const int ch = g0 + flagged[f];
+    const long i = (long)ni * c + ch;
+    const float2 k = coef[i];
+    float m = 0.f;
+    for (int r = t; r < hw; r += 256) m = fmaxf(m, fabsf(gn_out(gn_load1(in, c, ni, (long)ni * hw + r, ch), k, silu)));
+    m = wave_max(m);
+    if ((t & 63) == 0) fmx[t >> 6] = m;
+    __syncthreads();
+    if (t == 0) amax[i] = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));
+    __syncthreads();
   }
 }
 
@@ -243,8 +265,7 @@ __global__ void __launch_bounds__(1024) k_gn_amax(const f16* __restrict__ x, con
 // sample blockIdx.y and rows ty, ty + by, ... of its row range: the per-channel coefficients
 // and fake-quant scales are loaded / computed once per thread, rows stream through.
 // The two sources are both multiples of 8 channels wide (host check).
-__global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, const f16* __restrict__ x2,
-                                                  int c1, int hw, int c, int rows_per_block,
+__global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int rows_per_block,
                                                   const float2* __restrict__ coef, int silu, int qmax,
                                                   const float* __restrict__ amax, f16* __restrict__ y) {
   const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
@@ -255,6 +276,8 @@ __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, con
   float2 k[8];
   float sq[8];
   double rq[8];
+  GnXf xf;
+  gn_xf_init(in, c, n, ch, xf);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     k[j] = coef[n * c + ch + j];
@@ -263,7 +286,7 @@ __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, con
   }
   for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
     const long row = n * hw + r;
-    const f16x8 v = *reinterpret_cast<const f16x8*>(gn_src(x, x2, c1, c, row, ch));
+    const f16x8 v = gn_load8(in, c, row, ch, xf);
     f16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -276,40 +299,49 @@ __global__ void __launch_bounds__(256) k_gn_apply(const f16* __restrict__ x, con
 
 extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
   const GnGeom g = gn_geom(n, hw, c);
-  return 4 * n * g.zs * c + 2 * n * c + n * c + n * c;  // partials (float4), coef (float2), amax, flags
+  return 4 * n * g.zs * c + 2 * n * c + n * c + n * c;  // partials (float4), coef (float2), amax, spare
 }
 
-extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
-                            float eps, const void* gamma, const void* beta, int silu, int q_bits,
-                            void* y, float* ws, void* stream) {
-  QD_REQUIRE(x && gamma && beta && y && ws, "null pointer");
+static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float eps, const void* gamma,
+                         const void* beta, int silu, int q_bits, void* y, float* ws, hipStream_t st) {
+  QD_REQUIRE(in.x && gamma && beta && y && ws, "null pointer");
   QD_REQUIRE(groups > 0 && c % groups == 0, "groups must divide C");
   QD_REQUIRE(c % 8 == 0, "GroupNorm needs C % 8 == 0");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "workspace must be 16-B aligned");
-  if (x2) QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c, "bad concat split (must be a multiple of 8)");
-  else c1 = c;
   QD_REQUIRE(q_bits == 0 || (q_bits >= 2 && q_bits <= 16), "bad q_bits");
+  QD_REQUIRE(c / groups <= 1024, "GroupNorm supports at most 1024 channels per group");
   if ((long)n * hw == 0) return 0;
-  hipStream_t st = S(stream);
   const int cg = c / groups;
   const GnGeom g = gn_geom(n, hw, c);
   float4* part = reinterpret_cast<float4*>(ws);
   float2* coef = reinterpret_cast<float2*>(part + (long)n * g.zs * c);
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
-  int* flag = reinterpret_cast<int*>(amax + (long)n * c);
-  const dim3 grid(g.gx, n, g.z), block(g.bx, g.by);
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
-  k_gn_stats<<<dim3(g.gx, n, g.zs), dim3(g.bx, g.bys), 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, cg, g.rpbs,
-                                                                 part);
-  k_gn_coeff<<<n * groups, 256, 0, st>>>(part, (const f16*)x, (const f16*)x2, c1, hw, c, cg, g.zs, eps,
-                                         (const f16*)gamma, (const f16*)beta, silu, qmax > 0, coef, amax, flag);
-  if (qmax && silu)  // only channels whose extremes cannot bound the SiLU output stream here
-    k_gn_amax<<<dim3(g.gx, n, g.zs), dim3(g.bx, g.bys), 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, g.rpbs,
-                                                                  coef, silu, flag, amax);
-  k_gn_apply<<<grid, block, 0, st>>>((const f16*)x, (const f16*)x2, c1, hw, c, g.rpb, coef, silu, qmax, amax,
-                                     (f16*)y);
+  k_gn_stats<<<dim3(g.gx, n, g.zs), dim3(g.bx, g.bys), 0, st>>>(in, hw, c, cg, g.rpbs, part);
+  k_gn_coeff<<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta, silu,
+                                         qmax > 0, coef, amax);
+  k_gn_apply<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>(in, hw, c, g.rpb, coef, silu, qmax, amax, (f16*)y);
   QD_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
+                            float eps, const void* gamma, const void* beta, int silu, int q_bits,
+                            void* y, float* ws, void* stream) {
+  if (x2) QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c, "bad concat split (must be a multiple of 8)");
+  else c1 = c;
+  GnIn in{(const f16*)x, (const f16*)x2, c1, nullptr, 0, nullptr, 0};
+  return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
+}
+
+extern "C" int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int in_bits, const void* cadd,
+                                  int cadd_ld, int n, int hw, int c, int groups, float eps, const void* gamma,
+                                  const void* beta, int silu, int q_bits, void* y, float* ws, void* stream) {
+  QD_REQUIRE(in_bits == 0 || (in_bits >= 2 && in_bits <= 16 && in_amax), "bad input quant bits / amax");
+  if (cadd_ld <= 0) cadd_ld = c;
+  QD_REQUIRE(!cadd || (cadd_ld >= c && cadd_ld % 8 == 0), "bad cadd leading dim");
+  GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld};
+  return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
 }
 
 // ---------------------------------------------------------------------------------------

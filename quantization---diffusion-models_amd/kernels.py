@@ -328,7 +328,11 @@ def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
 
 
 # ---------------------------------------------------------------- norms / elementwise
-def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, out=None):
+def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, out=None, fq_in=None):
+    """GroupNorm(+SiLU)(+per-(n,c) output fake-quant) of NHWC x (| x2 along C).
+    fq_in = (amax [N*C] fp32, bits, cadd [N, C] or None): x is a RAW conv output and the
+    normalised input is its finalized value half(fq(x) + cadd) (fq_finalize semantics),
+    recomputed on the fly instead of materialised."""
     _chk(x, "x")
     n = x.shape[0]
     c1 = x.shape[-1]
@@ -338,6 +342,18 @@ def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, o
         out = _empty((*x.shape[:-1], c), torch.float16, x.device)
     wsn = _lib.load().qd_groupnorm_workspace(n, hw, c, groups)
     ws = _empty((wsn,), torch.float32, x.device)
+    if fq_in is not None:
+        if x2 is not None:
+            raise ValueError("fq_in GroupNorm takes a single source")
+        amax, bits, cadd = fq_in
+        ld = 0
+        if cadd is not None:
+            if cadd.dim() != 2 or cadd.stride(1) != 1 or cadd.dtype != torch.float16:
+                raise ValueError("cadd must be an fp16 [N, C] tensor with unit column stride")
+            ld = cadd.stride(0)
+        _lib.call("qd_groupnorm_fq_in", _p(x), _p(amax), bits, _p(cadd), ld, n, hw, c, groups, float(eps),
+                  _p(gamma), _p(beta), 1 if silu else 0, q_bits, _p(out), _p(ws), _stream())
+        return out
     _lib.call("qd_groupnorm", _p(x), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma), _p(beta),
               1 if silu else 0, q_bits, _p(out), _p(ws), _stream())
     return out

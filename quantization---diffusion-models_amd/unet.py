@@ -407,9 +407,13 @@ def _conv_weight(layer, co_pad=None):
     return wk, b
 
 
-def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=False, c_valid=0, co_pad=None):
+def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=False, c_valid=0, co_pad=None,
+             defer=False):
     """NHWC conv of an nn.Conv2d or WxAxConv2d with the reference's act fake-quant semantics:
-    q_x = act_quant(x) -> y = conv(q_x) + b -> q_y = act_quant(y) -> [+ residual | + temb]."""
+    q_x = act_quant(x) -> y = conv(q_x) + b -> q_y = act_quant(y) -> [+ residual | + temb].
+    defer=True (no residual): return (y_raw, (amax, bits, chan_add)) instead of finalizing, for
+    a consumer that applies the output quant + add on the fly (groupnorm_nhwc fq_in); the spec
+    is None when y is already final."""
     if isinstance(layer, WxAxConv2d):
         layer._check_supported()
     wk, bias = _conv_weight(layer, co_pad)
@@ -417,7 +421,8 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
     ci = layer.weight.shape[1]
     q = conv_qbits(layer)
     if q < 0:  # non-per_channel act granularity: run the drop-in NCHW module (same kernels)
-        return _conv_via_module(layer, x, residual, chan_add, upsample, co_pad)
+        y = _conv_via_module(layer, x, residual, chan_add, upsample, co_pad)
+        return (y, None) if defer else y
     if q and not prequant:
         amax = K.act_absmax(x, "per_channel", K.NHWC)
         x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
@@ -425,10 +430,15 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         n = x.shape[0]
         amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
         y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)
+        if defer and residual is None:
+            return y, (amax, q, chan_add)
         return K.fq_finalize(y, amax, q, residual=residual, chan_add=chan_add, out=y)
     if chan_add is None:
-        return K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, residual=residual)
+        y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, residual=residual)
+        return (y, None) if defer else y
     y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias)
+    if defer and residual is None:
+        return y, (None, 0, chan_add)
     return K.fq_finalize(y, None, 0, residual=residual, chan_add=chan_add, out=y)
 
 
@@ -503,10 +513,11 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
                          silu=True, q_bits=max(q1, 0))
     if tp is None:
         tp = run_linear(res.time_emb_proj, temb_silu)
-    h = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp)
+    # conv1's output quant + temb add are applied inside norm2 (never materialised)
+    h, spec = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp, defer=True)
     q2 = conv_qbits(res.conv2)
     h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
-                         silu=True, q_bits=max(q2, 0))
+                         silu=True, q_bits=max(q2, 0), fq_in=spec)
     sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
     return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc)
 

@@ -417,3 +417,35 @@ def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     ref = (h * F.gelu(gt).half().float()).half().float()
     tol = 2 * ulp16(ref) + 2 * ulp16(h) * gt.abs() + 2.5 * h.abs() * ulp16(gt) + 1e-3
     assert ((fused - ref).abs() <= tol).all(), (variant, (fused - ref).abs().max().item())
+
+
+@pytest.mark.parametrize("bits,with_cadd", [(8, True), (0, True), (8, False), (4, True)])
+def test_groupnorm_fq_in_matches_finalize_then_norm(bits, with_cadd, dev):
+    """GroupNorm on a raw conv output with the output quant + temb add applied on the fly equals
+    fq_finalize followed by GroupNorm, bit for bit; includes channels whose SiLU output stays
+    below the extremes bound (tiny gamma, negative beta) so the fallback amax scan runs."""
+    k = K()
+    g = torch.Generator().manual_seed(bits * 3 + with_cadd)
+    n, hw, c = 2, 256, 640
+    y = (torch.randn(n, hw, c, generator=g) * 1.5).half().to(dev)
+    amax = y.float().abs().amax(dim=1).reshape(-1).contiguous() if bits else None
+    big = (torch.randn(n, 2 * c, generator=g) * 0.3).half().to(dev)
+    cadd = big[:, 100 * 8: 100 * 8 + c] if with_cadd else None  # row-strided view, like the stacked temb
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
+    bet = (0.1 * torch.randn(c, generator=g)).half()
+    gam[::37] = 0.01
+    bet[::37] = -0.5
+    gam, bet = gam.to(dev), bet.to(dev)
+    fin = k.fq_finalize(y, amax, bits, chan_add=cadd)
+    ref = k.groupnorm_nhwc(fin, 32, 1e-5, gam, bet, silu=True, q_bits=8)
+    got = k.groupnorm_nhwc(y, 32, 1e-5, gam, bet, silu=True, q_bits=8, fq_in=(amax, bits, cadd))
+    assert torch.equal(got, ref)
+    # the fallback-scanned channels are quantized with their exact amax
+    # (torch-CPU Half ops, the reference's op-boundary rounding, as test_groupnorm_fused)
+    gn = F.group_norm(fin.cpu().transpose(1, 2).reshape(n, c, hw, 1), 32, gam.cpu(), bet.cpu(), 1e-5)
+    ref2 = FT.per_channel(F.silu(gn), 8)
+    got2 = got.cpu().transpose(1, 2).reshape(n, c, hw, 1)
+    step = ref2.float().abs().amax(dim=(2, 3), keepdim=True) / 127
+    err = (got2.float() - ref2.float()).abs()
+    assert (err <= step * 1.01 + 1e-3).all(), err.max().item()
+    assert (err <= 1e-3).float().mean() > 0.995
