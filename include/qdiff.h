@@ -71,6 +71,13 @@ int qd_act_fakequant(const void* x, void* y, int layout, int n, int c, int h, in
 int qd_act_apply(const void* x, void* y, int layout, int n, int c, int h, int w, int gran,
                  int group, int n_bits, const float* amax, void* stream);
 
+/* quantize_activation_per_channel_absmax (fake_quant.py:123-131) of the NHWC channel concat
+ * [x (c1) | x2 (c2)] -> y [n, hw, c1 + c2]: the UNet skip concat feeding a quantized conv,
+ * materialised only in its quantized form.  amax: fp32 [n*(c1+c2)] workspace (zeroed by the
+ * call unless amax_zeroed). */
+int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,
+                          float* amax, int amax_zeroed, void* y, void* stream);
+
 /* ---------------- weight fake-quant (offline, on device) ----------------------------- */
 /* Row-group absmax RTN of quantize_weight_absmax / _per_channel_ / _per_tensor_
  * (fake_quant.py:21-105).  w is [rows, cols] fp16 (a 4-D conv weight is [Co*Ci*kh, kw]);
@@ -204,6 +211,12 @@ int qd_channel_absmax_accum(const void* x, int64_t rows, int c, float* amax_ws, 
 int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const int* fc_rows, int nfc, int c,
                    const void* act_mean, float alpha, float* wmax_ws, void* scales_out,
                    void* stream);
+
+/* ---------------- self-tests (test infrastructure) ---------------------------------- */
+/* Exhaustive check of the reciprocal shortcut used by every fake-quant apply kernel against the
+ * IEEE-division form (all fp16 scales, values around every quantization midpoint): counts[0] =
+ * reciprocal errors > 1 ulp, counts[1] = differing fake-quant results (device int[2]). */
+int qd_selftest_recip(int* counts, void* stream);
 
 #ifdef __cplusplus
 }

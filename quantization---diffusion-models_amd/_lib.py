@@ -25,6 +25,7 @@ SIGNATURES = {
     "qd_act_absmax": [P, I, I, I, I, I, I, I, P, P],
     "qd_act_fakequant": [P, P, I, I, I, I, I, I, I, I, P, P],
     "qd_act_apply": [P, P, I, I, I, I, I, I, I, I, P, P],
+    "qd_act_quant_cat_nhwc": [P, I, P, I, I, I, I, P, I, P, P],
     "qd_weight_quant": [P, I, I, I, I, P, P, P, P],
     "qd_pack_int4": [P, I, I, P, P],
     "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
@@ -46,6 +47,7 @@ SIGNATURES = {
     "qd_channel_absmax_accum": [P, I64, I, P, P, P, P],
     "qd_smooth_fold": [P, P, P, P, I, I, P, F, P, P, P],
     "qd_gemm_force": [I],
+    "qd_selftest_recip": [P, P],
 }
 
 # size queries (no status code)

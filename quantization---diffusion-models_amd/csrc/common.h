@@ -19,6 +19,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define QD_WAVE 64
 
+// Keep a batch of loads issued back to back: hipcc sinks a load into the (guarded) block that
+// consumes it and waits for it there, serialising a row batch; an empty asm that "uses" each
+// loaded value right after the batch pins the loads in front of it (one vmcnt wait each).
+#define QD_PIN(x) asm volatile("" ::"v"(x))
+
 namespace qd {
 
 // half(1e-5): the fp16 image of clamp_(min=1e-5) (no fp16 lies strictly between 1e-5 and it).
@@ -47,6 +52,31 @@ __device__ __forceinline__ f16 fq_apply_r(float x, float s, double rs) {
   f16 t = (f16)(float)((double)x * rs);
   float q = __builtin_rintf((float)t);
   return (f16)(q * s);
+}
+
+// rs for fq_apply_r: 1 / (double)s from the hardware f64 reciprocal estimate and two Newton
+// steps (relative error <= ~2^-52, the bound the fq_apply_r argument allows, instead of the
+// ~30-instruction IEEE f64 division).  s == 0 -> +inf, as the division.
+__device__ __forceinline__ double rcp_exact(float s) {
+  const double d = (double)s;
+  double r = __builtin_amdgcn_rcp(d);
+  r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+  r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+  return s == 0.f ? __builtin_inf() : r;
+}
+
+// Per-channel fake-quant state of 8 consecutive channels: two 16-B amax loads issued together
+// (a per-element conditional load would make hipcc serialise them), then s and 1/s.
+// amax8 must be 16-B aligned (channel offsets are multiples of 8).
+__device__ __forceinline__ void fq_scales8(const float* amax8, int qmax, float (&s)[8], double (&rs)[8]) {
+  const float4 a0 = reinterpret_cast<const float4*>(amax8)[0];
+  const float4 a1 = reinterpret_cast<const float4*>(amax8)[1];
+  const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s[j] = fq_scale(a[j], qmax);
+    rs[j] = rcp_exact(s[j]);
+  }
 }
 
 __device__ __forceinline__ float wave_max(float v) {

@@ -52,22 +52,36 @@ struct GnXf {
 };
 
 __device__ __forceinline__ void gn_xf_init(const GnIn& in, int c, long n, int ch, GnXf& t) {
+  if (in.qmax > 0) {
+    fq_scales8(in.amax + n * c + ch, in.qmax, t.s, t.rs);
+  } else {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    t.s[j] = in.qmax > 0 ? fq_scale(in.amax[n * c + ch + j], in.qmax) : 0.f;
-    t.rs[j] = in.qmax > 0 ? 1.0 / (double)t.s[j] : 0.0;
-    t.ca[j] = in.cadd ? (float)in.cadd[n * in.cadd_ld + ch + j] : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      t.s[j] = 0.f;
+      t.rs[j] = 0.0;
+    }
   }
+  f16x8 ca = {};
+  if (in.cadd) ca = *reinterpret_cast<const f16x8*>(in.cadd + n * in.cadd_ld + ch);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t.ca[j] = (float)ca[j];
 }
 
+// XF: 0 plain source(s); 1 finalize transform (output quant if in.qmax > 0, + cadd if set:
+// a zero cadd adds +0, which leaves every fp16 value - including -0 - bit-identical... except
+// -0 + +0 = +0; the callers pass cadd only when the reference adds it)
+template <int XF>
 __device__ __forceinline__ f16x8 gn_load8(const GnIn& in, int c, long row, int ch, const GnXf& t) {
   const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
   f16x8 v = *reinterpret_cast<const f16x8*>(p);
-  if (in.qmax > 0 || in.cadd) {
+  if constexpr (XF == 1) {
+    const bool q = in.qmax > 0, a = in.cadd != nullptr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const f16 q = in.qmax > 0 ? fq_apply_r((float)v[j], t.s[j], t.rs[j]) : v[j];
-      v[j] = in.cadd ? (f16)((float)q + t.ca[j]) : q;
+      f16 o = v[j];
+      if (q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
+      if (a) o = (f16)((float)o + t.ca[j]);
+      v[j] = o;
     }
   }
   return v;
@@ -79,7 +93,7 @@ __device__ __forceinline__ float gn_load1(const GnIn& in, int c, long n, long ro
   f16 v = *p;
   if (in.qmax > 0) {
     const float s = fq_scale(in.amax[n * c + ch], in.qmax);
-    v = fq_apply_r((float)v, s, 1.0 / (double)s);
+    v = fq_apply_r((float)v, s, rcp_exact(s));
   }
   if (in.cadd) v = (f16)((float)v + (float)in.cadd[n * in.cadd_ld + ch]);
   return (float)v;
@@ -111,6 +125,7 @@ __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
   return (float)o;
 }
 
+template <int XF>
 __global__ void __launch_bounds__(1024) k_gn_stats(GnIn in, int hw, int c, int cg, int rows_per_block,
                                                    float4* __restrict__ part) {
   __shared__ float2 red[1024][8];
@@ -131,16 +146,26 @@ __global__ void __launch_bounds__(1024) k_gn_stats(GnIn in, int hw, int c, int c
     sh[j] = active ? gn_load1(in, c, n, n * hw, (ch + j) / cg * cg) : 0.f;
   }
   if (active) {
-    for (int r = r0 + ty; r < r1; r += by) {
-      const f16x8 v = gn_load8(in, c, n * hw + r, ch, xf);
+    // 4 rows per batch, all loads issued before any use (memory-level parallelism)
+    for (int rb = r0 + ty; rb < r1; rb += 4 * by) {
+      f16x8 v[4];
+      // unconditional loads (row clamped): a guarded load makes hipcc wait per load
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xv = (float)v[j];
-        const float a = xv - sh[j];
-        s1[j] += a;
-        s2[j] = fmaf(a, a, s2[j]);
-        mn[j] = fminf(mn[j], xv);
-        mx[j] = fmaxf(mx[j], xv);
+      for (int u = 0; u < 4; ++u) v[u] = gn_load8<XF>(in, c, n * hw + min(rb + u * by, r1 - 1), ch, xf);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (rb + u * by >= r1) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xv = (float)v[u][j];
+          const float a = xv - sh[j];
+          s1[j] += a;
+          s2[j] = fmaf(a, a, s2[j]);
+          mn[j] = fminf(mn[j], xv);
+          mx[j] = fmaxf(mx[j], xv);
+        }
       }
     }
   }
@@ -265,8 +290,9 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
 // sample blockIdx.y and rows ty, ty + by, ... of its row range: the per-channel coefficients
 // and fake-quant scales are loaded / computed once per thread, rows stream through.
 // The two sources are both multiples of 8 channels wide (host check).
+template <int XF, int SILU, bool Q>
 __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int rows_per_block,
-                                                  const float2* __restrict__ coef, int silu, int qmax,
+                                                  const float2* __restrict__ coef, int qmax,
                                                   const float* __restrict__ amax, f16* __restrict__ y) {
   const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
   if (chunk * 8 >= c) return;
@@ -278,22 +304,36 @@ __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int ro
   double rq[8];
   GnXf xf;
   gn_xf_init(in, c, n, ch, xf);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    k[j] = coef[n * c + ch + j];
-    sq[j] = qmax > 0 ? fq_scale(amax[n * c + ch + j], qmax) : 0.f;
-    rq[j] = qmax > 0 ? 1.0 / (double)sq[j] : 0.0;
+  {
+    const float4* cp = reinterpret_cast<const float4*>(coef + n * c + ch);
+    const float4 k0 = cp[0], k1 = cp[1], k2 = cp[2], k3 = cp[3];
+    k[0] = make_float2(k0.x, k0.y); k[1] = make_float2(k0.z, k0.w);
+    k[2] = make_float2(k1.x, k1.y); k[3] = make_float2(k1.z, k1.w);
+    k[4] = make_float2(k2.x, k2.y); k[5] = make_float2(k2.z, k2.w);
+    k[6] = make_float2(k3.x, k3.y); k[7] = make_float2(k3.z, k3.w);
   }
-  for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
-    const long row = n * hw + r;
-    const f16x8 v = gn_load8(in, c, row, ch, xf);
-    f16x8 o;
+  if constexpr (Q) {
+    fq_scales8(amax + n * c + ch, qmax, sq, rq);
+  }
+  const int by = blockDim.y;
+  for (int rb = r0 + threadIdx.y; rb < r1; rb += 4 * by) {
+    f16x8 v[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float val = gn_out((float)v[j], k[j], silu);
-      o[j] = qmax > 0 ? fq_apply_r(val, sq[j], rq[j]) : (f16)val;
+    for (int u = 0; u < 4; ++u) v[u] = gn_load8<XF>(in, c, n * hw + min(rb + u * by, r1 - 1), ch, xf);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + u * by >= r1) break;
+      f16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float val = gn_out((float)v[u][j], k[j], SILU);
+        if constexpr (Q) o[j] = fq_apply_r(val, sq[j], rq[j]);
+        else o[j] = (f16)val;
+      }
+      *reinterpret_cast<f16x8*>(y + (n * hw + rb + u * by) * c + ch) = o;
     }
-    *reinterpret_cast<f16x8*>(y + row * c + ch) = o;
   }
 }
 
@@ -317,10 +357,27 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   float2* coef = reinterpret_cast<float2*>(part + (long)n * g.zs * c);
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
-  k_gn_stats<<<dim3(g.gx, n, g.zs), dim3(g.bx, g.bys), 0, st>>>(in, hw, c, cg, g.rpbs, part);
+  const bool xf = in.qmax > 0 || in.cadd;
+  const dim3 gs(g.gx, n, g.zs), bs(g.bx, g.bys);
+  if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part);
+  else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part);
   k_gn_coeff<<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta, silu,
                                          qmax > 0, coef, amax);
-  k_gn_apply<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>(in, hw, c, g.rpb, coef, silu, qmax, amax, (f16*)y);
+  const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
+#define QD_GN_APPLY(XFV, SV, QV) \
+  k_gn_apply<XFV, SV, QV><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, qmax, amax, (f16*)y)
+  const int sel = (xf ? 4 : 0) | (silu ? 2 : 0) | (qmax > 0 ? 1 : 0);
+  switch (sel) {
+    case 0: QD_GN_APPLY(0, 0, false); break;
+    case 1: QD_GN_APPLY(0, 0, true); break;
+    case 2: QD_GN_APPLY(0, 1, false); break;
+    case 3: QD_GN_APPLY(0, 1, true); break;
+    case 4: QD_GN_APPLY(1, 0, false); break;
+    case 5: QD_GN_APPLY(1, 0, true); break;
+    case 6: QD_GN_APPLY(1, 1, false); break;
+    default: QD_GN_APPLY(1, 1, true); break;
+  }
+#undef QD_GN_APPLY
   QD_CHECK_LAUNCH();
   return 0;
 }
@@ -486,20 +543,23 @@ extern "C" int qd_add(const void* a, const void* b, void* y, int64_t count, void
   return 0;
 }
 
+// 16-B chunks (c1, c2 multiples of 8)
 __global__ void k_concat(const f16* __restrict__ a, int c1, const f16* __restrict__ b, int c2, long m,
                          f16* __restrict__ out) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  const int c = c1 + c2;
-  if (e >= m * c) return;
-  const long r = e / c;
-  const int ch = e % c;
-  out[e] = ch < c1 ? a[r * c1 + ch] : b[r * c2 + ch - c1];
+  const int cc = (c1 + c2) >> 3;
+  if (e >= m * cc) return;
+  const long r = e / cc;
+  const int ch = (int)(e - r * cc) * 8;
+  const f16* src = ch < c1 ? a + r * c1 + ch : b + r * c2 + ch - c1;
+  *reinterpret_cast<f16x8*>(out + e * 8) = *reinterpret_cast<const f16x8*>(src);
 }
 
 extern "C" int qd_concat_c(const void* a, int c1, const void* b, int c2, int64_t m, void* out, void* stream) {
   QD_REQUIRE(a && b && out, "null pointer");
+  QD_REQUIRE(c1 % 8 == 0 && c2 % 8 == 0, "concat needs both widths to be multiples of 8");
   if (m == 0) return 0;
-  k_concat<<<grid1(m * (c1 + c2)), 256, 0, S(stream)>>>((const f16*)a, c1, (const f16*)b, c2, m, (f16*)out);
+  k_concat<<<grid1(m * ((c1 + c2) / 8)), 256, 0, S(stream)>>>((const f16*)a, c1, (const f16*)b, c2, m, (f16*)out);
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -57,8 +57,9 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 
 // NHWC per-(n, c) column max over rows.  block (64, 4): x = 8-channel chunk, y = row lane.
 // grid (ceil(c/8/64), n, row_splits).  requires c % 8 == 0.
-__global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, int hw, int c,
-                                                     int rows_per_split, float* __restrict__ amax) {
+// x2 != null: channels [c1, c) come from x2 (row stride c - c1), [0, c1) from x (row stride c1)
+__global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, const f16* __restrict__ x2, int c1,
+                                                     int hw, int c, int rows_per_split, float* __restrict__ amax) {
   __shared__ float red[4][64][8];
   const int chunk = blockIdx.x * 64 + threadIdx.x;
   const int n = blockIdx.y;
@@ -68,11 +69,22 @@ __global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) m[j] = 0.f;
   if (chunk * 8 < c) {
-    const f16* base = x + (size_t)n * hw * c + chunk * 8;
-    for (int r = r0 + threadIdx.y; r < r1; r += 4) {
-      f16x8 v = *reinterpret_cast<const f16x8*>(base + (size_t)r * c);
+    const int ch = chunk * 8;
+    const bool first = x2 == nullptr || ch < c1;
+    const int ld = x2 == nullptr ? c : (first ? c1 : c - c1);
+    const f16* base = first ? x + (size_t)n * hw * ld + ch : x2 + (size_t)n * hw * ld + (ch - c1);
+    for (int rb = r0 + threadIdx.y; rb < r1; rb += 16) {
+      f16x8 v[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)v[j]));
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f16x8*>(base + (size_t)min(rb + 4 * u, r1 - 1) * ld);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (rb + 4 * u >= r1) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)v[u][j]));
+      }
     }
   }
 #pragma unroll
@@ -162,28 +174,35 @@ static CrGeom cr_geom(int n, long hw, int c) {
   return g;
 }
 
-__global__ void __launch_bounds__(256) k_apply_nhwc(const f16* __restrict__ x, f16* __restrict__ y,
-                                                    int hw, int c, int c_valid, int qmax, int rows_per_block,
-                                                    const float* __restrict__ amax) {
+__global__ void __launch_bounds__(256) k_apply_nhwc(const f16* __restrict__ x, const f16* __restrict__ x2, int c1,
+                                                    f16* __restrict__ y, int hw, int c, int c_valid, int qmax,
+                                                    int rows_per_block, const float* __restrict__ amax) {
   const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
   if (chunk * 8 >= c) return;
   const int ch = chunk * 8;
+  const bool first = x2 == nullptr || ch < c1;
+  const int ld = x2 == nullptr ? c : (first ? c1 : c - c1);
+  const f16* src = first ? x + ch : x2 + (ch - c1);
   const long n = blockIdx.y;
   const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
   float sc[8];
   double rs[8];
+  fq_scales8(amax + n * c + ch, qmax, sc, rs);
+  const int by = blockDim.y;
+  for (int rb = r0 + threadIdx.y; rb < r1; rb += 4 * by) {
+    f16x8 v[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = fq_scale(amax[n * c + ch + j], qmax);
-    rs[j] = 1.0 / (double)sc[j];
-  }
-  for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
-    const long e = (n * hw + r) * c + ch;
-    const f16x8 v = *reinterpret_cast<const f16x8*>(x + e);
-    f16x8 o;
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f16x8*>(src + (n * hw + min(rb + u * by, r1 - 1)) * ld);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = ch + j < c_valid ? fq_apply_r((float)v[j], sc[j], rs[j]) : v[j];
-    *reinterpret_cast<f16x8*>(y + e) = o;
+    for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + u * by >= r1) break;
+      f16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = ch + j < c_valid ? fq_apply_r((float)v[u][j], sc[j], rs[j]) : v[u][j];
+      *reinterpret_cast<f16x8*>(y + (n * hw + rb + u * by) * c + ch) = o;
+    }
   }
 }
 
@@ -241,7 +260,7 @@ static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, 
       int rps = 64;
       while (rps < hw && ((hw + rps - 1) / rps) * n * ((chunks + 63) / 64) > 2048) rps *= 2;
       dim3 grid((chunks + 63) / 64, n, (int)((hw + rps - 1) / rps));
-      k_colmax_nhwc<<<grid, dim3(64, 4), 0, st>>>((const f16*)x, (int)hw, c, rps, amax);
+      k_colmax_nhwc<<<grid, dim3(64, 4), 0, st>>>((const f16*)x, nullptr, c, (int)hw, c, rps, amax);
     } else {
       const long rows = (long)n * c;
       k_rowmax<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, rows, (int)hw, amax);
@@ -276,8 +295,8 @@ static int launch_apply(const void* x, void* y, int layout, int n, int c, int h,
     QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
     const int c_valid = group > 0 ? std::min(group, c) : c;
     const CrGeom g = cr_geom(n, hw, c);
-    k_apply_nhwc<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>((const f16*)x, (f16*)y, (int)hw, c, c_valid, qm,
-                                                                   g.rpb, amax);
+    k_apply_nhwc<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>((const f16*)x, nullptr, c, (f16*)y, (int)hw, c,
+                                                                   c_valid, qm, g.rpb, amax);
   } else if (gran == QD_GRAN_PER_CHANNEL) {
     k_apply_generic<<<grid1(count), 256, 0, st>>>((const f16*)x, (f16*)y, count, 0, hw, h, w, 1, qm, amax);
   } else if (gran == QD_GRAN_PER_TOKEN) {
@@ -457,30 +476,49 @@ __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, con
   double rs[8];
   f16x8 ca = {};
   if (cadd && !res) ca = *reinterpret_cast<const f16x8*>(cadd + n * cadd_ld + ch);
+  if (qmax > 0) {
+    fq_scales8(amax + n * c + ch, qmax, sc, rs);
+  } else {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = qmax > 0 ? fq_scale(amax[n * c + ch + j], qmax) : 0.f;
-    rs[j] = qmax > 0 ? 1.0 / (double)sc[j] : 0.0;
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = 0.f;
+      rs[j] = 0.0;
+    }
   }
-  for (int r = r0 + threadIdx.y; r < r1; r += blockDim.y) {
-    const long e = (n * hw + r) * c + ch;
-    const f16x8 v = *reinterpret_cast<const f16x8*>(y + e);
-    f16x8 o;
-    if (qmax > 0) {
+  const int by = blockDim.y;
+  for (int rb = r0 + threadIdx.y; rb < r1; rb += 4 * by) {
+    f16x8 v[4], rr[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fq_apply_r((float)v[j], sc[j], rs[j]);
-    } else {
-      o = v;
+    for (int u = 0; u < 4; ++u) {
+      const long e = (n * hw + min(rb + u * by, r1 - 1)) * c + ch;
+      v[u] = *reinterpret_cast<const f16x8*>(y + e);
+      rr[u] = *reinterpret_cast<const f16x8*>((res ? res : y) + e);
     }
-    if (res) {
-      const f16x8 rr = *reinterpret_cast<const f16x8*>(res + e);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)rr[j]);
-    } else if (cadd) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)ca[j]);
+    for (int u = 0; u < 4; ++u) {
+      QD_PIN(v[u]);
+      QD_PIN(rr[u]);
     }
-    *reinterpret_cast<f16x8*>(out + e) = o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + u * by >= r1) break;
+      const long e = (n * hw + rb + u * by) * c + ch;
+      f16x8 o;
+      if (qmax > 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fq_apply_r((float)v[u][j], sc[j], rs[j]);
+      } else {
+        o = v[u];
+      }
+      if (res) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)rr[u][j]);
+      } else if (cadd) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)ca[j]);
+      }
+      *reinterpret_cast<f16x8*>(out + e) = o;
+    }
   }
 }
 
@@ -499,6 +537,70 @@ extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, i
                                                                       n_bits ? qmax_of(n_bits) : 0, g.rpb,
                                                                       (const f16*)residual, (const f16*)chan_add,
                                                                       chan_add_ld, (f16*)out);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// Self-test of the fq_apply_r / rcp_exact shortcut against the IEEE division form fq_apply:
+// every non-negative finite fp16 scale s, and for each s the fp16 values x next to every
+// quantization midpoint (k + 1/2) s, |k| <= 130, plus the midpoint images themselves.
+// counts[0] = scales whose rcp_exact differs from 1 / (double)s by more than 1 f64 ulp,
+// counts[1] = (s, x) pairs whose fake-quant results differ.  Test infrastructure only.
+__global__ void k_selftest_recip(int* counts) {
+  const unsigned short sb = (unsigned short)(blockIdx.x);
+  const f16 sh = __builtin_bit_cast(f16, sb);
+  const float s = (float)sh;
+  if (!(s >= 0.f) || __builtin_isinf(s)) return;
+  const double r = rcp_exact(s), e = 1.0 / (double)s;
+  if (threadIdx.x == 0 && s > 0.f) {
+    const double ulp = __builtin_fabs(e) * 2.220446049250313e-16;
+    if (__builtin_fabs(r - e) > ulp) atomicAdd(&counts[0], 1);
+  }
+  int bad = 0;
+  for (int k = (int)threadIdx.x - 130; k <= 130; k += blockDim.x) {
+    const f16 mid = (f16)(((float)k + 0.5f) * s);
+    const unsigned short mb = __builtin_bit_cast(unsigned short, mid);
+    for (int dlt = -2; dlt <= 2; ++dlt) {
+      const f16 x = __builtin_bit_cast(f16, (unsigned short)(mb + dlt));
+      const float xf = (float)x;
+      if (__builtin_isnan(xf) || __builtin_isinf(xf)) continue;
+      const f16 a = fq_apply(xf, s), b = fq_apply_r(xf, s, r);
+      if (__builtin_bit_cast(unsigned short, a) != __builtin_bit_cast(unsigned short, b) &&
+          !(__builtin_isnan((float)a) && __builtin_isnan((float)b)))
+        ++bad;
+    }
+  }
+  if (bad) atomicAdd(&counts[1], bad);
+}
+
+extern "C" int qd_selftest_recip(int* counts, void* stream) {
+  QD_REQUIRE(counts, "null pointer");
+  hipStream_t st = S(stream);
+  qd_zero_f32(reinterpret_cast<float*>(counts), 2, st);  // int 0 == f32 +0 bits
+  k_selftest_recip<<<65536, 64, 0, st>>>(counts);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// Per-(n, c) fake-quant of the channel concat [x | x2] (NHWC), written as one tensor: the
+// UNet skip concat feeding a quantized conv_shortcut, materialised only in quantized form.
+extern "C" int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,
+                                     float* amax, int amax_zeroed, void* y, void* stream) {
+  QD_REQUIRE(x && x2 && y && amax, "null pointer");
+  QD_REQUIRE(c1 % 8 == 0 && c2 % 8 == 0 && c1 > 0 && c2 > 0, "concat widths must be multiples of 8");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "bad n_bits");
+  const int c = c1 + c2;
+  if ((long)n * hw == 0) return 0;
+  hipStream_t st = S(stream);
+  if (!amax_zeroed) qd_zero_f32(amax, (size_t)n * c, st);
+  const int chunks = c / 8;
+  int rps = 64;
+  while (rps < hw && ((hw + rps - 1) / rps) * n * ((chunks + 63) / 64) > 2048) rps *= 2;
+  k_colmax_nhwc<<<dim3((chunks + 63) / 64, n, (hw + rps - 1) / rps), dim3(64, 4), 0, st>>>(
+      (const f16*)x, (const f16*)x2, c1, hw, c, rps, amax);
+  const CrGeom g = cr_geom(n, hw, c);
+  k_apply_nhwc<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>((const f16*)x, (const f16*)x2, c1, (f16*)y, hw, c,
+                                                                 c, qmax_of(n_bits), g.rpb, amax);
   QD_CHECK_LAUNCH();
   return 0;
 }

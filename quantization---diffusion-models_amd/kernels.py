@@ -104,6 +104,21 @@ def act_apply_nhwc(x, amax, n_bits, out=None, c_valid=0):
     return y
 
 
+def act_quant_cat_nhwc(x, x2, n_bits, out=None):
+    """Per-(n, c) fake-quant of the NHWC channel concat [x | x2] into one [N, H, W, C1+C2] tensor."""
+    _chk(x, "x")
+    _chk(x2, "x2")
+    n, c1, c2 = x.shape[0], x.shape[-1], x2.shape[-1]
+    hw = x.numel() // (n * c1)
+    if x2.numel() // (n * c2) != hw:
+        raise ValueError("concat sources differ in N / HW")
+    y = out if out is not None else _empty((*x.shape[:-1], c1 + c2), torch.float16, x.device)
+    amax, zeroed = A.zeroed_f32(n * (c1 + c2), x.device)
+    _lib.call("qd_act_quant_cat_nhwc", _p(x), c1, _p(x2), c2, n, hw, n_bits, _p(amax), 1 if zeroed else 0, _p(y),
+              _stream())
+    return y
+
+
 # ---------------------------------------------------------------- weight quant
 def weight_quant(w2d, group, n_bits, want_codes=True, want_scales=True, want_dq=True):
     """Row-group absmax RTN of a [rows, cols] fp16 weight (fake_quant.py:21-105)."""

@@ -506,11 +506,28 @@ def ff_geglu(layer, x2d):
 
 def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
     """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1).
-    tp: this block's time_emb_proj(silu(temb)) when precomputed by temb_projections()."""
+    tp: this block's time_emb_proj(silu(temb)) when precomputed by temb_projections().
+    The up-block skip concat is never materialised in fp16: norm1 reads both sources and a
+    quantized conv_shortcut receives the per-(n, c) fake-quant of the concat directly."""
+    qs = conv_qbits(res.conv_shortcut) if res.conv_shortcut is not None else 0
+    if skip is not None and qs > 0:
+        sc = run_conv(res.conv_shortcut, K.act_quant_cat_nhwc(x, skip, qs), prequant=True)
+        h = K.groupnorm_nhwc(x, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
+                             silu=True, q_bits=max(conv_qbits(res.conv1), 0), x2=skip)
+        return _resnet_tail(res, h, temb_silu, tp, sc)
     xin = K.concat_c(x, skip) if skip is not None else x
     q1 = conv_qbits(res.conv1)
     h = K.groupnorm_nhwc(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
                          silu=True, q_bits=max(q1, 0))
+    if tp is None:
+        tp = run_linear(res.time_emb_proj, temb_silu)
+    sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
+    return _resnet_tail(res, h, temb_silu, tp, sc)
+
+
+def _resnet_tail(res, h, temb_silu, tp, sc):
+    """conv1 (+ temb) -> norm2 + SiLU -> conv2 + shortcut, h = silu(norm1(x)) [quantized]."""
+    q1 = conv_qbits(res.conv1)
     if tp is None:
         tp = run_linear(res.time_emb_proj, temb_silu)
     # conv1's output quant + temb add are applied inside norm2 (never materialised)
@@ -518,7 +535,6 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
     q2 = conv_qbits(res.conv2)
     h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                          silu=True, q_bits=max(q2, 0), fq_in=spec)
-    sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
     return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc)
 
 

@@ -449,3 +449,23 @@ def test_groupnorm_fq_in_matches_finalize_then_norm(bits, with_cadd, dev):
     err = (got2.float() - ref2.float()).abs()
     assert (err <= step * 1.01 + 1e-3).all(), err.max().item()
     assert (err <= 1e-3).float().mean() > 0.995
+
+
+def test_act_quant_cat_matches_concat_then_quant(dev):
+    k = K()
+    g = torch.Generator().manual_seed(9)
+    a = (torch.randn(2, 16, 16, 640, generator=g) * 3).half().to(dev)
+    b2 = torch.randn(2, 16, 16, 320, generator=g).half().to(dev)
+    got = k.act_quant_cat_nhwc(a, b2, 8)
+    cat = k.concat_c(a, b2)
+    ref = k.act_fakequant(cat, "per_channel", 8, layout=k.NHWC)
+    assert torch.equal(got, ref)
+
+
+def test_fast_reciprocal_fake_quant_is_exact(dev):
+    """rcp_exact + fq_apply_r (all apply kernels) == the IEEE-division fake-quant, for every fp16
+    scale and the values next to every quantization midpoint."""
+    from qdiff import _lib
+    counts = torch.zeros(2, dtype=torch.int32, device=dev)
+    _lib.call("qd_selftest_recip", counts.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert counts.tolist() == [0, 0]
