@@ -89,11 +89,13 @@ def dominant_kernel_roofline(dev, iters=20):
     ms = e0.elapsed_time(e1) / iters
     flops = 2.0 * (n * h * w) * c * (9 * c)
     tflops = flops / (ms * 1e-3) / 1e12
+    choice = _conv_choice()
+    tr = pmc_traffic(choice["variant"] if choice else None)
     return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": (pmc_traffic() or {}).get("hbm_bytes_per_launch"),
-            "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": pmc_traffic(),
+            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": (tr or {}).get("hbm_bytes_per_launch"),
+            "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": tr,
             "kernel": "conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880) implicit GEMM",
-            "kernel_choice": _conv_choice(),
+            "kernel_choice": choice,
             "avg_us": round(ms * 1e3, 2)}
 
 
@@ -102,20 +104,29 @@ def _conv_choice():
     from qdiff import kernels as K
     for key, c in K.gemm_choices().items():
         if key[:8] == ("conv", 8, 64, 64, 320, 320, 3, 3):
-            return {"variant": c[1], "family": "k_gemm_dma" if c[1] >= 100 else "k_gemm"} if c else None
+            fam = "k_conv_halo" if c and c[1] >= 200 else "k_gemm_dma" if c and c[1] >= 100 else "k_gemm"
+            return {"variant": c[1], "family": fam} if c else None
     return None
 
 
-def pmc_traffic():
+def pmc_traffic(variant=None):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 --pmc
     measurement (profiles/*pmc_dominant.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes over
-    scripts/roof_kernel.py - the same kernel and shape as dominant_kernel_roofline())."""
+    scripts/roof_kernel.py - the same kernel and shape as dominant_kernel_roofline(), per GEMM
+    variant when the file holds several)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_dominant.json")))
     if not files:
         return None
     with open(files[-1]) as f:
         d = json.load(f)
+    if "by_variant" in d:
+        rec = d["by_variant"].get(str(variant))
+        if rec is None:
+            return None
+        return {"hbm_bytes_per_launch": rec["hbm_bytes_per_launch"], "kernel": rec["kernel_name"][:80],
+                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+                "source": os.path.relpath(files[-1], ROOT)}
     return {"hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
             "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
             "source": os.path.relpath(files[-1], ROOT)}

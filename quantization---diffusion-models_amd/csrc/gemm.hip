@@ -484,6 +484,15 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, f16* lds, unsig
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, (int)voff, 0, 0, 0);
 }
 
+// LDS stage layout of the DMA kernels: rows of BKT halves (BKT = 64: 8 chunks of 16 B,
+// 128-B rows, chunk ^= row & 7;  BKT = 32: 4 chunks, 64-B rows, chunk ^= (row >> 1) & 3) -
+// both conflict-free for the 16-row ds_read_b128 fragment reads.
+template <int BKT>
+__device__ __forceinline__ int swz_t(int row, int chunk) {
+  if constexpr (BKT == 64) return row * 64 + ((chunk ^ (row & 7)) << 3);
+  else return row * 32 + ((chunk ^ ((row >> 1) & 3)) << 3);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -492,11 +501,13 @@ __device__ __forceinline__ void wait_vm() {
 
 // thread (wave w, lane l), load slot j: wave-instruction g = j * NW + w covers rows 8g..8g+7;
 // lane l -> row 8g + (l >> 3), LDS chunk l & 7 holding K chunk (l & 7) ^ (l >> 3).
-template <int BM, int NT, int AMODE>
+template <int BM, int NT, int AMODE, int BKT>
 struct ADma {
   static constexpr int NW = NT / 64;
-  static constexpr int L = BM * 8 / NT;
-  static_assert(BM * 8 % NT == 0, "A tile rows must split evenly over the wave-instructions");
+  static constexpr int CPR = BKT / 8;    // 16-B chunks per LDS row
+  static constexpr int RPW = 64 / CPR;   // rows per wave-instruction (1 KB)
+  static constexpr int L = BM * CPR / NT;
+  static_assert(BM * CPR % NT == 0, "A tile rows must split evenly over the wave-instructions");
   __amdgpu_buffer_rsrc_t rs;
   unsigned rowoff[L];
   int pix[L], ih0[L], iw0[L];
@@ -505,10 +516,10 @@ struct ADma {
   __device__ void init(const GemmArgs& p, int m0, int kbeg, int wid) {
     rs = rsrc(p.a, p.a_bytes);
     const int lane = threadIdx.x & 63;
-    gc = ((lane & 7) ^ (lane >> 3)) * 8;
+    gc = BKT == 64 ? ((lane & 7) ^ (lane >> 3)) * 8 : ((lane & 3) ^ ((lane >> 3) & 3)) * 8;
 #pragma unroll
     for (int j = 0; j < L; ++j) {
-      const int m = m0 + (j * NW + wid) * 8 + (lane >> 3);
+      const int m = m0 + (j * NW + wid) * RPW + lane / CPR;
       const bool ok = m < p.M;
       if (AMODE == AM_LINEAR) {
         rowoff[j] = ok ? (unsigned)m * (unsigned)p.lda * 2u : OOB;
@@ -537,11 +548,11 @@ struct ADma {
     if (AMODE == AM_LINEAR) {
       const unsigned ko = k0 + gc < p.K ? (unsigned)(k0 + gc) * 2u : OOB;
 #pragma unroll
-      for (int j = 0; j < L; ++j) glds16(rs, sa + (j * NW + wid) * 8 * BK, rowoff[j] + ko);
+      for (int j = 0; j < L; ++j) glds16(rs, sa + (j * NW + wid) * RPW * BKT, rowoff[j] + ko);
     } else if (AMODE == AM_CONV) {
 #pragma unroll
-      for (int j = 0; j < L; ++j) glds16(rs, sa + (j * NW + wid) * 8 * BK, conv_off(p, j, ky, kx, ci0 + gc));
-      ci0 += BK;
+      for (int j = 0; j < L; ++j) glds16(rs, sa + (j * NW + wid) * RPW * BKT, conv_off(p, j, ky, kx, ci0 + gc));
+      ci0 += BKT;
       if (ci0 == p.Cip) {
         ci0 = 0;
         if (++kx == p.kw) {
@@ -555,19 +566,21 @@ struct ADma {
       const int kyy = kpos / p.kw, kxx = kpos - kyy * p.kw;
 #pragma unroll
       for (int j = 0; j < L; ++j)
-        glds16(rs, sa + (j * NW + wid) * 8 * BK, k < p.K ? conv_off(p, j, kyy, kxx, ci) : OOB);
+        glds16(rs, sa + (j * NW + wid) * RPW * BKT, k < p.K ? conv_off(p, j, kyy, kxx, ci) : OOB);
     }
   }
 };
 
-template <int BN, int NT>
+template <int BN, int NT, int BKT>
 struct BDma {
-  // BN / 8 row groups over NW waves; when they do not split evenly the first (BN / 8) % NW
-  // waves issue one wave-instruction more (wave-uniform guard; the per-wave count feeds vmcnt)
+  // BN / RPW row groups over NW waves; when they do not split evenly the first G % NW waves
+  // issue one wave-instruction more (wave-uniform guard; the per-wave count feeds vmcnt)
   static constexpr int NW = NT / 64;
-  static constexpr int G = BN / 8;
+  static constexpr int CPR = BKT / 8;
+  static constexpr int RPW = 64 / CPR;
+  static constexpr int G = BN / RPW;
   static constexpr int L = (G + NW - 1) / NW;
-  static_assert(BN % 8 == 0, "B tile rows in groups of 8");
+  static_assert(BN % RPW == 0, "B tile rows in whole wave-instruction groups");
   __amdgpu_buffer_rsrc_t rs;
   unsigned rowoff[L];
   int gc;
@@ -575,10 +588,10 @@ struct BDma {
   __device__ void init(const GemmArgs& p, int n0, int wid) {
     rs = rsrc(p.b, p.b_bytes);
     const int lane = threadIdx.x & 63;
-    gc = ((lane & 7) ^ (lane >> 3)) * 8;
+    gc = BKT == 64 ? ((lane & 7) ^ (lane >> 3)) * 8 : ((lane & 3) ^ ((lane >> 3) & 3)) * 8;
 #pragma unroll
     for (int j = 0; j < L; ++j) {
-      const int n = n0 + (j * NW + wid) * 8 + (lane >> 3);
+      const int n = n0 + (j * NW + wid) * RPW + lane / CPR;
       rowoff[j] = n < p.N ? (unsigned)n * (unsigned)p.K * 2u : OOB;
     }
   }
@@ -586,7 +599,7 @@ struct BDma {
     const unsigned ko = k0 + gc < p.K ? (unsigned)(k0 + gc) * 2u : OOB;
 #pragma unroll
     for (int j = 0; j < L; ++j)
-      if (G % NW == 0 || j * NW + wid < G) glds16(rs, sb + (j * NW + wid) * 8 * BK, rowoff[j] + ko);
+      if (G % NW == 0 || j * NW + wid < G) glds16(rs, sb + (j * NW + wid) * RPW * BKT, rowoff[j] + ko);
   }
 };
 
@@ -612,25 +625,28 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 //     MFMA(k, half 0) | read(k, half 1)  -> wait(tile k+1) -> barrier -> issue tile k+2 ->
 //     MFMA(k, half 1) | read(k+1, half 0)
 //   (the stage written after the barrier held tile k-1, whose last reads precede it).
-constexpr int dma_lds_halves(int bm, int bn, int st) {
-  return st * (bm + bn) * BK > bm * (bn + 8) ? st * (bm + bn) * BK : bm * (bn + 8);
+constexpr int dma_lds_halves(int bm, int bn, int st, int bkt = 64) {
+  return st * (bm + bn) * bkt > bm * (bn + 8) ? st * (bm + bn) * bkt : bm * (bn + 8);
 }
 // minimum waves per SIMD for __launch_bounds__: (blocks that fit the 160 KB LDS) x waves / 4
-constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt) {
-  return (163840 / (2 * dma_lds_halves(bm, bn, st))) * nt / 256 > 0 ? (163840 / (2 * dma_lds_halves(bm, bn, st))) * nt / 256 : 1;
+constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt, int bkt = 64) {
+  return (163840 / (2 * dma_lds_halves(bm, bn, st, bkt))) * nt / 256 > 0
+             ? (163840 / (2 * dma_lds_halves(bm, bn, st, bkt))) * nt / 256
+             : 1;
 }
 
-template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int AMODE, bool SPLIT>
-__global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN))
+template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT>
+__global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
     k_gemm_dma(GemmArgs p) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ASZ = BM * BK, SSZ = (BM + BN) * BK;
-  constexpr int LDSZ = dma_lds_halves(BM, BN, ST);
-  static_assert(PIPE == 0 || ST >= 3, "split-phase pipeline needs >= 3 stages");
-  using AL = ADma<BM, NT, AMODE>;
-  using BL = BDma<BN, NT>;
+  constexpr int ASZ = BM * BKT, SSZ = (BM + BN) * BKT;
+  constexpr int LDSZ = dma_lds_halves(BM, BN, ST, BKT);
+  constexpr int KSUB = BKT / 32;  // 32-deep MFMA slices per stage
+  static_assert(PIPE == 0 || (ST >= 3 && BKT == 64), "split-phase pipeline needs >= 3 stages of 64");
+  using AL = ADma<BM, NT, AMODE, BKT>;
+  using BL = BDma<BN, NT, BKT>;
   __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
 
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
@@ -662,27 +678,34 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int nk = (kend - kbeg + BKT - 1) / BKT;
 #pragma unroll
   for (int s = 0; s < ST - 1; ++s) {
     if (s < nk) {
-      al.issue(p, kbeg + s * BK, smem + s * SSZ, wid);
-      bl.issue(p, kbeg + s * BK, smem + s * SSZ + ASZ, wid);
+      al.issue(p, kbeg + s * BKT, smem + s * SSZ, wid);
+      bl.issue(p, kbeg + s * BKT, smem + s * SSZ + ASZ, wid);
     }
   }
   auto read_frags = [&](const f16* As, int ks, f16x8 (&af)[TM], f16x8 (&bf)[TN]) {
     const f16* Bs = As + ASZ;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz(wm0 + i * 16 + fr, ks * 4 + fq));
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BKT>(wm0 + i * 16 + fr, ks * 4 + fq));
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz(wn0 + j * 16 + fr, ks * 4 + fq));
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BKT>(wn0 + j * 16 + fr, ks * 4 + fq));
   };
   auto mfmas = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
+#ifdef QD_ABLATE_NO_MFMA  // diagnostic build: staging + fragment reads only (values kept live)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bf[j]));
+#else
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+#endif
   };
   auto sync = [&](int ahead) {  // own loads of the awaited tile landed, `ahead` later tiles in flight
     wait_vm_rt(ahead * per);
@@ -698,14 +721,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
       if (kt + ST - 1 < nk) {
         int nx = cur + ST - 1;
         if (nx >= ST) nx -= ST;
-        al.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ, wid);
-        bl.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ + ASZ, wid);
+        al.issue(p, kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ, wid);
+        bl.issue(p, kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ + ASZ, wid);
       }
-      f16x8 af[TM], bf[TN];
-      read_frags(smem + cur * SSZ, 0, af, bf);
-      mfmas(af, bf);
-      read_frags(smem + cur * SSZ, 1, af, bf);
-      mfmas(af, bf);
+#pragma unroll
+      for (int ks = 0; ks < KSUB; ++ks) {
+        f16x8 af[TM], bf[TN];
+        read_frags(smem + cur * SSZ, ks, af, bf);
+        mfmas(af, bf);
+      }
       if (++cur == ST) cur = 0;
     }
   } else {
@@ -725,8 +749,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
         if (kt + ST - 1 < nk) {
           int nx = cur + ST - 1;
           if (nx >= ST) nx -= ST;
-          al.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ, wid);
-          bl.issue(p, kbeg + (kt + ST - 1) * BK, smem + nx * SSZ + ASZ, wid);
+          al.issue(p, kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ, wid);
+          bl.issue(p, kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ + ASZ, wid);
         }
         read_frags(smem + nxt * SSZ, 0, a0, b0);
       }
@@ -738,6 +762,142 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   gemm_epilogue<BM, BN, NT, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
+}
+
+// ---- halo-reuse implicit-GEMM conv (3x3, stride 1, pad 1) ----------------------------------
+// A block owns 256 output pixels = RB = 256 / W whole image rows of one image (W in {16, 32,
+// 64}) x BN output channels.  K is walked chunk-major: for each 64-channel chunk of the input
+// the (RB + 2) x (W + 2) halo of those rows is staged in LDS ONCE (LDS-DMA, zero halo from OOB
+// offsets) and all 9 filter taps read their shifted A fragments from it; only the 9 weight
+// tiles stream per chunk.  The implicit-GEMM kernels above re-load every A row for each tap
+// (9x the activation bytes); for the SD1.5 64x64 convs this cuts the L2->LDS traffic per block
+// ~2.8x - the load pipeline, not the MFMAs, bounds those kernels (ablation: DESIGN.md).
+// Halo chunk c+1 is staged under chunk c's taps, 1/8 of its rows per tap step; weight tiles are
+// double-buffered one tap ahead.  Summation order over K differs from the tap-major kernels
+// (chunk-major), so its outputs may differ from theirs in the last fp16 bit.
+constexpr int HALO_ROWS_MAX = 400;  // (RB + 2) * (W + 2) <= 396 for W in {16, 32, 64}
+
+template <int BN>
+__global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
+  constexpr int BM = 256, NT = 512, NW = 8, WGN = 2;
+  constexpr int WM = 64, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  constexpr int HSZ = HALO_ROWS_MAX * BK;  // halves per halo buffer
+  constexpr int BSZ = BN * BK;
+  constexpr int LDSZ = 2 * HSZ + 2 * BSZ > BM * (BN + 8) ? 2 * HSZ + 2 * BSZ : BM * (BN + 8);
+  constexpr int HG = HALO_ROWS_MAX / 8;                     // halo wave-instruction groups (max)
+  constexpr int HL = (HG + NW - 1) / NW;                    // per wave
+  static_assert(HL <= 8, "halo rows must stage within the 8 tap steps of a chunk");
+  using BL = BDma<BN, NT, 64>;
+  __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
+  f16* const halo0 = smem;
+  f16* const bring = smem + 2 * HSZ;
+
+  const int W = p.W, RB = BM / W, W2 = W + 2;
+  const int hrows = (RB + 2) * W2;
+  const int nbm = p.M / BM, nbn = p.N / BN;
+  const int ntile = nbm * nbn, nwg = ntile * p.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = wg / p.splits, split = wg - tile * p.splits;
+  const int bm = tile / nbn, bn = tile - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int img = m0 / (p.Ho * p.Wo), oh0 = (m0 - img * p.Ho * p.Wo) / W;
+  const int c_beg = split * p.kps, c_end = c_beg + p.kps;  // 64-channel chunks of this split
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // halo staging: wave-instruction g covers halo rows 8g .. 8g+7 (lane -> row 8g + (lane >> 3),
+  // LDS chunk lane & 7 holding K chunk (lane & 7) ^ (lane >> 3)); slot j of this wave is g = 8j + wid
+  const __amdgpu_buffer_rsrc_t ars = rsrc(p.a, p.a_bytes);
+  const int gc = ((lane & 7) ^ (lane >> 3)) * 8;
+  unsigned hoff[HL];
+#pragma unroll
+  for (int j = 0; j < HL; ++j) {
+    const int hr = (j * NW + wid) * 8 + (lane >> 3);
+    const int hy = hr / W2, hx = hr - hy * W2;
+    const int ih = oh0 - 1 + hy, iw = hx - 1;
+    const bool ok = hr < hrows && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    const int sh = p.ups ? ih >> 1 : ih, sw = p.ups ? iw >> 1 : iw;
+    hoff[j] = ok ? (unsigned)(((img * p.Hs + sh) * p.Ws + sw) * p.Cip + gc) * 2u : OOB;
+  }
+  auto halo_issue = [&](int j, int chunk, f16* hb) {
+    if (j * NW + wid < (hrows + 7) / 8) glds16(ars, hb + (j * NW + wid) * 8 * BK, hoff[j] + (unsigned)(chunk * BK * 2));
+  };
+  auto halo_cnt = [&](int j) { return (j < HL && j * NW + wid < (hrows + 7) / 8) ? 1 : 0; };
+
+  BL bl;
+  bl.init(p, n0, wid);
+  const int bcnt = BL::count(wid);
+  // weight tile of (tap t, chunk c): K offset t * Cip + c * 64 ([Co][kh][kw][Cip] layout)
+  auto b_issue = [&](int s, f16* dst) {
+    const int c = c_beg + s / 9, t = s - (s / 9) * 9;
+    bl.issue(p, t * p.Cip + c * BK, dst, wid);
+  };
+
+  // per-lane halo row of each A fragment row (tap (0, 0)); tap (ky, kx) adds ky * W2 + kx
+  int hr0[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm0 + i * 16 + fr;
+    const int r = ml / W, x = ml - r * W;
+    hr0[i] = r * W2 + x;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (c_end - c_beg) * 9;
+  // prologue: the first chunk's whole halo, then the first weight tile
+#pragma unroll
+  for (int j = 0; j < HL; ++j) halo_issue(j, c_beg, halo0);
+  b_issue(0, bring);
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int cl = s / 9, t = s - cl * 9;
+    // own loads of weight tile s landed (halo rows issued after it in step s-1 may stay in flight)
+    wait_vm_rt(t >= 1 && cl + 1 < c_end - c_beg ? halo_cnt(t - 1) : 0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 1 < nsteps) b_issue(s + 1, bring + ((s + 1) & 1) * BSZ);
+    if (t < 8 && cl + 1 < c_end - c_beg) halo_issue(t, c_beg + cl + 1, halo0 + ((cl + 1) & 1) * HSZ);
+    const f16* hb = halo0 + (cl & 1) * HSZ;
+    const f16* Bs = bring + (s & 1) * BSZ;
+    const int ky = t / 3, kx = t - ky * 3;
+    const int tap = ky * W2 + kx;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(hb + swz(hr0[i] + tap, ks * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz(wn0 + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true>(p, acc, smem, m0, n0, wm0, wn0, split);
+  else gemm_epilogue<BM, BN, NT, TM, TN, false>(p, acc, smem, m0, n0, wm0, wn0, split);
+}
+
+// halo kernel applicability: 3x3 / stride 1 / pad 1, 64-channel chunks, whole-row 256-pixel tiles
+static bool halo_ok(const GemmArgs& p, int bn) {
+  return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && p.Cip % 64 == 0 && p.N % bn == 0 &&
+         (p.W == 16 || p.W == 32 || p.W == 64) && p.Ho == p.H && p.Wo == p.W && p.H % (256 / p.W) == 0 &&
+         (p.rows_per_sample % 64 == 0);
 }
 
 // split-K reduction + epilogue: block = 64 rows x 256 columns (64 column quads x 4 row groups
@@ -799,6 +959,7 @@ struct Plan {
 struct DmaVar {
   int bm, bn, wgm, wgn, st, pipe;
   double eff;
+  int bkt = 64;
 };
 static constexpr DmaVar kDmaC[] = {
     {128, 160, 2, 2, 2, 0, 1.00},  // 0: 2 blocks / CU
@@ -811,11 +972,17 @@ static constexpr DmaVar kDmaC[] = {
     {256, 128, 4, 2, 3, 1, 1.00},  // 7: split-phase
     {128, 160, 2, 2, 3, 1, 1.00},  // 8: split-phase, 1 block / CU
     {256, 160, 4, 2, 3, 0, 1.00},  // 9
+    {128, 160, 2, 2, 4, 0, 1.00, 32},  // 10: BK 32, 4 stages (3 in flight), 2 blocks / CU
+    {128, 128, 2, 2, 4, 0, 1.00, 32},  // 11: BK 32, 4 stages, 2 blocks / CU
+    {128, 320, 2, 4, 4, 0, 1.00, 32},  // 12: BK 32, 4 stages, 1 block / CU
+    {256, 256, 2, 4, 4, 0, 1.00, 32},  // 13: BK 32, 4 stages, 1 block / CU
 };
 static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
 
 extern "C" int qd_gemm_force(int variant) {
-  QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) || (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))),
+  QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
+                 (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
+                 variant == 201,
              "qd_gemm_force: -1, 0..3 or 100 + DMA variant");
   g_force = variant;
   return 0;
@@ -851,14 +1018,28 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       }
     }
   }
-  if (g_force >= 100 && !quant_w) {
+  if ((g_force == 200 || g_force == 201) && !quant_w && !geglu && K % 576 == 0) {
+    // halo conv (applicability is checked at launch; the split only needs the chunk count)
+    const int bn = g_force == 200 ? 160 : 128;
+    if (N % bn == 0 && M % 256 == 0) {
+      const long tiles_mn = (long)(M / 256) * (N / bn);
+      const int nc = K / 576;
+      best = {2, 256, bn, 0, 1, nc};
+      for (int sp = 2; sp <= nc; ++sp) {
+        if (nc % sp != 0) continue;
+        if (tiles_mn * sp > 256) break;
+        best.splits = sp;
+        best.kps = nc / sp;
+      }
+    }
+  } else if (g_force >= 100 && g_force < 200 && !quant_w) {
     const DmaVar& d = kDmaC[g_force - 100];
     const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
     if (ok) {
       best = {1, d.bm, d.bn, g_force - 100, 1, K};
       // split K (whole 64-deep steps, >= 8 per split) while the blocks fit one resident round
       const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
-      const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st)), by_waves = 2048 / (64 * d.wgm * d.wgn);
+      const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
       const int per_cu = std::max(1, std::min(by_lds, by_waves));
       for (int sp = 2; sp <= 32 && !geglu && K % 64 == 0; ++sp) {
         if ((K / 64) % sp != 0 || K / sp < 512) continue;
@@ -885,7 +1066,7 @@ template <int V, int AMODE, bool SPLIT>
 static void launch_dma_v(const GemmArgs& p, hipStream_t st) {
   constexpr DmaVar d = kDmaC[V];
   const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
-  k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, AMODE, SPLIT><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+  k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
 }
 
 template <int AMODE, bool SPLIT>
@@ -900,13 +1081,21 @@ static void launch_dma(const GemmArgs& p, int var, hipStream_t st) {
     case 6: launch_dma_v<6, AMODE, SPLIT>(p, st); break;
     case 7: launch_dma_v<7, AMODE, SPLIT>(p, st); break;
     case 8: launch_dma_v<8, AMODE, SPLIT>(p, st); break;
-    default: launch_dma_v<9, AMODE, SPLIT>(p, st); break;
+    case 9: launch_dma_v<9, AMODE, SPLIT>(p, st); break;
+    case 10: launch_dma_v<10, AMODE, SPLIT>(p, st); break;
+    case 11: launch_dma_v<11, AMODE, SPLIT>(p, st); break;
+    case 12: launch_dma_v<12, AMODE, SPLIT>(p, st); break;
+    default: launch_dma_v<13, AMODE, SPLIT>(p, st); break;
   }
 }
 
 template <int AMODE, bool SPLIT>
 static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t st) {
-  if (pl.kind == 1) launch_dma<AMODE, SPLIT>(p, pl.var, st);
+  if (pl.kind == 2) {
+    const int nwg = (p.M / 256) * (p.N / pl.bn) * p.splits;
+    if (pl.bn == 160) k_conv_halo<160><<<nwg, 512, 0, st>>>(p);
+    else k_conv_halo<128><<<nwg, 512, 0, st>>>(p);
+  } else if (pl.kind == 1) launch_dma<AMODE, SPLIT>(p, pl.var, st);
   else if (pl.bm == 128 && pl.bn == 160) launch_fmt<128, 160, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128 && pl.bn == 128) launch_fmt<128, 128, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128) launch_fmt<128, 64, AMODE, SPLIT>(p, fmt, st);
@@ -919,7 +1108,18 @@ template <int AMODE>
 static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t st) {
   Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
                       (p.epi & QD_EPI_GEGLU) != 0);
-  if (AMODE == AM_CONV_ANY || !ws || ws_elems < split_ws_elems(pl, p.M, p.N)) {
+  if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn))) {  // halo conv not applicable
+    const int f = g_force;
+    g_force = -1;
+    pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
+                   (p.epi & QD_EPI_GEGLU) != 0);
+    g_force = f;
+  }
+  if (pl.kind == 2 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N)) && pl.splits > 1) {
+    pl.splits = 1;  // halo split is over 64-channel chunks
+    pl.kps = p.K / 576;
+  }
+  if (pl.kind != 2 && (AMODE == AM_CONV_ANY || !ws || ws_elems < split_ws_elems(pl, p.M, p.N))) {
     if (pl.splits > 1) {  // no room for slabs: best unsplit plan
       pl.splits = 1;
       pl.kps = p.K;

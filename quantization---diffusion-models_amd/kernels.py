@@ -162,8 +162,16 @@ def conv_weight_khwc(w, ci_pad):
 # QD_GEMM_TUNE=0 disables the search (library planner only).
 REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
 DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109)  # LDS-DMA variants (fp16 weights)
+HALO_VARIANTS = (200, 201)  # 3x3 conv with the activation halo staged once per channel chunk
 _TUNE = {}
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
+_OVERRIDE = None  # benchmarking: force every GEMM onto one qd_gemm_force id (see force_gemm)
+
+
+def force_gemm(variant=None):
+    """Benchmark hook: run every following GEMM with qd_gemm_force(variant) (None: tuned)."""
+    global _OVERRIDE
+    _OVERRIDE = variant
 
 
 def gemm_choices():
@@ -240,7 +248,7 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
 
     def launch(c, y, am, ep, scratch):
         w, fmt, sc, gr = ops[c[0]]
-        _force(c[1])
+        _force(c[1] if _OVERRIDE is None else _OVERRIDE)
         try:
             if scratch:
                 n = _lib.load().qd_gemm_workspace(M, N, K, WFMT[fmt], rows_per_sample, ep)
@@ -299,7 +307,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     M, Kd = n * ho * wo, kh * kw * cip
 
     def launch(c, y, am, ep, scratch):
-        _force(c[1])
+        _force(c[1] if _OVERRIDE is None else _OVERRIDE)
         try:
             if cip % 64:
                 ws, wsn = None, 0
@@ -318,7 +326,10 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        c = _choose(key, _cands([(w_khwc, "f16", None, 0)]), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+        cands = _cands([(w_khwc, "f16", None, 0)])
+        if kh == 3 and kw == 3 and stride == 1 and pad == 1 and cip % 64 == 0:
+            cands += [(0, v) for v in HALO_VARIANTS]
+        c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
     launch(c if c is not None else (0, -1), out, amax, epi, False)

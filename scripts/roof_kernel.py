@@ -11,10 +11,10 @@ import torch  # noqa: E402
 import qdiff_boot  # noqa: E402,F401
 from qdiff import kernels as K  # noqa: E402
 
+if len(sys.argv) > 2:  # GEMM kernel family / tile override (qd_gemm_force id), for A/B profiles
+    K.force_gemm(int(sys.argv[2]))
+
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-if len(sys.argv) > 2:  # GEMM kernel family / tile override (qd_gemm_force), for A/B profiles
-    from qdiff import _lib
-    _lib.call("qd_gemm_force", int(sys.argv[2]))
 dev = torch.device("cuda:0")
 n, h, w, c = 8, 64, 64, 320
 g = torch.Generator(device="cpu").manual_seed(0)

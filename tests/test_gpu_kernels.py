@@ -373,7 +373,7 @@ def forced_gemm():
     _lib.call("qd_gemm_force", -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 110)))
+@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 114)) + [200, 201])
 def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     """Every kernel family / tile (register-staged and LDS-DMA) on ragged shapes: rows past M,
     conv halo, stride 2, fused 2x upsample, the 4-channel conv_in (any-Ci decode), K tails,
@@ -469,3 +469,35 @@ def test_fast_reciprocal_fake_quant_is_exact(dev):
     counts = torch.zeros(2, dtype=torch.int32, device=dev)
     _lib.call("qd_selftest_recip", counts.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert counts.tolist() == [0, 0]
+
+
+@pytest.mark.parametrize("variant", [200, 201])
+def test_conv_halo_kernel(variant, forced_gemm, dev):
+    """Halo-staged 3x3 conv: 16/32/64-wide images, fused 2x upsample, split-K over channel
+    chunks (ragged 64-channel chunk counts), bias + amax + residual epilogues."""
+    k = K()
+    forced_gemm(variant)
+    g = torch.Generator().manual_seed(variant)
+    for cin, cout, hw, ups, n, res in ((128, 320, 16, False, 2, True), (320, 640, 32, False, 2, False),
+                                       (192, 160, 64, False, 1, True), (64, 128, 16, True, 2, False),
+                                       (1280, 1280, 16, False, 2, False)):
+        x = torch.randn(n, cin, hw, hw, generator=g).half()
+        w = (torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5).half()
+        b = torch.randn(cout, generator=g).half()
+        xh = k.nchw_to_nhwc(x.to(dev), cin)
+        wk = k.conv_weight_khwc(w.to(dev), cin)
+        H = 2 * hw if ups else hw
+        r = torch.randn(n, H, H, cout, generator=g).half().to(dev) if res else None
+        amax = torch.empty(n * cout, dtype=torch.float32, device=dev)
+        y = k.conv2d_nhwc(xh, wk, cin, 1, 1, ups, bias=b.to(dev), residual=r, amax=amax)
+        xin = F.interpolate(x.float(), scale_factor=2.0, mode="nearest") if ups else x.float()
+        pre = F.conv2d(xin, w.float(), b.float(), 1, 1).half().float()
+        got = k.nhwc_to_nchw(y).cpu().float()
+        if res:
+            ref = (pre + k.nhwc_to_nchw(r).cpu().float()).half().float()
+            tol = ulp16(pre) + ulp16(ref) + 1e-3
+            assert ((got - ref).abs() <= tol).all(), (variant, cin, cout, hw)
+        else:
+            assert_fp16_close(got, pre, ulps=2.0, atol=1e-3)
+        # amax is of the pre-residual output (the conv output the reference fake-quantizes)
+        assert torch.allclose(amax.view(n, cout).cpu(), pre.abs().amax(dim=(2, 3)), rtol=2e-3, atol=1e-3)
