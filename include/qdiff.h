@@ -218,6 +218,44 @@ int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const int* fc_rows
  * reciprocal errors > 1 ulp, counts[1] = differing fake-quant results (device int[2]). */
 int qd_selftest_recip(int* counts, void* stream);
 
+/* ---------------- SD3 / SD3.5 MMDiT -------------------------------------------------------
+ * The diffusers SD3Transformer2DModel ops the reference runs around its WxAxLinear layers
+ * (models/StableDiffusion3_5.py:37-45 hands the transformer to the quantizer swap,
+ * quantize/quantizer.py:491-533; the model itself is third-party diffusers code).  fp16 in/out,
+ * each torch op computed in fp32 and rounded to fp16 once. */
+/* AdaLayerNormZero / AdaLayerNormContinuous apply (LayerNorm without affine, eps):
+ * y = half(half(half(LN(x)) * half(1 + scale[b])) + shift[b]), x / y [rows, c],
+ * b = row / tokens_per_sample; shift / scale [B, mod_ld] (column slices of the adaLN linear). */
+int qd_adaln_modulate(const void* x, long rows, int c, int tokens_per_sample, float eps, const void* shift,
+                      const void* scale, int mod_ld, void* y, void* stream);
+/* JointTransformerBlock gated residual: out = half(x + half(gate[b] * y)); y row stride y_ld,
+ * gate [B, gate_ld], b = row / tokens_per_sample.  out may alias x. */
+int qd_gated_residual(const void* x, const void* y, int y_ld, const void* gate, int gate_ld, long rows, int c,
+                      int tokens_per_sample, void* out, void* stream);
+/* diffusers RMSNorm(head_dim) (Attention.norm_q / norm_k / norm_added_q / norm_added_k), in place
+ * over each d-wide head of `rows` rows: half(half(x * rsqrt(mean(x^2) + eps)) * w).  Row r lives
+ * at x + ((r / rows_per_group) * group_stride + r % rows_per_group) * ld (rows_per_group <= 0:
+ * contiguous rows).  d in {16, 32, 64, 128}. */
+int qd_rmsnorm_heads(void* x, long rows, int heads, int d, int ld, long rows_per_group, long group_stride,
+                     const void* weight, float eps, void* stream);
+/* F.gelu(x, approximate="tanh") (FeedForward activation_fn="gelu-approximate"); n % 8 == 0. */
+int qd_gelu_tanh(const void* x, void* y, int64_t n, void* stream);
+/* PatchEmbed position add: out[b, s, :] = half(x[b, s, :] + pos[s, :]), pos [s, c] (cropped). */
+int qd_add_pos(const void* x, const void* pos, int b, long s, int c, void* out, void* stream);
+/* Grouped strided row copy: dst row ((r / rows_per_group) * group_stride + r % rows_per_group)
+ * (stride dst_ld) = src row r (stride src_ld), `cols` halves; builds the joint [x; context]
+ * q|k|v sequence of JointAttnProcessor2_0 (torch.cat along the sequence). */
+int qd_copy_rows(const void* src, int src_ld, void* dst, int dst_ld, long rows, int cols, long rows_per_group,
+                 long group_stride, void* stream);
+/* SD3Transformer2DModel unpatchify: tokens [B, h*w, p*p*c] -> NHWC [B, h*p, w*p, c]. */
+int qd_unpatchify(const void* tokens, int b, int h, int w, int p, int c, void* out, void* stream);
+/* CFG + FlowMatchEulerDiscreteScheduler.step on fp16 latents [B, L]: v = u + g*(c - u) from the
+ * model output [2B, L] (uncond first), x += (sigma[i+1] - sigma[i]) * v with sample.to(float32)
+ * semantics; sigmas fp32 [steps + 1]; i read from and then incremented in `step_idx`.  Also
+ * writes the next model input [2B, L] (latents duplicated) when next_in != NULL. */
+int qd_cfg_euler_step(void* latents, const void* model_out, int b, int64_t l, float guidance, const float* sigmas,
+                      int* step_idx, void* next_in, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

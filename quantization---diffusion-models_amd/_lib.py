@@ -48,6 +48,14 @@ SIGNATURES = {
     "qd_smooth_fold": [P, P, P, P, I, I, P, F, P, P, P],
     "qd_gemm_force": [I],
     "qd_selftest_recip": [P, P],
+    "qd_adaln_modulate": [P, I64, I, I, F, P, P, I, P, P],
+    "qd_gated_residual": [P, P, I, P, I, I64, I, I, P, P],
+    "qd_rmsnorm_heads": [P, I64, I, I, I, I64, I64, P, F, P],
+    "qd_gelu_tanh": [P, P, I64, P],
+    "qd_add_pos": [P, P, I, I64, I, P, P],
+    "qd_copy_rows": [P, I, P, I, I64, I, I64, I64, P],
+    "qd_unpatchify": [P, I, I, I, I, I, P, P],
+    "qd_cfg_euler_step": [P, P, I, I64, F, P, P, P, P],
 }
 
 # size queries (no status code)

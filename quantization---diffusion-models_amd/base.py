@@ -180,13 +180,13 @@ class BaseAWQForDiffusion(nn.Module):
         with open(os.path.join(save_dir, "qdiff_quant.json"), "w") as f:
             json.dump(self.quant_config.full_dict(), f, indent=2)
         codes = {}
-        for name, m in self.pipeline.unet.named_modules():
+        for name, m in self.pipeline.denoiser.named_modules():
             if isinstance(m, WxAxLinear) and m.qcodes is not None:
                 codes[f"{name}.qcodes"] = m.qcodes.detach().cpu().contiguous()
                 codes[f"{name}.qscales"] = m.qscales.detach().cpu().contiguous()
                 codes[f"{name}.qmeta"] = torch.tensor([m.qgroup, m.n_bits_W], dtype=torch.int32)
         if codes:
-            save_file(codes, os.path.join(save_dir, "unet", "qdiff_codes.safetensors"))
+            save_file(codes, os.path.join(save_dir, self.pipeline.denoiser_name, "qdiff_codes.safetensors"))
 
     def _load_quantized_modules(self, module, bitWidth=4, group_size=128, act_bits=16, full_config=None):
         return load_quantized_modules(module, bitWidth, group_size, act_bits, full_config)
@@ -198,12 +198,19 @@ class BaseAWQForDiffusion(nn.Module):
                        offload_folder=None, download_kwargs=None, device="cuda"):
         """base.py:736-826 (usable on an instance, as in the reference, or on the class)."""
         from safetensors.torch import load_file
+        from .mmdit import MMDiTConfig, SD3Transformer2DModel
         from .unet import UNet2DConditionModel, UNetConfig
         with open(os.path.join(model_path, "quant_components.json")) as f:
             comps = json.load(f)
-        with open(os.path.join(model_path, "unet", "config.json")) as f:
+        with open(os.path.join(model_path, "model_index.json")) as f:
+            cls_name = json.load(f)["_class_name"]
+        sub = "transformer" if "transformer" in comps else "unet"
+        with open(os.path.join(model_path, sub, "config.json")) as f:
             ucfg_d = json.load(f)
-        unet = UNet2DConditionModel(UNetConfig.from_diffusers(ucfg_d)).half().to(device)
+        if sub == "transformer":
+            net = SD3Transformer2DModel(MMDiTConfig.from_diffusers(ucfg_d)).half().to(device)
+        else:
+            net = UNet2DConditionModel(UNetConfig.from_diffusers(ucfg_d)).half().to(device)
         qc = ucfg_d["quantization_config"]
         full = None
         fpath = os.path.join(model_path, "qdiff_quant.json")
@@ -211,23 +218,24 @@ class BaseAWQForDiffusion(nn.Module):
             with open(fpath) as f:
                 full = json.load(f)
         qcfg = AwqConfig(**full) if full else AwqConfig(**AwqConfig.from_transformers_dict(AwqConfig, qc))
-        load_quantized_modules(unet, bitWidth=qc["bits"], group_size=qc["group_size"], act_bits=qc["act_bits"],
+        load_quantized_modules(net, bitWidth=qc["bits"], group_size=qc["group_size"], act_bits=qc["act_bits"],
                                full_config=full)
-        sd = load_file(os.path.join(model_path, "unet", "diffusion_pytorch_model.safetensors"))
-        unet.load_state_dict({k: v.to(device) for k, v in sd.items()}, strict=True)
-        cpath = os.path.join(model_path, "unet", "qdiff_codes.safetensors")
+        sd = load_file(os.path.join(model_path, sub, "diffusion_pytorch_model.safetensors"))
+        net.load_state_dict({k: v.to(device) for k, v in sd.items()}, strict=True)
+        cpath = os.path.join(model_path, sub, "qdiff_codes.safetensors")
         if os.path.exists(cpath):
             codes = load_file(cpath)
-            for name, m in unet.named_modules():
+            for name, m in net.named_modules():
                 if isinstance(m, WxAxLinear) and f"{name}.qcodes" in codes:
                     g, nb = codes[f"{name}.qmeta"].tolist()
                     m.qcodes = codes[f"{name}.qcodes"].to(device)
                     m.qscales = codes[f"{name}.qscales"].to(device)
                     m.qgroup, m.n_bits_W = g, nb
                     m.qfmt = "i4" if nb <= 4 else "i8"
-        with open(os.path.join(model_path, "model_index.json")) as f:
-            cls_name = json.load(f)["_class_name"]
-        pipe = QDiffPipeline(unet, cls_name, config={"_class_name": cls_name})
+        if sub == "transformer":
+            pipe = QDiffPipeline(transformer=net, class_name=cls_name, config={"_class_name": cls_name})
+        else:
+            pipe = QDiffPipeline(net, cls_name, config={"_class_name": cls_name})
         if isinstance(self_or_cls, type):
             obj = self_or_cls(pipe, cls_name, is_quantized=True, config={"_class_name": cls_name}, quant_config=qcfg)
         else:

@@ -484,6 +484,107 @@ def cfg_ddim_step(latents, unet_out, guidance, alpha_t, alpha_prev, step_idx, ne
     return latents
 
 
+# ---------------------------------------------------------------- SD3 / SD3.5 MMDiT ops
+def _rows_view(t, name):
+    """(rows, cols, row stride) of a 2-D fp16 HIP view with unit column stride."""
+    if t.dtype != torch.float16 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be a 2-D fp16 HIP tensor with unit column stride")
+    return t.shape[0], t.shape[1], t.stride(0)
+
+
+def adaln(x, tokens_per_sample, shift, scale, eps=1e-6, out=None):
+    """AdaLayerNormZero / AdaLayerNormContinuous apply on x [rows, C]:
+    half(half(half(LN(x)) * half(1 + scale[b])) + shift[b]), b = row // tokens_per_sample;
+    shift / scale [B, C] column slices (same row stride) of the adaLN projection output."""
+    _chk(x, "x")
+    c = x.shape[-1]
+    rows = x.numel() // c
+    _, cs, ld = _rows_view(shift, "shift")
+    _, cc, ld2 = _rows_view(scale, "scale")
+    if cs != c or cc != c or ld != ld2:
+        raise ValueError("shift / scale must be [B, C] slices with one row stride")
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
+    _lib.call("qd_adaln_modulate", _p(x), rows, c, tokens_per_sample, float(eps), _p(shift), _p(scale), ld, _p(o),
+              _stream())
+    return o
+
+
+def gated_residual(x, y, gate, tokens_per_sample, out=None):
+    """half(x + half(gate[b] * y)) on [rows, C]; y may be row-strided, gate a [B, C] slice."""
+    _chk(x, "x")
+    c = x.shape[-1]
+    rows = x.numel() // c
+    yr, yc, yld = _rows_view(y, "y")
+    _, gc, gld = _rows_view(gate, "gate")
+    if yr != rows or yc != c or gc != c:
+        raise ValueError("gated_residual shape mismatch")
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
+    _lib.call("qd_gated_residual", _p(x), _p(y), yld, _p(gate), gld, rows, c, tokens_per_sample, _p(o), _stream())
+    return o
+
+
+def rmsnorm_heads(x, rows, heads, d, ld, weight, eps=1e-6, rows_per_group=0, group_stride=0):
+    """In-place RMSNorm(head_dim) of `rows` rows starting at x's first element (row stride ld)."""
+    if x.dtype != torch.float16 or not x.is_cuda:
+        raise ValueError("x must be an fp16 HIP tensor")
+    _chk(weight, "weight")
+    _lib.call("qd_rmsnorm_heads", _p(x), rows, heads, d, ld, rows_per_group, group_stride, _p(weight), float(eps),
+              _stream())
+    return x
+
+
+def gelu_tanh(x, out=None):
+    _chk(x, "x")
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
+    _lib.call("qd_gelu_tanh", _p(x), _p(o), x.numel(), _stream())
+    return o
+
+
+def add_pos(x, pos, out=None):
+    """x [B, S, C] (or NHWC [B, h, w, C]) + pos [S, C] broadcast over B."""
+    _chk(x, "x")
+    _chk(pos, "pos")
+    b, c = x.shape[0], x.shape[-1]
+    s = x.numel() // (b * c)
+    if pos.numel() != s * c:
+        raise ValueError(f"pos must hold {s} x {c} values")
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
+    _lib.call("qd_add_pos", _p(x), _p(pos), b, s, c, _p(o), _stream())
+    return o
+
+
+def copy_rows(src, dst, rows_per_group=0, group_stride=0):
+    """Row r of src (2-D view) -> dst row (r // rpg) * group_stride + r % rpg (dst: a view whose
+    first element is row 0's destination, row stride dst.stride(0))."""
+    rows, cols, sld = _rows_view(src, "src")
+    if dst.dtype != torch.float16 or not dst.is_cuda or dst.stride(-1) != 1:
+        raise ValueError("dst must be an fp16 HIP tensor with unit last stride")
+    dld = dst.stride(-2) if dst.dim() >= 2 else cols
+    _lib.call("qd_copy_rows", _p(src), sld, _p(dst), dld, rows, cols, rows_per_group, group_stride, _stream())
+    return dst
+
+
+def unpatchify(tokens, b, h, w, p, c, out=None):
+    """[B*h*w, p*p*c] tokens -> NHWC [B, h*p, w*p, c] (diffusers SD3 unpatchify)."""
+    _chk(tokens, "tokens")
+    o = out if out is not None else _empty((b, h * p, w * p, c), torch.float16, tokens.device)
+    _lib.call("qd_unpatchify", _p(tokens), b, h, w, p, c, _p(o), _stream())
+    return o
+
+
+def cfg_euler_step(latents, model_out, guidance, sigmas, step_idx, next_in=None):
+    """CFG + FlowMatchEulerDiscreteScheduler.step; latents [B, ...] updated in place."""
+    _chk(latents, "latents")
+    _chk(model_out, "model_out")
+    b = latents.shape[0]
+    l = latents.numel() // b
+    if model_out.numel() != 2 * b * l:
+        raise ValueError("model output must be [2B, ...] of the latents' shape")
+    _lib.call("qd_cfg_euler_step", _p(latents), _p(model_out), b, l, float(guidance), _p(sigmas), _p(step_idx),
+              _p(next_in), _stream())
+    return latents
+
+
 def channel_absmax_accum(x2d, ws, sum_buf=None, amax_out=None):
     _chk(x2d, "x")
     rows, c = x2d.shape

@@ -15,7 +15,7 @@ import torch
 
 from .base import QUANTISABLE_COMPONENTS, BaseAWQForDiffusion
 from .calib import synthetic_calibration_set
-from .pipeline import synthetic_text_embeddings
+from .pipeline import FlowMatchDenoiseLoop, synthetic_text_embeddings
 from .pipeline_io import load_config
 from .unet import BasicTransformerBlock
 
@@ -143,8 +143,9 @@ class StableDiffusionXL(_DiffusionAdapter):
 
 
 class StableDiffusion3_5(_DiffusionAdapter):
-    """SD3.5 MMDiT adapter surface (StableDiffusion3_5.py).  The MMDiT transformer itself is not
-    built in this round (DESIGN.md 'next')."""
+    """SD3 / SD3.5 MMDiT adapter (models/StableDiffusion3_5.py): the transformer component is
+    quantized with quantTransformer=True (quantizer.py:1063-1064) and generate() drives the
+    flow-match denoising loop of diffusers' StableDiffusion3Pipeline on device."""
     has_unet = False
     has_transformer = True
 
@@ -160,6 +161,80 @@ class StableDiffusion3_5(_DiffusionAdapter):
 
     def get_transformer(self):
         return self.pipeline.transformer
+
+    def get_unet(self):
+        raise Exception("NO UNET IN THIS MODEL")
+
+    def get_smoothing_blocks(self):
+        raise NotImplementedError("SmoothQuant (quantType='sq') has no SD3.5 block mapping in the reference "
+                                  "(StableDiffusion3_5.py defines no get_layers_for_scaling_unet)")
+
+    def _text_context(self, prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
+                      pooled_prompt_embeds=None, negative_pooled_prompt_embeds=None, seq_len=333):
+        """[neg; pos] T5+CLIP sequence embeddings [2B, Sc, joint_attention_dim] and pooled CLIP
+        embeddings [2B, pooled_projection_dim] (synthetic stand-ins for the three text encoders)."""
+        cfg = self.pipeline.transformer.config
+        dev = self.pipeline.device
+        if prompt_embeds is None:
+            prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+            prompt_embeds = synthetic_text_embeddings(prompts, seq_len=seq_len, dim=cfg.joint_attention_dim,
+                                                      device=dev)
+        else:
+            prompts = None
+        b = prompt_embeds.shape[0]
+        if pooled_prompt_embeds is None:
+            names = [f"{p}\x00pooled" for p in prompts] if prompts else [f"pooled{i}" for i in range(b)]
+            pooled_prompt_embeds = synthetic_text_embeddings(names, seq_len=1, dim=cfg.pooled_projection_dim,
+                                                             device=dev)[:, 0]
+        neg = negative_prompt if negative_prompt is not None else ""
+        negs = [neg] * b if isinstance(neg, str) else list(neg)
+        if negative_prompt_embeds is None:
+            negative_prompt_embeds = synthetic_text_embeddings(negs, seq_len=prompt_embeds.shape[1],
+                                                               dim=cfg.joint_attention_dim, device=dev)
+        if negative_pooled_prompt_embeds is None:
+            negative_pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in negs], seq_len=1,
+                                                                      dim=cfg.pooled_projection_dim, device=dev)[:, 0]
+        ctx = torch.cat([negative_prompt_embeds.to(dev), prompt_embeds.to(dev)]).to(torch.float16).contiguous()
+        pooled = torch.cat([negative_pooled_prompt_embeds.to(dev), pooled_prompt_embeds.to(dev)])
+        return ctx, pooled.to(torch.float16).contiguous()
+
+    def get_loop(self, batch, height, width, steps, guidance, use_graph=True, ctx_len=333):
+        key = (batch, height, width, steps, float(guidance), use_graph, ctx_len)
+        if key not in self._loops:
+            self._loops[key] = FlowMatchDenoiseLoop(self.pipeline.transformer, batch, height, width, steps, guidance,
+                                                    device=self.pipeline.device, use_graph=use_graph,
+                                                    sched_cfg=self.pipeline.scheduler_config, ctx_len=ctx_len)
+        return self._loops[key]
+
+    @torch.no_grad()
+    def generate(self, prompt=None, height=1024, width=1024, num_inference_steps=50, guidance_scale=7.0,
+                 negative_prompt=None, num_images_per_prompt=1, generator=None, device="cpu", lat=None,
+                 output_type=None, prompt_embeds=None, negative_prompt_embeds=None, pooled_prompt_embeds=None,
+                 negative_pooled_prompt_embeds=None, use_graph=True, **kwargs):
+        """base.py:828-850 for StableDiffusion3Pipeline (its default guidance 7.0; the reference
+        passes 50 steps) -> the device flow-match loop; returns latents [B, 16, h, w] fp16."""
+        if self.pipeline is None:
+            raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
+        if output_type not in (None, "latent"):
+            raise NotImplementedError("VAE decoding is not part of this build (SURVEY.md §8f); use output_type='latent'")
+        ctx, pooled = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
+                                         pooled_prompt_embeds, negative_pooled_prompt_embeds)
+        if num_images_per_prompt > 1:
+            b0 = ctx.shape[0] // 2
+            r = num_images_per_prompt
+            ctx = torch.cat([ctx[:b0].repeat_interleave(r, 0), ctx[b0:].repeat_interleave(r, 0)])
+            pooled = torch.cat([pooled[:b0].repeat_interleave(r, 0), pooled[b0:].repeat_interleave(r, 0)])
+        b = ctx.shape[0] // 2
+        cin = self.pipeline.transformer.config.in_channels
+        shape = (b, cin, height // 8, width // 8)
+        if lat is None:
+            lat = torch.randn(shape, generator=generator, dtype=torch.float32).to(torch.float16)
+        loop = self.get_loop(b, height, width, num_inference_steps, guidance_scale, use_graph, ctx.shape[1])
+        return loop.run(lat.to(self.pipeline.device), ctx, pooled)
+
+    @torch.no_grad()
+    def run_sq_calibration(self, *a, **k):
+        raise NotImplementedError("SmoothQuant calibration is UNet-only in the reference")
 
 
 CLASS_MAP = {
@@ -177,8 +252,6 @@ class AWQ:
         cls_name = load_config(model_path)["_class_name"]
         if cls_name not in CLASS_MAP:
             raise NotImplementedError(f"{cls_name} is not supported")
-        if cls_name == "StableDiffusion3Pipeline":
-            raise NotImplementedError("the SD3.5 MMDiT transformer is not part of this build yet (DESIGN.md)")
         return CLASS_MAP[cls_name].from_pretrained(model_path, model_type, **kwargs)
 
     @staticmethod

@@ -15,7 +15,7 @@ import torch
 
 from . import arena as A
 from . import kernels as K
-from .scheduler import DDIMConfig, ddim_tables
+from .scheduler import DDIMConfig, FlowMatchConfig, ddim_tables, flowmatch_tables
 
 C_PAD = 8
 
@@ -132,3 +132,88 @@ class DenoiseLoop:
 
     def latents_nchw(self):
         return K.nhwc_to_nchw(self.lat, self.cin)
+
+
+class FlowMatchDenoiseLoop(DenoiseLoop):
+    """The SD3 / SD3.5 loop (diffusers StableDiffusion3Pipeline.__call__): for t in timesteps:
+    transformer(cat([latents]*2), t, prompt_embeds, pooled) -> CFG -> FlowMatchEuler step, with
+    the same device-resident, one-graph-per-step structure as DenoiseLoop.  Latents are NHWC
+    with the transformer's 16 channels (no padding); context_embedder / text_embedder outputs
+    are computed once per generate (step-invariant)."""
+
+    def __init__(self, transformer, batch, height=1024, width=1024, num_inference_steps=28, guidance_scale=7.0,
+                 device="cuda", use_graph=True, sched_cfg=FlowMatchConfig(), ctx_len=333):
+        self.unet = transformer
+        self.B = batch
+        self.h, self.w = height // 8, width // 8
+        self.steps = num_inference_steps
+        self.guidance = float(guidance_scale)
+        self.device = torch.device(device)
+        self.use_graph = use_graph
+        cfg = transformer.config
+        self.cin = cfg.in_channels
+        if self.cin % 8 or cfg.out_channels != self.cin:
+            raise ValueError("the flow-match loop needs in_channels == out_channels, a multiple of 8")
+        ts, sig = flowmatch_tables(num_inference_steps, sched_cfg)
+        self.timesteps = ts
+        self.ts_f32 = ts.to(self.device)
+        self.sigmas = sig.to(self.device)
+        f16 = dict(dtype=torch.float16, device=self.device)
+        self.lat = torch.zeros(batch, self.h, self.w, self.cin, **f16)
+        self.next_in = torch.zeros(2 * batch, self.h, self.w, self.cin, **f16)
+        self.temb_in = torch.zeros(2 * batch, 256, **f16)
+        self.step_idx = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.ctx = torch.zeros(2 * batch, ctx_len, cfg.joint_attention_dim, **f16)
+        self.pooled = torch.zeros(2 * batch, cfg.pooled_projection_dim, **f16)
+        self.ctx_kv = None
+        self.graph = None
+        self.last_out = None
+        self.arena = A.Arena()
+
+    @torch.no_grad()
+    def set_inputs(self, latents, ctx, pooled=None):
+        """latents [B, 16, h, w] fp16 NCHW; ctx [2B, Sc, 4096], pooled [2B, 2048] (uncond first)."""
+        if latents.shape != (self.B, self.cin, self.h, self.w):
+            raise ValueError(f"latents must be {(self.B, self.cin, self.h, self.w)}, got {tuple(latents.shape)}")
+        if ctx.shape != self.ctx.shape:
+            raise ValueError(f"context must be {tuple(self.ctx.shape)}, got {tuple(ctx.shape)}")
+        if pooled is None or pooled.shape != self.pooled.shape:
+            raise ValueError(f"pooled projections must be {tuple(self.pooled.shape)}")
+        lat = latents.to(device=self.device, dtype=torch.float16).contiguous()
+        K.nchw_to_nhwc(lat, self.cin, out=self.lat)
+        K.nchw_to_nhwc(lat, self.cin, out=self.next_in[: self.B])
+        K.nchw_to_nhwc(lat, self.cin, out=self.next_in[self.B:])
+        self.ctx.copy_(ctx)
+        self.pooled.copy_(pooled)
+        self.step_idx.zero_()
+        fresh = self.unet.prepare_context(self.ctx, self.pooled)
+        if self.ctx_kv is None:
+            self.ctx_kv = fresh
+        else:
+            for key, t in fresh.items():
+                self.ctx_kv[key].copy_(t)
+
+    @torch.no_grad()
+    def step(self, frozen=False):
+        with A.using(self.arena, frozen=frozen):
+            K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, 256, flip_sin_to_cos=True, shift=0.0,
+                                 out=self.temb_in)
+            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
+            K.cfg_euler_step(self.lat, out, self.guidance, self.sigmas, self.step_idx, self.next_in)
+        self.last_out = out
+        return out
+
+    @torch.no_grad()
+    def run(self, latents=None, ctx=None, pooled=None):
+        if latents is not None:
+            self.set_inputs(latents, ctx, pooled)
+        if self.use_graph and self.graph is None:
+            self.capture()
+            if latents is not None:
+                self.set_inputs(latents, ctx, pooled)
+        for _ in range(self.steps):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.step()
+        return self.latents_nchw()

@@ -1,4 +1,5 @@
-"""DDIM scheduler tables (diffusers DDIMScheduler, SD1.5 scheduler_config) for the device loop.
+"""Scheduler tables for the device loops: DDIM (diffusers DDIMScheduler, SD1.5
+scheduler_config) and flow-match Euler (FlowMatchEulerDiscreteScheduler, SD3 / SD3.5).
 
 Only the per-step constants are computed here (host setup, as diffusers does); the step itself
 is the fused ``qd_cfg_ddim_step`` kernel.  SD1.5 config: beta_start 0.00085, beta_end 0.012,
@@ -31,6 +32,26 @@ def alphas_cumprod(cfg: DDIMConfig = DDIMConfig()):
     else:
         raise NotImplementedError(f"beta_schedule {cfg.beta_schedule}")
     return torch.cumprod(1.0 - betas, dim=0)
+
+
+@dataclass
+class FlowMatchConfig:
+    """FlowMatchEulerDiscreteScheduler config of the SD3 / SD3.5 pipelines."""
+    num_train_timesteps: int = 1000
+    shift: float = 3.0
+
+
+def flowmatch_tables(num_inference_steps, cfg: FlowMatchConfig = FlowMatchConfig()):
+    """(timesteps f32 [S], sigmas f32 [S + 1]) of FlowMatchEulerDiscreteScheduler.set_timesteps
+    (static shift): the training sigmas t/T (float32) are shifted s*x / (1 + (s-1)*x), their
+    ends span a float64 linspace of S timesteps, which are shifted again; sigmas end with 0."""
+    n_t = cfg.num_train_timesteps
+    train = torch.from_numpy(np.linspace(1, n_t, n_t, dtype=np.float32)[::-1].copy()) / n_t
+    train = cfg.shift * train / (1 + (cfg.shift - 1) * train)
+    hi, lo = train[0].item() * n_t, train[-1].item() * n_t
+    sig = np.linspace(hi, lo, num_inference_steps) / n_t
+    sig = torch.from_numpy(cfg.shift * sig / (1 + (cfg.shift - 1) * sig)).to(torch.float32)
+    return sig * n_t, torch.cat([sig, torch.zeros(1)])
 
 
 def ddim_tables(num_inference_steps, cfg: DDIMConfig = DDIMConfig()):

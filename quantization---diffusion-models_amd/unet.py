@@ -454,8 +454,9 @@ def _conv_via_module(layer, x, residual, chan_add, upsample, co_pad):
     return yh
 
 
-def run_linear(layer, x2d, residual=None):
-    """x2d [M, K] -> [M, N] for an nn.Linear or WxAxLinear (fake_quant.py:214-225 semantics)."""
+def run_linear(layer, x2d, residual=None, out=None):
+    """x2d [M, K] -> [M, N] for an nn.Linear or WxAxLinear (fake_quant.py:214-225 semantics).
+    out: optional contiguous [M, N] destination."""
     hook = getattr(layer, "_qd_hook", None)
     if hook is not None:  # SmoothQuant calibration (calib.py)
         hook(x2d)
@@ -464,11 +465,11 @@ def run_linear(layer, x2d, residual=None):
         w, fmt, sc, g = layer.gemm_weight()
         wf = layer.weight if fmt != "f16" else None  # the same weight's fp16 dequantized buffer
         if layer.output_quant_name != "None":
-            y = K.linear(xin, w, fmt, sc, g, bias=layer.bias, weight_f16=wf)
+            y = K.linear(xin, w, fmt, sc, g, bias=layer.bias, weight_f16=wf, out=out)
             y = K.act_fakequant(y, layer.output_quant_name, layer.n_bits_A, out=y)
             return K.add(y, residual, out=y) if residual is not None else y
-        return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual, weight_f16=wf)
-    return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual)
+        return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual, weight_f16=wf, out=out)
+    return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual, out=out)
 
 
 def _geglu_operand(layer):
