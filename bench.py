@@ -37,11 +37,24 @@ def parse():
     ap.add_argument("--batch", type=int, default=4, help="prompts per GPU")
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--denoise-steps", type=int, default=50)
-    ap.add_argument("--mode", default="w8a8-sq", choices=["w8a8-sq", "w8a8", "w4a16", "fp16"])
+    ap.add_argument("--mode", default=None, choices=["w8a8-sq", "w8a8", "w4a16", "fp16"],
+                    help="default: w8a8-sq (sd15), w4a16 (sd35, SURVEY config C5)")
+    ap.add_argument("--model", default="sd15", choices=["sd15", "sd35"],
+                    help="sd35: SD3.5-Large MMDiT, 1024^2, 1 prompt per GPU (config C5) - a secondary line")
     ap.add_argument("--calib-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.mode is None:
+        a.mode = "w4a16" if a.model == "sd35" else "w8a8-sq"
+    if a.model == "sd35":
+        if a.mode == "w8a8-sq":
+            ap.error("SmoothQuant has no SD3.5 block mapping in the reference")
+        if a.res == 512:
+            a.res = 1024
+        if a.batch == 4:
+            a.batch = 1
+    return a
 
 
 QCFG = {
@@ -51,7 +64,23 @@ QCFG = {
 }
 
 
+def mmdit_gflop_per_sample(cfg, s, sc):
+    """Analytic GFLOP of one SD3 transformer evaluation for one sample: token GEMMs (12 C^2 MACs
+    per token per stream per block: q, k, v, out + 4C FF; the last block's context stream only
+    its add_q/k/v 3 C^2) + joint attention (4 (S+Sc)^2 C) + patch embed / proj_out."""
+    c, n = cfg.inner_dim, cfg.num_layers
+    p2c = cfg.patch_size ** 2 * cfg.in_channels
+    macs = n * 12 * c * c * s + (n - 1) * 12 * c * c * sc + 3 * c * c * sc + 2 * s * c * p2c
+    return (2 * macs + n * 4 * (s + sc) ** 2 * c) / 1e9
+
+
 def build_model(args, dev):
+    if args.model == "sd35":
+        from qdiff.models import StableDiffusion3_5
+        model = StableDiffusion3_5.from_pretrained("synthetic:sd35", device=dev, seed=0)
+        if args.mode != "fp16":
+            model.quantize(quant_config=dict(QCFG[args.mode]), quantTransformer=True)
+        return model
     from qdiff.models import StableDiffusion1_x
     model = StableDiffusion1_x.from_pretrained("synthetic:sd15", device=dev, seed=0)
     sd_cpu = None
@@ -192,7 +221,9 @@ def main():
 
     T0 = time.time()
     model = build_model(args, dev)
-    log(f"model built + quantized ({args.mode})")
+    log(f"model built + quantized ({args.model} {args.mode})")
+    if args.model == "sd35":
+        return main_sd35(args, model, rank, world, dev, log)
     B = args.batch
     hw = args.res // 8
     loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.5, use_graph=True)
@@ -253,6 +284,146 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
             line["cpu_baseline"] = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def mmdit_dominant_roofline(model, dev, s, iters=10):
+    """The largest GEMM class of the SD3.5 step: ff.net.0.proj of block 0 on the CFG batch's
+    x-stream tokens (M = 2 S, N = 4C, K = C), through the same run_linear call the model makes
+    (int4 codes or the tuned fp16 LDS-DMA family), timed with HIP events on its stream."""
+    import torch
+    from qdiff.unet import run_linear
+    layer = model.pipeline.transformer.transformer_blocks[0].ff.net[0].proj
+    k, n = layer.in_features, layer.out_features
+    m = 2 * s
+    x = torch.randn(m, k, generator=torch.Generator().manual_seed(0)).half().to(dev)
+    for _ in range(3):
+        run_linear(layer, x)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        run_linear(layer, x)
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    tflops = 2.0 * m * n * k / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
+            "kernel": f"ff.net.0.proj GEMM M={m} N={n} K={k} ({getattr(layer, 'qfmt', 'f16')} weights)",
+            "avg_us": round(ms * 1e3, 2)}
+
+
+def cpu_baseline_sd35(threads, cfg, s, sc, steps):
+    """The reference's CPU path for SD3.5 (torch-CPU fp16 F.linear / SDPA, the ops the fake-quant
+    MMDiT runs) on a bounded sample: one FF-shaped linear over 256 tokens and one joint-attention
+    head group, extrapolated by the analytic FLOPs of a 1024^2 image (GEMM vs attention)."""
+    import torch
+    import torch.nn.functional as F
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    c = cfg.inner_dim
+    x = torch.randn(256, c, generator=g).half()
+    w = (torch.randn(4 * c, c, generator=g) * 0.02).half()
+    t0 = time.time()
+    F.linear(x, w)
+    t_lin = time.time() - t0
+    lin_rate = 2 * 256 * 4 * c * c / t_lin
+    L = s + sc
+    q = torch.randn(1, 2, L, cfg.attention_head_dim, generator=g).half()
+    t0 = time.time()
+    F.scaled_dot_product_attention(q, q, q)
+    t_att = time.time() - t0
+    att_rate = 4 * 2 * L * L * cfg.attention_head_dim / t_att
+    att_gflop = cfg.num_layers * 4 * L * L * c / 1e9
+    gemm_gflop = mmdit_gflop_per_sample(cfg, s, sc) - att_gflop
+    per_image = steps * 2 * (gemm_gflop * 1e9 / lin_rate + att_gflop * 1e9 / att_rate)
+    return {"value": round(1.0 / per_image, 10), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": (f"fp16 linear {c}->{4 * c} x256 tokens {t_lin:.2f}s ({lin_rate / 1e9:.2f} GFLOP/s), SDPA "
+                       f"2 heads x {L}^2 d{cfg.attention_head_dim} {t_att:.2f}s ({att_rate / 1e9:.2f} GFLOP/s); "
+                       f"image = {steps} steps x CFG 2 x class FLOPs / class rates"),
+            "seconds_per_image": round(per_image, 1)}
+
+
+def main_sd35(args, model, rank, world, dev, log):
+    """SD3.5-Large W4A16 g128 1024^2 (SURVEY config C5: batch 8 on 8 GPUs = 1 prompt per GPU)."""
+    import torch
+    import torch.distributed as dist
+    from qdiff import dist as qdist
+    from qdiff.pipeline import synthetic_text_embeddings
+    cfg = model.pipeline.transformer.config
+    B = args.batch
+    hw = args.res // 8
+    sc = 333
+    s = (hw // cfg.patch_size) ** 2
+    loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.0, use_graph=True, ctx_len=sc)
+    full_ctx = torch.empty(2 * B * world, sc, cfg.joint_attention_dim, dtype=torch.float16, device=dev)
+    full_pooled = torch.empty(2 * B * world, cfg.pooled_projection_dim, dtype=torch.float16, device=dev)
+    if rank == 0:
+        prompts = [f"a photograph of synthetic scene {i}" for i in range(B * world)]
+        negs = [""] * (B * world)
+        full_ctx.copy_(torch.cat([synthetic_text_embeddings(negs, seq_len=sc, dim=cfg.joint_attention_dim, device=dev),
+                                  synthetic_text_embeddings(prompts, seq_len=sc, dim=cfg.joint_attention_dim,
+                                                            device=dev)]))
+        full_pooled.copy_(torch.cat([
+            synthetic_text_embeddings([f"{p}\x00pooled" for p in negs], seq_len=1, dim=cfg.pooled_projection_dim,
+                                      device=dev)[:, 0],
+            synthetic_text_embeddings([f"{p}\x00pooled" for p in prompts], seq_len=1, dim=cfg.pooled_projection_dim,
+                                      device=dev)[:, 0]]))
+    g = torch.Generator().manual_seed(42 + rank)
+    lat = torch.randn(B, cfg.in_channels, hw, hw, generator=g).half().to(dev)
+
+    def one_step():
+        qdist.broadcast_context(full_ctx, 0)
+        qdist.broadcast_context(full_pooled, 0)
+        out = loop.run(lat, qdist.shard_context(full_ctx, rank, world), qdist.shard_context(full_pooled, rank, world))
+        return qdist.gather_latents(out, 0)
+
+    for _ in range(args.warmup):
+        one_step()
+    log("warmup done")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    value = B * world * args.steps / dt
+    if rank == 0:
+        assert out is not None and torch.isfinite(out.float()).all(), "non-finite latents"
+        log(f"timed {args.steps} steps: {dt:.3f}s")
+        gflop = mmdit_gflop_per_sample(cfg, s, sc)
+        path_tflops = value * args.denoise_steps * 2 * gflop / 1e3
+        line = {
+            "metric": f"images/sec SD3.5-Large {args.mode.upper()} {args.res}x{args.res} {args.denoise_steps}-step",
+            "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+            "data": "synthetic (random-init SD3.5-Large MMDiT weights N(0,1/fan_in), synthetic text embeddings)",
+            "config": {"workload": f"SD3.5-Large MMDiT {args.mode} g128 fake-quant, {args.res}x{args.res}, {B} "
+                                   f"prompt(s)/GPU (CFG batch {2 * B}), {args.denoise_steps} flow-match Euler "
+                                   f"steps, HIP graph per step (SURVEY config C5)",
+                       "global_batch": B * world, "seq_len": sc, "parallelism": f"dp{world}"},
+            "roofline": mmdit_dominant_roofline(model, dev, s),
+            "path_roofline": {"achieved": round(path_tflops / world, 1), "peak": PEAK_F16_TFLOPS,
+                              "unit": "TFLOP/s per GPU", "frac": round(path_tflops / world / PEAK_F16_TFLOPS, 4),
+                              "flop_per_image": round(2 * args.denoise_steps * gflop * 1e9)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline ...")
+            line["cpu_baseline"] = cpu_baseline_sd35(min(args.cpu_threads, len(os.sched_getaffinity(0))), cfg, s, sc,
+                                                     args.denoise_steps)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

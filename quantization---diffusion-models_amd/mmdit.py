@@ -104,7 +104,9 @@ class PatchEmbed(nn.Module):
         self.pos_embed_max_size = cfg.pos_embed_max_size
         self.proj = nn.Conv2d(cfg.in_channels, cfg.inner_dim, p, stride=p, bias=True)
         pe = get_2d_sincos_pos_embed(cfg.inner_dim, cfg.pos_embed_max_size, base_size=cfg.sample_size // p)
-        self.register_buffer("pos_embed", torch.from_numpy(pe).float().unsqueeze(0), persistent=True)
+        # on the default device (a torch.device context), like the module's parameters
+        self.register_buffer("pos_embed", torch.from_numpy(pe).float().unsqueeze(0).to(torch.empty(0).device),
+                             persistent=True)
 
     def cropped(self, h, w):
         """cropped_pos_embed(h * p, w * p) as a contiguous [h * w, C] tensor."""
@@ -231,14 +233,16 @@ class SD3Transformer2DModel(nn.Module):
 
     # ---------------------------------------------------------------- init
     @torch.no_grad()
-    def init_synthetic(self, seed=0):
-        """Weights N(0, 1/fan_in) (CPU generator), biases 0, norm weights 1; the
-        pos_embed buffer keeps its sincos table."""
-        gen = torch.Generator("cpu").manual_seed(seed)
+    def init_synthetic(self, seed=0, rng_device="cpu"):
+        """Weights N(0, 1/fan_in), biases 0, norm weights 1; the pos_embed buffer
+        keeps its sincos table.  rng_device "cpu" (device-independent values, the parity tests)
+        or the parameters' HIP device (the 8 B-parameter SD3.5-Large draws in seconds)."""
+        gen = torch.Generator(rng_device).manual_seed(seed)
         for name, p in self.named_parameters():
             if name.endswith("weight") and p.dim() >= 2:
                 fan_in = p[0].numel()
-                p.copy_((torch.randn(p.shape, generator=gen) / fan_in ** 0.5).to(p.dtype))
+                w = torch.randn(p.shape, generator=gen, device=rng_device)
+                p.copy_((w / fan_in ** 0.5).to(p.dtype))
             elif name.endswith("bias"):
                 p.zero_()
             elif name.endswith("weight"):
@@ -282,7 +286,8 @@ class SD3Transformer2DModel(nn.Module):
         key = (hp, wp, pe.data_ptr(), pe._version)
         cache = getattr(self, "_qd_pos", None)
         if cache is None or cache[0] != key:
-            cache = (key, self.pos_embed.cropped(hp, wp).to(torch.float16).contiguous())
+            dev = self.pos_embed.proj.weight.device
+            cache = (key, self.pos_embed.cropped(hp, wp).to(device=dev, dtype=torch.float16).contiguous())
             self._qd_pos = cache
         return cache[1]
 

@@ -112,12 +112,14 @@ def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16):
     if model_path in SYNTHETIC:
         mcfg = SYNTHETIC[model_path][1] or (tiny_mmdit_config() if mmdit else tiny_config())
         if mmdit:
-            # built on the target device (a full SD3.5-Large is 8 B parameters)
+            # built and drawn on the target device (a full SD3.5-Large is 8 B parameters)
             with torch.device(device):
                 net = SD3Transformer2DModel(mcfg).to(dtype)
+            big = SYNTHETIC[model_path][1] is not None and torch.device(device).type == "cuda"
+            net.init_synthetic(seed, rng_device=device if big else "cpu")
         else:
             net = UNet2DConditionModel(mcfg).to(dtype)
-        net.init_synthetic(seed)
+            net.init_synthetic(seed)
     else:
         sub = "transformer" if mmdit else "unet"
         with open(os.path.join(model_path, sub, "config.json")) as f:

@@ -196,6 +196,39 @@ def test_sd3_medium_shaped_block_no_qk_norm():
     _check_parity(got, ref, ref32, "SD3-M-shaped tiny MMDiT W4A8")
 
 
+@pytest.mark.timeout(600)
+def test_sd35_large_width_two_blocks_512():
+    """SD3.5-Large width (C = 2432, 38 heads x 64, RMSNorm qk-norm, joint_attention_dim 4096,
+    pooled 2048, pos_embed_max_size 192) with 2 of its 38 blocks, 512^2 latents (S = 1024) and
+    the 333-token T5+CLIP context, W4A16 g128, CFG batch 2 - against the fp32 oracle with the
+    spread bound of the tiny model (the half CPU oracle is too slow at this width on the box)."""
+    import dataclasses as dc
+    import time
+    from qdiff.mmdit import SD35_LARGE, SD3Transformer2DModel
+    from qdiff.models import StableDiffusion3_5
+    from qdiff.pipeline_io import QDiffPipeline
+    t0 = time.time()
+    cfg = dc.replace(SD35_LARGE, num_layers=2, sample_size=64)
+    with torch.device(DEV):
+        tr = SD3Transformer2DModel(cfg).half()
+    tr.init_synthetic(7, rng_device=DEV)
+    sd = {k: v.detach().cpu() for k, v in tr.state_dict().items()}
+    model = StableDiffusion3_5(QDiffPipeline(transformer=tr, class_name="StableDiffusion3Pipeline"),
+                               "StableDiffusion3Pipeline", False, {}, None)
+    qc = dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False)
+    model.quantize(quant_config=dict(qc), quantTransformer=True)
+    x, enc, pooled = _inputs(cfg, 13, b=1, sc=333)
+    got = _one_eval(model, x, 974.1, enc, pooled)
+    torch.cuda.synchronize()
+    print(f"[sd35-width] gpu eval {time.time() - t0:.1f}s", flush=True)
+    ref32 = RefMMDiT(_cfgdict(cfg), sd, qc, variant="fp32").forward(x, 974.1, enc, pooled)
+    print(f"[sd35-width] fp32 oracle {time.time() - t0:.1f}s", flush=True)
+    mx32, mean32 = _rel_errs(got, ref32)
+    print(f"SD3.5-L width, 2 blocks, W4A16: gpu-vs-fp32 max {mx32:.4g} mean {mean32:.4g}")
+    assert torch.isfinite(got).all()
+    assert mx32 <= 0.02 and mean32 <= 0.004, (mx32, mean32)
+
+
 def test_quantized_buffers_bit_exact_and_output_quant_names():
     from oracle.unet_ref import quantize_state_dict
     from qdiff.fake_quant import WxAxLinear
