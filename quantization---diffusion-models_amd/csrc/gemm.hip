@@ -764,6 +764,222 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   gemm_epilogue<BM, BN, NT, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
+// ---- ping-pong GEMM (256 x BN tile, 8 waves, BK 32, 4-stage LDS-DMA ring) ----------------
+// 8 waves = 2 (M halves) x 4 (N quarters); wave tile 128 x BN/4.  The two M-half wave groups
+// run one barrier apart ("ping-pong"): each SIMD hosts one wave of each group, and between two
+// consecutive workgroup barriers one group issues its MFMAs while the other issues its LDS
+// fragment reads and its share of the LDS-DMA prefetch, so the matrix pipe is fed by one group
+// while the other waits on memory.  A K-tile (32 deep) is two phases per wave:
+//   phase a: read A frags 0-3 + all B frags, issue A loads of K-tile kt+2 | MFMAs (i 0-3)
+//   phase b: read A frags 4-7, wait for K-tile kt+1, issue B loads of kt+2  | MFMAs (i 4-7)
+// each phase = [ds_reads, DMA issue] s_barrier lgkmcnt(0) [MFMAs] s_barrier.
+// Hazards (phase p of a wave of group g sits between barriers 2p+g-1 .. 2p+g+1):
+//  RAW: K-tile t is waited for (own counted vmcnt) in phase b of t-1, before that phase's first
+//       barrier, and read in phase a of t or later, i.e. after a barrier every wave of both groups
+//       passed after its wait;
+//  WAR: K-tile t+2 overwrites the stage of t-2, whose last reads (phase b of t-2) retired before
+//       barrier 4t-4 at the latest; the overwrite is issued after barrier 4t-1.
+// The 256-row tile halves the L2->LDS bytes per flop of the 128-row DMA tiles, the staging rate
+// that bounds them.
+constexpr int pp_lds_halves(int bn) {
+  return 4 * (256 + bn) * 32 > 128 * (bn + 8) ? 4 * (256 + bn) * 32 : 128 * (bn + 8);
+}
+
+template <int BN, int AMODE, bool SPLIT>
+__global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
+  constexpr int BM = 256, BK = 32, NT = 512;
+  constexpr int WN = BN / 4, TN = WN / 16, TM = 8;
+  constexpr int ASZ = BM * BK, SSZ = (BM + BN) * BK;
+  static_assert(WN % 16 == 0, "wave tile width");
+  using AL = ADma<BM, NT, AMODE, BK>;
+  using BL = BDma<BN, NT, BK>;
+  __shared__ __attribute__((aligned(16))) f16 smem[pp_lds_halves(BN)];
+
+  const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int nwg = ntile * p.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = wg / p.splits, split = wg - tile * p.splits;
+  const int bm = tile / nbn, bn = tile - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int kbeg = split * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int wm0 = wr * 128, wn0 = wc * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  AL al;
+  BL bl;
+  al.init(p, m0, kbeg, wid);
+  bl.init(p, n0, wid);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  // prologue: K-tiles 0 and 1 in flight, wait for 0
+  if (nk > 0) {
+    al.issue(p, kbeg, smem, wid);
+    bl.issue(p, kbeg, smem + ASZ, wid);
+  }
+  if (nk > 1) {
+    al.issue(p, kbeg + BK, smem + SSZ, wid);
+    bl.issue(p, kbeg + BK, smem + SSZ + ASZ, wid);
+    wait_vm_rt(AL::L + BL::count(wid));
+  } else {
+    wait_vm<0>();
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 runs one barrier behind
+  asm volatile("" ::: "memory");
+
+  f16x8 af[4], bf[TN];
+  auto mfma_block = [&](int ih) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[ih * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto bar = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const f16* As = smem + (kt & 3) * SSZ;
+    const f16* Bs = As + ASZ;
+    const bool pre = kt + 2 < nk;
+    f16* nxt = smem + ((kt + 2) & 3) * SSZ;
+    // ---- phase a
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + i * 16 + fr, fq));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BK>(wn0 + j * 16 + fr, fq));
+    if (pre) al.issue(p, kbeg + (kt + 2) * BK, nxt, wid);
+    bar();
+    mfma_block(0);
+    bar();
+    // ---- phase b
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + 64 + i * 16 + fr, fq));
+    if (kt + 1 < nk) {
+      if (pre) wait_vm_rt(AL::L);
+      else wait_vm<0>();
+    }
+    if (pre) bl.issue(p, kbeg + (kt + 2) * BK, nxt + ASZ, wid);
+    bar();
+    mfma_block(1);
+    bar();
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
+  const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
+  const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
+  const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
+  if constexpr (SPLIT) {
+    float* part = p.part + (long)split * p.M * p.N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn0 + j * 16 + fq * 4;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm0 + i * 16 + fr;
+        if (m < p.M) *reinterpret_cast<f32x4*>(part + (long)m * p.N + n) = acc[i][j];
+      }
+    }
+    return;
+  }
+  // epilogue in two 128-row passes (one per wave group) through a [128][BN + 8] fp16 LDS tile:
+  // h = half(acc + bias) -> per-column amax (rows_per_sample % 128 == 0) -> (+GEGLU) (+residual)
+  constexpr int LP = BN + 8;
+  f16* ct = smem;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wr == pass) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn0 + j * 16 + fq * 4;
+        const int n = n0 + nl;
+        const bool col_ok = n < p.N;
+        f16x4 bq = {};
+        if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+        float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ml = i * 16 + fr;
+          const bool ok = m0 + wm0 + ml < p.M && col_ok;
+          f16x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
+            if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+          }
+          *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
+        }
+        if (do_amax && !geglu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
+          const int row0 = m0 + wm0;
+          if (fr == 0 && col_ok && row0 < p.M) {
+            float* a = p.amax + (long)(row0 / p.rows_per_sample) * p.N + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int cpr = geglu ? BN / 16 : BN / 8;
+    const int on0 = geglu ? n0 >> 1 : n0, oN = geglu ? p.N >> 1 : p.N;
+    const int mb = m0 + pass * 128;
+#pragma unroll 2
+    for (int e = threadIdx.x; e < 128 * cpr; e += NT) {
+      const int row = e / cpr, c = e - row * cpr;
+      const int m = mb + row, n = on0 + c * 8;
+      if (m < p.M && n < oN) {
+        f16x8 v;
+        if (geglu) {
+          const int tc = (c >> 1) * 32 + (c & 1) * 8;
+          const f16x8 hv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc);
+          const f16x8 gv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc + 16);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)hv[r] * (float)(f16)gelu_f((float)gv[r]));
+        } else {
+          v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+        }
+        if (has_res) {
+          const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
+        }
+        *reinterpret_cast<f16x8*>(p.y + (long)m * p.ldy + n) = v;
+      }
+    }
+    if (pass == 0) __syncthreads();
+  }
+}
+
 // ---- halo-reuse implicit-GEMM conv (3x3, stride 1, pad 1) ----------------------------------
 // A block owns 256 output pixels = RB = 256 / W whole image rows of one image (W in {16, 32,
 // 64}) x BN output channels.  K is walked chunk-major: for each 64-channel chunk of the input
@@ -900,14 +1116,17 @@ static bool halo_ok(const GemmArgs& p, int bn) {
          (p.rows_per_sample % 64 == 0);
 }
 
-// split-K reduction + epilogue: block = 64 rows x 256 columns (64 column quads x 4 row groups
-// of 16 rows); slabs summed in split order (deterministic); amax: one atomic per column per
-// 64 rows (rows_per_sample % 64 == 0).
+// split-K reduction + epilogue: block = 4*RPT rows x 256 columns (64 column quads x 4 row
+// groups of RPT rows; RPT small enough that the launch has >= ~512 blocks - the slab read is
+// latency-bound, not bandwidth-bound, at the small M that splits K); slabs summed in split order
+// (deterministic: every RPT gives identical results); the RPT rows of a thread are loaded
+// together per split.  amax: one atomic per column per 4*RPT rows (rows_per_sample % 16 == 0).
+template <int RPT>
 __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   __shared__ float red[4][256];
   const int cq = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int n = blockIdx.x * 256 + cq * 4;
-  const int mb = blockIdx.y * 64;
+  const int mb = blockIdx.y * (4 * RPT);
   const bool col_ok = n < p.N;
   const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
@@ -916,15 +1135,30 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
   float cm[4] = {0.f, 0.f, 0.f, 0.f};
   if (col_ok) {
-    for (int rr = 0; rr < 16; ++rr) {
-      const int m = mb + rg * 16 + rr;
+    const long mn = (long)p.M * p.N;
+    f32x4 s[RPT];
+    long off[RPT];
+#pragma unroll
+    for (int rr = 0; rr < RPT; ++rr) {
+      const int m = min(mb + rg * RPT + rr, p.M - 1);  // clamped: rows >= M are computed, not stored
+      off[rr] = (long)m * p.N + n;
+      s[rr] = *reinterpret_cast<const f32x4*>(p.part + off[rr]);
+    }
+    for (int k = 1; k < p.splits; ++k) {
+      f32x4 t[RPT];
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) t[rr] = *reinterpret_cast<const f32x4*>(p.part + k * mn + off[rr]);
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) s[rr] += t[rr];
+    }
+#pragma unroll
+    for (int rr = 0; rr < RPT; ++rr) {
+      const int m = mb + rg * RPT + rr;
       if (m >= p.M) break;
-      f32x4 s = *reinterpret_cast<const f32x4*>(p.part + (long)m * p.N + n);
-      for (int k = 1; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(p.part + ((long)k * p.M + m) * p.N + n);
       f16x4 h;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        h[r] = (f16)(s[r] + (float)bq[r]);
+        h[r] = (f16)(s[rr][r] + (float)bq[r]);
         cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
       }
       if (has_res) {
@@ -982,8 +1216,8 @@ static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register
 extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
                  (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
-                 variant == 201,
-             "qd_gemm_force: -1, 0..3 or 100 + DMA variant");
+                 variant == 201 || (variant >= 300 && variant <= 302),
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant, 200/201 halo conv, 300-302 ping-pong");
   g_force = variant;
   return 0;
 }
@@ -1030,6 +1264,19 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         if (tiles_mn * sp > 256) break;
         best.splits = sp;
         best.kps = nc / sp;
+      }
+    }
+  } else if (g_force >= 300 && g_force <= 302 && !quant_w) {
+    // ping-pong 256 x {256, 320, 192} tile: wave rows 128 (amax needs whole-sample wave tiles)
+    const int bnp = g_force == 300 ? 256 : g_force == 301 ? 320 : 192;
+    if (!amax || rows_per_sample % 128 == 0) {
+      best = {3, 256, bnp, 0, 1, K};
+      const long tiles_mn = (long)((M + 255) / 256) * ((N + bnp - 1) / bnp);
+      for (int sp = 2; sp <= 32 && !geglu && K % 32 == 0; ++sp) {
+        if ((K / 32) % sp != 0 || K / sp < 512) continue;
+        if (tiles_mn * sp > 256L) break;
+        best.splits = sp;
+        best.kps = K / sp;
       }
     }
   } else if (g_force >= 100 && g_force < 200 && !quant_w) {
@@ -1091,7 +1338,12 @@ static void launch_dma(const GemmArgs& p, int var, hipStream_t st) {
 
 template <int AMODE, bool SPLIT>
 static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t st) {
-  if (pl.kind == 2) {
+  if (pl.kind == 3) {
+    const int nwg = ((p.M + 255) / 256) * ((p.N + pl.bn - 1) / pl.bn) * p.splits;
+    if (pl.bn == 256) k_gemm_pp<256, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    else if (pl.bn == 320) k_gemm_pp<320, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    else k_gemm_pp<192, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+  } else if (pl.kind == 2) {
     const int nwg = (p.M / 256) * (p.N / pl.bn) * p.splits;
     if (pl.bn == 160) k_conv_halo<160><<<nwg, 512, 0, st>>>(p);
     else k_conv_halo<128><<<nwg, 512, 0, st>>>(p);
@@ -1132,8 +1384,12 @@ static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t
   } else {
     p.part = ws;
     launch_tile<AMODE, true>(p, pl, fmt, st);
-    dim3 g((p.N + 255) / 256, (p.M + 63) / 64);
-    k_splitk_reduce<<<g, 256, 0, st>>>(p);
+    const int gx = (p.N + 255) / 256;
+    if ((long)gx * ((p.M + 15) / 16) >= 512) {
+      k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
+    } else {
+      k_splitk_reduce<1><<<dim3(gx, (p.M + 3) / 4), 256, 0, st>>>(p);
+    }
   }
 }
 

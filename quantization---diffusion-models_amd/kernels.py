@@ -161,7 +161,7 @@ def conv_weight_khwc(w, ci_pad):
 # candidates reduce fixed-order fp32 slabs (deterministic for a given choice).
 # QD_GEMM_TUNE=0 disables the search (library planner only).
 REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
-DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109)  # LDS-DMA variants (fp16 weights)
+DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 300, 301, 302)  # LDS-DMA variants (fp16 weights; 3xx ping-pong 256-row)
 HALO_VARIANTS = (200, 201)  # 3x3 conv with the activation halo staged once per channel chunk
 _TUNE = {}
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
