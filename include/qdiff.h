@@ -101,6 +101,9 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 #define QD_EPI_AMAX_ZEROED 16 /* with QD_EPI_AMAX: amax already holds zeros (pooled, zeroed once
                                  per step); the call skips its own zero-fill launch */
 #define QD_EPI_GEGLU 8       /* B holds [hidden; gate] halves (N = 2*I): out[M, I] = h * gelu(g) */
+#define QD_EPI_GELU_TANH 32  /* out = half(gelu_tanh(half(y + bias))): diffusers GELU(approximate="tanh")
+                                (SD3 FeedForward net.0) applied to the rounded projection output;
+                                no residual / amax / GEGLU with it */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.

@@ -101,6 +101,12 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)
 // exact-erf GELU as torch's F.gelu(approximate='none')
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// tanh-approximate GELU as torch's F.gelu(approximate='tanh') (fp32 opmath)
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float inner = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.0f + tanhf(inner));
+}
+
 }  // namespace qd
 
 #define QD_CHECK_LAUNCH()                                              \

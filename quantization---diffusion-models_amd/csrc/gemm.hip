@@ -324,6 +324,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
     const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
+    const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
     {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -380,6 +381,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           for (int r = 0; r < 8; ++r) v[r] = (f16)((float)hv[r] * (float)(f16)gelu_f((float)gv[r]));
         } else {
           v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+          if (gtanh) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = (f16)gelu_tanh_f((float)v[r]);
+          }
         }
         if (has_res) {
           const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
@@ -896,6 +901,7 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
   const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
   const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
+  const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
   if constexpr (SPLIT) {
     float* part = p.part + (long)split * p.M * p.N;
 #pragma unroll
@@ -967,6 +973,10 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
           for (int r = 0; r < 8; ++r) v[r] = (f16)((float)hv[r] * (float)(f16)gelu_f((float)gv[r]));
         } else {
           v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+          if (gtanh) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = (f16)gelu_tanh_f((float)v[r]);
+          }
         }
         if (has_res) {
           const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
@@ -1131,6 +1141,7 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
   const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
+  const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
   f16x4 bq = {};
   if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
   float cm[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1160,6 +1171,10 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
       for (int r = 0; r < 4; ++r) {
         h[r] = (f16)(s[rr][r] + (float)bq[r]);
         cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+      }
+      if (gtanh) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] = (f16)gelu_tanh_f((float)h[r]);
       }
       if (has_res) {
         const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)m * p.ldy + n);
@@ -1409,6 +1424,8 @@ static int check_common(const GemmArgs& p, int fmt) {
              "amax epilogue needs rows_per_sample % 64 == 0");
   QD_REQUIRE(!(p.epi & QD_EPI_GEGLU) || (!(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL)) && p.N % 32 == 0),
              "GEGLU epilogue: N % 32 == 0, no residual / amax");
+  QD_REQUIRE(!(p.epi & QD_EPI_GELU_TANH) || !(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL | QD_EPI_GEGLU)),
+             "GELU-tanh epilogue: no residual / amax / GEGLU");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");

@@ -70,6 +70,26 @@ __device__ __forceinline__ void gn_xf_init(const GnIn& in, int c, long n, int ch
 // XF: 0 plain source(s); 1 finalize transform (output quant if in.qmax > 0, + cadd if set:
 // a zero cadd adds +0, which leaves every fp16 value - including -0 - bit-identical... except
 // -0 + +0 = +0; the callers pass cadd only when the reference adds it)
+__device__ __forceinline__ f16x8 gn_raw8(const GnIn& in, int c, long row, int ch) {
+  const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
+  return *reinterpret_cast<const f16x8*>(p);
+}
+
+template <int XF>
+__device__ __forceinline__ f16x8 gn_xf8(const GnIn& in, f16x8 v, const GnXf& t) {
+  if constexpr (XF == 1) {
+    const bool q = in.qmax > 0, a = in.cadd != nullptr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f16 o = v[j];
+      if (q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
+      if (a) o = (f16)((float)o + t.ca[j]);
+      v[j] = o;
+    }
+  }
+  return v;
+}
+
 template <int XF>
 __device__ __forceinline__ f16x8 gn_load8(const GnIn& in, int c, long row, int ch, const GnXf& t) {
   const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
@@ -101,7 +121,7 @@ __device__ __forceinline__ float gn_load1(const GnIn& in, int c, long n, long ro
 
 struct GnGeom {
   int bx, by, gx, z, rpb;  // apply pass
-  int bys, zs, rpbs;       // stats pass: 1024-thread blocks, 4 rows per thread
+  int bys, zs, rpbs;       // stats pass: 256-thread blocks, up to 16 rows per thread
 };
 static GnGeom gn_geom(int n, int hw, int c) {
   GnGeom g;
@@ -113,8 +133,10 @@ static GnGeom gn_geom(int n, int hw, int c) {
   while (g.rpb > g.by && (long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) < 2048) g.rpb /= 2;
   while ((long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) > 8192) g.rpb *= 2;
   g.z = (hw + g.rpb - 1) / g.rpb;
-  g.bys = std::max(1, 1024 / g.bx);
-  g.rpbs = g.bys * 4;
+  // stats: 8 loads in flight per thread, 16 rows per thread while the grid keeps >= 512 blocks
+  g.bys = g.by;
+  g.rpbs = g.bys * 16;
+  while (g.rpbs > g.bys * 8 && (long)g.gx * n * ((hw + g.rpbs - 1) / g.rpbs) < 256) g.rpbs /= 2;
   g.zs = (hw + g.rpbs - 1) / g.rpbs;
   return g;
 }
@@ -126,9 +148,9 @@ __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
 }
 
 template <int XF>
-__global__ void __launch_bounds__(1024) k_gn_stats(GnIn in, int hw, int c, int cg, int rows_per_block,
-                                                   float4* __restrict__ part) {
-  __shared__ float2 red[1024][8];
+__global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg, int rows_per_block,
+                                                  float4* __restrict__ part) {
+  __shared__ float2 red[256][8];
   const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
   const int chunk = blockIdx.x * bx + tx;
   const bool active = chunk * 8 < c;
@@ -146,20 +168,21 @@ __global__ void __launch_bounds__(1024) k_gn_stats(GnIn in, int hw, int c, int c
     sh[j] = active ? gn_load1(in, c, n, n * hw, (ch + j) / cg * cg) : 0.f;
   }
   if (active) {
-    // 4 rows per batch, all loads issued before any use (memory-level parallelism)
-    for (int rb = r0 + ty; rb < r1; rb += 4 * by) {
-      f16x8 v[4];
+    // 8 rows per batch, all loads issued before any use (memory-level parallelism)
+    for (int rb = r0 + ty; rb < r1; rb += 8 * by) {
+      f16x8 v[8];
       // unconditional loads (row clamped): a guarded load makes hipcc wait per load
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = gn_load8<XF>(in, c, n * hw + min(rb + u * by, r1 - 1), ch, xf);
+      for (int u = 0; u < 8; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * by, r1 - 1), ch);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+      for (int u = 0; u < 8; ++u) QD_PIN(v[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         if (rb + u * by >= r1) break;
+        const f16x8 w = gn_xf8<XF>(in, v[u], xf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float xv = (float)v[u][j];
+          const float xv = (float)w[j];
           const float a = xv - sh[j];
           s1[j] += a;
           s2[j] = fmaf(a, a, s2[j]);
@@ -217,17 +240,30 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
   __shared__ float stat[2];
   __shared__ int nflag;
   __shared__ int flagged[1024];
+  __shared__ int cmin[1024], cmax[1024];  // per-channel min / max as order-preserving ints
   __shared__ float fmx[4];
   const int groups = c / cg;
   const int ni = blockIdx.x / groups, g0 = (blockIdx.x % groups) * cg;
   const int t = threadIdx.x;
   if (t == 0) nflag = 0;
+  for (int j = t; j < cg; j += 256) {
+    cmin[j] = 0x7fffffff;
+    cmax[j] = (int)0x80000000;
+  }
+  __syncthreads();
+  // one pass over the (z, channel) partials: group sums in registers, channel extremes by LDS
+  // integer min / max of the order-preserving image of the float (exact, order-independent)
   float s1 = 0.f, s2 = 0.f;
   for (int e = t; e < Z * cg; e += 256) {
     const int z = e / cg, j = e - z * cg;
     const float4 v = part[((long)ni * Z + z) * c + g0 + j];
     s1 += v.x;
     s2 += v.y;
+    if (quant) {
+      const int a = __float_as_int(v.z), b = __float_as_int(v.w);
+      atomicMin(&cmin[j], a ^ ((a >> 31) & 0x7fffffff));
+      atomicMax(&cmax[j], b ^ ((b >> 31) & 0x7fffffff));
+    }
   }
   s1 = wave_sum(s1);
   s2 = wave_sum(s2);
@@ -253,12 +289,9 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const float2 k = make_float2(sc, fmaf(-sc, stat[0], (float)beta[ch]));
     coef[i] = k;
     if (!quant) continue;
-    float mn = INFINITY, mx = -INFINITY;
-    for (int z = 0; z < Z; ++z) {
-      const float4 v = part[((long)ni * Z + z) * c + ch];
-      mn = fminf(mn, v.z);
-      mx = fmaxf(mx, v.w);
-    }
+    const int ia = cmin[j], ib = cmax[j];
+    const float mn = __int_as_float(ia ^ ((ia >> 31) & 0x7fffffff));
+    const float mx = __int_as_float(ib ^ ((ib >> 31) & 0x7fffffff));
     const float lo = fabsf(gn_out(mn, k, silu)), hi = fabsf(gn_out(mx, k, silu));
     const float top = fabsf(gn_out(sc >= 0.f ? mx : mn, k, silu));  // largest z
     if (!silu) {
@@ -319,16 +352,17 @@ __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int ro
   for (int rb = r0 + threadIdx.y; rb < r1; rb += 4 * by) {
     f16x8 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = gn_load8<XF>(in, c, n * hw + min(rb + u * by, r1 - 1), ch, xf);
+    for (int u = 0; u < 4; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * by, r1 - 1), ch);
 #pragma unroll
     for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (rb + u * by >= r1) break;
+      const f16x8 w = gn_xf8<XF>(in, v[u], xf);
       f16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float val = gn_out((float)v[u][j], k[j], SILU);
+        const float val = gn_out((float)w[j], k[j], SILU);
         if constexpr (Q) o[j] = fq_apply_r(val, sq[j], rq[j]);
         else o[j] = (f16)val;
       }

@@ -55,13 +55,15 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 // amax reductions
 // ---------------------------------------------------------------------------------------
 
-// NHWC per-(n, c) column max over rows.  block (64, 4): x = 8-channel chunk, y = row lane.
-// grid (ceil(c/8/64), n, row_splits).  requires c % 8 == 0.
+// NHWC per-(n, c) column max over rows.  block (bx, by), bx * by <= 256: x = 8-channel chunk
+// (bx = min(chunks, 64): no idle lanes at C = 320), y = row lane, 8 row loads in flight per
+// thread.  grid (ceil(chunks / bx), n, row_splits).  requires c % 8 == 0.
 // x2 != null: channels [c1, c) come from x2 (row stride c - c1), [0, c1) from x (row stride c1)
 __global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, const f16* __restrict__ x2, int c1,
                                                      int hw, int c, int rows_per_split, float* __restrict__ amax) {
-  __shared__ float red[4][64][8];
-  const int chunk = blockIdx.x * 64 + threadIdx.x;
+  __shared__ float red[256][8];
+  const int bx = blockDim.x, by = blockDim.y;
+  const int chunk = blockIdx.x * bx + threadIdx.x;
   const int n = blockIdx.y;
   const int r0 = blockIdx.z * rows_per_split;
   const int r1 = min(hw, r0 + rows_per_split);
@@ -73,31 +75,42 @@ __global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, 
     const bool first = x2 == nullptr || ch < c1;
     const int ld = x2 == nullptr ? c : (first ? c1 : c - c1);
     const f16* base = first ? x + (size_t)n * hw * ld + ch : x2 + (size_t)n * hw * ld + (ch - c1);
-    for (int rb = r0 + threadIdx.y; rb < r1; rb += 16) {
-      f16x8 v[4];
+    for (int rb = r0 + threadIdx.y; rb < r1; rb += 8 * by) {
+      f16x8 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f16x8*>(base + (size_t)min(rb + 4 * u, r1 - 1) * ld);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f16x8*>(base + (size_t)min(rb + by * u, r1 - 1) * ld);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+      for (int u = 0; u < 8; ++u) QD_PIN(v[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (rb + 4 * u >= r1) break;
+      for (int u = 0; u < 8; ++u) {
+        if (rb + by * u >= r1) break;
 #pragma unroll
         for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)v[u][j]));
       }
     }
   }
+  const int t = threadIdx.y * bx + threadIdx.x;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[threadIdx.y][threadIdx.x][j] = m[j];
+  for (int j = 0; j < 8; ++j) red[t][j] = m[j];
   __syncthreads();
   if (threadIdx.y == 0 && chunk * 8 < c) {
+    for (int k = 1; k < by; ++k)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = fmaxf(fmaxf(red[0][threadIdx.x][j], red[1][threadIdx.x][j]),
-                      fmaxf(red[2][threadIdx.x][j], red[3][threadIdx.x][j]));
-      atomic_max_pos(&amax[(size_t)n * c + chunk * 8 + j], v);
-    }
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], red[k * bx + threadIdx.x][j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomic_max_pos(&amax[(size_t)n * c + chunk * 8 + j], m[j]);
   }
+}
+
+// launch geometry of k_colmax_nhwc: 16 rows per thread while the grid keeps >= 512 blocks
+static void colmax_launch(const f16* x, const f16* x2, int c1, int n, long hw, int c, float* amax, hipStream_t st) {
+  const int chunks = c / 8;
+  const int bx = chunks < 64 ? chunks : 64, by = 256 / bx;
+  const int gx = (chunks + bx - 1) / bx;
+  long rps = (long)by * 16;
+  while (rps > by && (long)gx * n * ((hw + rps - 1) / rps) < 512) rps /= 2;
+  k_colmax_nhwc<<<dim3(gx, n, (unsigned)((hw + rps - 1) / rps)), dim3(bx, by), 0, st>>>(x, x2, c1, (int)hw, c,
+                                                                                      (int)rps, amax);
 }
 
 // contiguous-row max: one wave per row of length len (NCHW per-(n,c) rows, per-token rows).
@@ -256,11 +269,7 @@ static int launch_absmax(const void* x, int layout, int n, int c, int h, int w, 
     if (!zeroed) qd_zero_f32(amax, (size_t)n * c, st);
     if (layout == QD_LAYOUT_NHWC) {
       QD_REQUIRE(c % 8 == 0, "per_channel NHWC needs C % 8 == 0");
-      const int chunks = c / 8;
-      int rps = 64;
-      while (rps < hw && ((hw + rps - 1) / rps) * n * ((chunks + 63) / 64) > 2048) rps *= 2;
-      dim3 grid((chunks + 63) / 64, n, (int)((hw + rps - 1) / rps));
-      k_colmax_nhwc<<<grid, dim3(64, 4), 0, st>>>((const f16*)x, nullptr, c, (int)hw, c, rps, amax);
+      colmax_launch((const f16*)x, nullptr, c, n, hw, c, amax, st);
     } else {
       const long rows = (long)n * c;
       k_rowmax<<<grid1(rows, 4), 256, 0, st>>>((const f16*)x, rows, (int)hw, amax);
@@ -593,11 +602,7 @@ extern "C" int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int 
   if ((long)n * hw == 0) return 0;
   hipStream_t st = S(stream);
   if (!amax_zeroed) qd_zero_f32(amax, (size_t)n * c, st);
-  const int chunks = c / 8;
-  int rps = 64;
-  while (rps < hw && ((hw + rps - 1) / rps) * n * ((chunks + 63) / 64) > 2048) rps *= 2;
-  k_colmax_nhwc<<<dim3((chunks + 63) / 64, n, (hw + rps - 1) / rps), dim3(64, 4), 0, st>>>(
-      (const f16*)x, (const f16*)x2, c1, hw, c, rps, amax);
+  colmax_launch((const f16*)x, (const f16*)x2, c1, n, hw, c, amax, st);
   const CrGeom g = cr_geom(n, hw, c);
   k_apply_nhwc<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, st>>>((const f16*)x, (const f16*)x2, c1, (f16*)y, hw, c,
                                                                  c, qmax_of(n_bits), g.rpb, amax);

@@ -20,6 +20,7 @@ WFMT = {"f16": 0, "i8": 1, "i4": 2}
 EPI_BIAS, EPI_RESIDUAL, EPI_AMAX = 1, 2, 4
 EPI_AMAX_ZEROED = 16
 EPI_GEGLU = 8
+EPI_GELU_TANH = 32
 GRAN_ZEROED = 0x100
 
 
@@ -191,23 +192,31 @@ def _choose(key, cands, run):
     if not _TUNE_ON or torch.cuda.is_current_stream_capturing() or len(cands) == 1:
         return cands[0] if len(cands) == 1 else None
     st = torch.cuda.current_stream()
+    times = {}
+    # two interleaved rounds of 4 timed launches per candidate, best round kept: a candidate's
+    # time is not skewed by where in the sweep the clocks / caches happened to be
+    for rnd in range(2):
+        for c in cands:
+            if rnd and c not in times:
+                continue
+            try:
+                run(c)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(4):
+                    run(c)
+                e1.record(st)
+                e1.synchronize()
+                t = e0.elapsed_time(e1)
+            except RuntimeError:  # a candidate the library rejects for this shape
+                continue
+            finally:
+                _force(-1)
+            times[c] = min(times.get(c, float("inf")), t)
     best, best_t = None, float("inf")
     for c in cands:
-        try:
-            run(c)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(3):
-                run(c)
-            e1.record(st)
-            e1.synchronize()
-            t = e0.elapsed_time(e1)
-        except RuntimeError:  # a candidate the library rejects for this shape
-            continue
-        finally:
-            _force(-1)
-        if t < best_t * 0.98:
-            best, best_t = c, t
+        if c in times and times[c] < best_t * 0.98:
+            best, best_t = c, times[c]
     _TUNE[key] = best
     return best
 
@@ -223,10 +232,11 @@ def _cands(ops):
 
 
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
-           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None):
+           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None, gelu_tanh=False):
     """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K).
     geglu: W rows (and bias) interleaved in 16-row [hidden | gate] blocks (geglu_interleave);
     returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue).
+    gelu_tanh: returns half(gelu_tanh(half(x . W^T + b))) (SD3 FeedForward GELU(approximate="tanh")).
     weight_f16: the same weight's fp16 dequantized buffer (bit-identical to dequantizing the
     codes); when given, the kernel search also considers the fp16 LDS-DMA family."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
@@ -239,7 +249,7 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
         out = _empty((M, N // 2 if geglu else N), torch.float16, x2d.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
-          (EPI_GEGLU if geglu else 0)
+          (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0)
     if residual is not None:
         _chk(residual, "residual")
     ops = [(weight, wfmt, scales, group)]

@@ -424,8 +424,19 @@ def _joint_rows_out(layer, o, n, s0, s1):
 
 
 def _ff(ff, x):
-    f = run_linear(ff.net[0].proj, x)
-    f = K.gelu_tanh(f, out=f)
+    """FeedForward(activation_fn="gelu-approximate"): net.0.proj + GELU-tanh (fused into the
+    GEMM epilogue when the projection has no calibration hook / act quant) -> net.2."""
+    proj = ff.net[0].proj
+    plain = getattr(proj, "_qd_hook", None) is None and not (
+        isinstance(proj, WxAxLinear) and (proj.quantize_act or proj.output_quant_name != "None"))
+    if plain:
+        w, fmt, sc, g = _linear_op(proj)
+        wf = proj.weight if fmt != "f16" else None
+        b = proj.bias if isinstance(proj, WxAxLinear) else _f16(proj.bias)
+        f = K.linear(x, w, fmt, sc, g, bias=b, weight_f16=wf, gelu_tanh=True)
+    else:
+        f = run_linear(proj, x)
+        f = K.gelu_tanh(f, out=f)
     return run_linear(ff.net[2], f)
 
 

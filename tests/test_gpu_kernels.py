@@ -365,12 +365,15 @@ def test_timestep_embedding_and_ddim(dev):
 # ------------------------------------------------------------------ GEMM kernel families
 @pytest.fixture
 def forced_gemm():
-    from qdiff import _lib
+    """Run every GEMM of the test on one qd_gemm_force id (kernels.force_gemm overrides the
+    tuner's per-shape choice; -1 / None = tuned).  A variant that does not apply to a shape
+    falls back to the library planner inside libqdiff."""
+    from qdiff import kernels
 
     def force(v):
-        _lib.call("qd_gemm_force", v)
+        kernels.force_gemm(None if v is None or v < 0 else v)
     yield force
-    _lib.call("qd_gemm_force", -1)
+    kernels.force_gemm(None)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 114)) + [200, 201, 300, 301, 302])
@@ -501,3 +504,22 @@ def test_conv_halo_kernel(variant, forced_gemm, dev):
             assert_fp16_close(got, pre, ulps=2.0, atol=1e-3)
         # amax is of the pre-residual output (the conv output the reference fake-quantizes)
         assert torch.allclose(amax.view(n, cout).cpu(), pre.abs().amax(dim=(2, 3)), rtol=2e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 100, 106, 300, 301])
+def test_linear_gelu_tanh_epilogue(variant, forced_gemm, dev):
+    """SD3 FeedForward net.0: half(gelu_tanh(half(x W^T + b))) fused into the GEMM epilogue (also
+    through the split-K reduce: K = 4096 at small M)."""
+    k = K()
+    forced_gemm(variant)
+    g = torch.Generator().manual_seed(17)
+    for M, N, Kd in ((300, 640, 320), (64, 512, 4096), (1024, 1280, 640)):
+        x = torch.randn(M, Kd, generator=g).half()
+        w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half()
+        b = torch.randn(N, generator=g).half()
+        y = k.linear(x.to(dev), w.to(dev), "f16", bias=b.to(dev), gelu_tanh=True).cpu().float()
+        pre = (x.float() @ w.float().t() + b.float()).half()
+        ref = F.gelu(pre.float(), approximate="tanh").half().float()
+        # a 1-ulp move of the pre-activation propagates through gelu' <= 1.13
+        tol = 1.13 * ulp16(pre.float()) + ulp16(ref) + 1e-3
+        assert ((y - ref).abs() <= tol).all(), (variant, M, N, Kd, (y - ref).abs().max())
