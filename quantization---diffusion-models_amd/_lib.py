@@ -11,6 +11,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libqdiff.so")
+# A/B timing of two builds on one box (scripts/ab.sh) points this at a second in-tree build
+LIB_PATH = os.environ.get("QD_LIB_PATH", LIB_PATH)
 
 P = ctypes.c_void_p
 I = ctypes.c_int

@@ -10,6 +10,8 @@
 // Linear outputs as they are), so no head split/merge copies exist.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace qd;
 
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -197,15 +199,21 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
     f16x8 pf[NQ][2];
 #pragma unroll
     for (int g = 0; g < NQ; ++g) {
+      // 16 scores -> one max: 8 three-input maxes (hipcc does not form v_max3_f32 from the chain)
       float mx = sacc[g][0][0];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sacc[g][j][r]);
+      for (int e = 1; e < 16; e += 2) {
+        const float a = sacc[g][e >> 2][e & 3], b = e + 1 < 16 ? sacc[g][(e + 1) >> 2][(e + 1) & 3] : a;
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mx) : "v"(mx), "v"(a), "v"(b));
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(mrow[g], mx * scale_log2);
-      if (__any(mnew > mrow[g])) {  // wave-uniform: lanes whose max did not grow get alpha = 1
+      // deferred rescale: the running max is only moved when some lane's max grew by more than
+      // 8 (log2 domain), so P stays <= 2^8 (exact in fp16's range, same relative rounding) and
+      // the O / denominator rescale is skipped on almost every tile after the first.  The
+      // decision precedes this tile's exponentials, so nothing at the old scale is pending.
+      if (__any(mnew > mrow[g] + 8.0f)) {  // wave-uniform; lanes that did not grow get alpha = 1
         const float alpha = __builtin_amdgcn_exp2f(mrow[g] - mnew);
 #pragma unroll
         for (int j = 0; j < TD; ++j) oacc[g][j] *= alpha;
@@ -294,6 +302,26 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, hipStream_t st) {
   constexpr int NB = DP <= 96 ? 2 : 1;
   const float sl2 = scale * 1.4426950408889634f;
+  // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1); unset: heuristic
+  static const int forced = [] {
+    const char* e = getenv("QD_ATTN_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1) {
+    k_attn<DP, DV, NB, 8, 2><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+    return;
+  }
+  if (forced == 2) {
+    k_attn<DP, DV, NB, 8, 1><<<((sq + 127) / 128) * b * heads, 512, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+    return;
+  }
+  if (forced == 3) {
+    k_attn<DP, DV, NB, 4, 1><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+    return;
+  }
   // long sequences: 8 waves x 2 query groups (256 queries) share each staged K/V tile while the
   // grid still holds >= 2 blocks per CU; then 8 x 1 (128 queries); 4 x 1 on short ones
   if (sq >= 512 && DP <= 96 && (long)((sq + 255) / 256) * b * heads >= 512) {

@@ -101,10 +101,14 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)
 // exact-erf GELU as torch's F.gelu(approximate='none')
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
-// tanh-approximate GELU as torch's F.gelu(approximate='tanh') (fp32 opmath)
+// tanh-approximate GELU, torch's F.gelu(approximate='tanh') = 0.5 x (1 + tanh(u)),
+// u = sqrt(2/pi) (x + 0.044715 x^3), evaluated as the identical x / (1 + exp(-2u)): one hardware
+// exp + one reciprocal instead of the library tanhf (fp32 result within a few ulp, so the fp16
+// output equals torch's except when the value sits within ~1e-6 of an fp16 rounding boundary).
+// exp(-2u) -> inf for x << 0 gives -0, as torch; exp -> 0 for x >> 0 gives x.
 __device__ __forceinline__ float gelu_tanh_f(float x) {
-  const float inner = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.0f + tanhf(inner));
+  const float u = 0.7978845608028654f * fmaf(0.044715f * x, x * x, x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * u));
 }
 
 }  // namespace qd

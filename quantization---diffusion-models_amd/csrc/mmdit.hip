@@ -192,18 +192,14 @@ extern "C" int qd_rmsnorm_heads(void* x, long rows, int heads, int d, int ld, lo
 }
 
 // ---------------------------------------------------------------------------------------
-// torch gelu(approximate="tanh"): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))), fp32 opmath
+// torch gelu(approximate="tanh"): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))) (common.h)
 __global__ void k_gelu_tanh(const f16* __restrict__ x, f16* __restrict__ y, long n8) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
   if (e >= n8) return;
   const f16x8 v = reinterpret_cast<const f16x8*>(x)[e];
   f16x8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float a = (float)v[j];
-    const float inner = 0.7978845608028654f * (a + 0.044715f * a * a * a);
-    o[j] = (f16)(0.5f * a * (1.0f + tanhf(inner)));
-  }
+  for (int j = 0; j < 8; ++j) o[j] = (f16)gelu_tanh_f((float)v[j]);
   reinterpret_cast<f16x8*>(y)[e] = o;
 }
 

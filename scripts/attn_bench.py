@@ -1,0 +1,26 @@
+"""Attention kernel timing on the path's shapes (HIP events), for configuration sweeps:
+QD_ATTN_CFG=1|2|3 python scripts/attn_bench.py"""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import qdiff_boot  # noqa
+from qdiff import kernels as K
+
+dev = "cuda:0"
+for (b, s, skv, heads, d, ld) in ((8, 4096, 4096, 8, 40, 960), (8, 1024, 1024, 10, 64, 1920), (2, 4429, 4429, 38, 64, 7296),
+                                  (8, 4096, 77, 8, 40, 320)):
+    c = heads * d
+    x = torch.randn(b, s, ld, device=dev).half()
+    kv = torch.randn(b, skv, ld, device=dev).half()
+    q, k, v = x[:, :, :c], kv[:, :, c:2 * c] if ld >= 2 * c else kv[:, :, :c], kv[:, :, ld - c:]
+    for _ in range(3):
+        K.attention(q, k, v, heads)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        K.attention(q, k, v, heads)
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / 10 * 1e3
+    fl = 4.0 * b * heads * s * skv * d
+    print(f"cfg={os.environ.get('QD_ATTN_CFG', '-')} b={b} sq={s} skv={skv} h={heads} d={d}: {us:.1f} us  {fl / us / 1e6:.0f} TFLOP/s", flush=True)
