@@ -188,7 +188,8 @@ int qd_attention(const void* q, int ldq, const void* k, int ldk, const void* v, 
 
 /* ---------------- time embedding / scheduler ---------------------------------------- */
 /* diffusers Timesteps(dim, flip_sin_to_cos, downscale_freq_shift) on timesteps[step_idx[0]]
- * for b rows: out[b, dim] fp16. `timesteps` fp32 device array, `step_idx` int32 device scalar. */
+ * for b rows: out[b, dim] fp16. `timesteps` fp32 device array, `step_idx` int32 device scalar.
+ * flip_sin_to_cos | 2: row r embeds timesteps[r] instead (SDXL add_time_proj of the time_ids). */
 int qd_timestep_embedding(const float* timesteps, const int* step_idx, int b, int dim,
                           int flip_sin_to_cos, float shift, void* out, void* stream);
 /* CFG + DDIM step (eta = 0) on fp16 latents [B, L]: eps = u + g*(c - u) from the UNet output
@@ -199,6 +200,17 @@ int qd_timestep_embedding(const float* timesteps, const int* step_idx, int b, in
 int qd_cfg_ddim_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
                      const float* alpha_t, const float* alpha_prev, int* step_idx,
                      void* next_in, int c, int c_pad, void* stream);
+/* CFG + EulerDiscreteScheduler.step (epsilon, s_churn 0; the SDXL pipeline's scheduler) on fp16
+ * latents [B, L]: sample in fp32, x0 = x - sigma*eps, x += (x - x0)/sigma * (sigma_next - sigma);
+ * writes the next UNet input [2B, L] = latents / dscale[i + 1] (scale_model_input).  sigmas,
+ * dscale fp32 [steps + 1]; step index read from and incremented in `step_idx`. */
+int qd_cfg_euler_discrete_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
+                               const float* sigmas, const float* dscale, int* step_idx, void* next_in, int c,
+                               int c_pad, void* stream);
+/* latents = half(latents * mul); next_in[0..n) = next_in[n..2n) = half(latents / div) when
+ * next_in != NULL (EulerDiscrete init_noise_sigma scaling + the first scale_model_input). */
+int qd_scale_latents(void* latents, int64_t n, float mul, float div, void* next_in, int c, int c_pad,
+                     void* stream);
 
 /* ---------------- calibration (SmoothQuant) ------------------------------------------ */
 /* Mean_Max_Activation_Hook (utils/calib_data.py:105-124): per-channel max |x| of x[rows, C]

@@ -218,15 +218,29 @@ class RefUNet:
         t = self.cfg.get("transformer_layers_per_block", 1)
         return t[i] if isinstance(t, (list, tuple)) else t
 
+    def add_embeds(self, text_embeds, time_ids):
+        """SDXL "text_time" conditioning input (UNet2DConditionModel.get_aug_embed): Timesteps of
+        the flattened time_ids (fp32), reshaped per sample, concatenated after the pooled text
+        embeddings (fp16 | fp32 -> fp32) and cast to fp16."""
+        cfg = self.cfg
+        te = timestep_embedding(time_ids.flatten().float(), cfg["addition_time_embed_dim"],
+                                cfg.get("flip_sin_to_cos", True), cfg.get("freq_shift", 0))
+        te = te.reshape(text_embeds.shape[0], -1)
+        return torch.cat([text_embeds, te], dim=-1).to(F16)
+
     @torch.no_grad()
-    def forward(self, x, t, ctx):
-        """x [2B, 4, h, w] fp16, t int timestep, ctx [2B, S, D] fp16 -> eps [2B, 4, h, w] fp16."""
+    def forward(self, x, t, ctx, add_emb=None):
+        """x [2B, 4, h, w] fp16, t timestep (int; float for the Euler scheduler), ctx [2B, S, D]
+        fp16, add_emb [2B, P] fp16 (SDXL add_embeds) -> eps [2B, 4, h, w] fp16."""
         cfg = self.cfg
         ch = cfg["block_out_channels"]
         b = x.shape[0]
-        temb = timestep_embedding(torch.full((b,), t, dtype=torch.int64), ch[0], cfg.get("flip_sin_to_cos", True),
-                                  cfg.get("freq_shift", 0)).to(F16)
+        tt = torch.full((b,), t, dtype=torch.float32 if isinstance(t, float) else torch.int64)
+        temb = timestep_embedding(tt, ch[0], cfg.get("flip_sin_to_cos", True), cfg.get("freq_shift", 0)).to(F16)
         temb = self.lin("time_embedding.linear_2", F.silu(self.lin("time_embedding.linear_1", temb)))
+        if cfg.get("addition_embed_type") == "text_time":
+            aug = self.lin("add_embedding.linear_2", F.silu(self.lin("add_embedding.linear_1", add_emb)))
+            temb = temb + aug
         h = self.conv("conv_in", x)
         skips = [h]
         nlev = len(ch)
@@ -279,4 +293,44 @@ def denoise(unet, latents, ctx, timesteps, a_t, a_p, guidance=7.5, steps=None):
         x = torch.cat([lat] * 2)
         eps = unet.forward(x, int(timesteps[i]), ctx)
         lat = ddim_step(eps, i, lat, a_t, a_p, guidance)
+    return lat
+
+
+# ------------------------------------------------------------------ Euler discrete (SDXL)
+def euler_tables(num_inference_steps, num_train=1000, beta_start=0.00085, beta_end=0.012, steps_offset=1):
+    """EulerDiscreteScheduler.set_timesteps ("leading", linear interpolation): (timesteps f32,
+    sigmas f32 [S + 1], init_noise_sigma 0-d f32)."""
+    betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train, dtype=torch.float32) ** 2
+    ac = torch.cumprod(1.0 - betas, dim=0)
+    ratio = num_train // num_inference_steps
+    ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.float32) + steps_offset
+    sig = np.array(((1 - ac) / ac) ** 0.5)
+    sig = np.interp(ts, np.arange(0, len(sig)), sig)
+    sigmas = torch.from_numpy(np.concatenate([sig, [0.0]]).astype(np.float32))
+    return torch.from_numpy(ts), sigmas, (sigmas.max() ** 2 + 1) ** 0.5
+
+
+def euler_step(eps_cfg_in, i, latents, sigmas, guidance):
+    """CFG + EulerDiscreteScheduler.step (epsilon, s_churn 0) in diffusers' op order."""
+    u, c = eps_cfg_in.chunk(2)
+    eps = u + guidance * (c - u)
+    sample = latents.to(torch.float32)
+    sigma_hat = sigmas[i] * (0.0 + 1)
+    pred = sample - sigma_hat * eps
+    deriv = (sample - pred) / sigma_hat
+    dt = sigmas[i + 1] - sigma_hat
+    return (sample + deriv * dt).to(eps.dtype)
+
+
+@torch.no_grad()
+def denoise_euler(unet, latents, ctx, add_emb, timesteps, sigmas, init_sigma, guidance=5.0, steps=None):
+    """The SDXL pipeline loop on CPU: latents * init_noise_sigma, then per step
+    scale_model_input (/ (sigma ** 2 + 1) ** 0.5), UNet, CFG, Euler step."""
+    lat = latents.to(F16) * init_sigma
+    n = len(timesteps) if steps is None else steps
+    for i in range(n):
+        x = torch.cat([lat] * 2)
+        x = x / ((sigmas[i] ** 2 + 1) ** 0.5)
+        eps = unet.forward(x, float(timesteps[i]), ctx, add_emb)
+        lat = euler_step(eps, i, lat, sigmas, guidance)
     return lat

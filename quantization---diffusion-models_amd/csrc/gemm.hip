@@ -790,12 +790,14 @@ constexpr int pp_lds_halves(int bn) {
   return 4 * (256 + bn) * 32 > 128 * (bn + 8) ? 4 * (256 + bn) * 32 : 128 * (bn + 8);
 }
 
-template <int BN, int AMODE, bool SPLIT>
+template <int BN, int WGM, int AMODE, bool SPLIT>
 __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   constexpr int BM = 256, BK = 32, NT = 512;
-  constexpr int WN = BN / 4, TN = WN / 16, TM = 8;
+  constexpr int WGN = 8 / WGM;                      // wave grid WGM x WGN (2x4 or 4x2)
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 16, TN = WN / 16, TH = TM / 2;  // TH m-frags per phase
   constexpr int ASZ = BM * BK, SSZ = (BM + BN) * BK;
-  static_assert(WN % 16 == 0, "wave tile width");
+  static_assert(WN % 16 == 0 && TM % 2 == 0 && (WGM == 2 || WGM == 4), "wave tile");
   using AL = ADma<BM, NT, AMODE, BK>;
   using BL = BDma<BN, NT, BK>;
   __shared__ __attribute__((aligned(16))) f16 smem[pp_lds_halves(BN)];
@@ -814,8 +816,9 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const int wm0 = wr * 128, wn0 = wc * WN;
+  const int wr = wid / WGN, wc = wid - wr * WGN;
+  const int grp = wid >> 2;  // ping-pong group = M half (waves w and w + 4 share a SIMD)
+  const int wm0 = wr * WM, wn0 = wc * WN;
   const int fr = lane & 15, fq = lane >> 4;
 
   AL al;
@@ -844,19 +847,19 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 runs one barrier behind
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 runs one barrier behind
   asm volatile("" ::: "memory");
 
-  f16x8 af[4], bf[TN];
+  f16x8 af[TH], bf[TN];
   auto mfma_block = [&](int ih) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TH; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[ih * 4 + i][j], 0, 0, 0);
+        acc[ih * TH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[ih * TH + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -873,7 +876,7 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
     f16* nxt = smem + ((kt + 2) & 3) * SSZ;
     // ---- phase a
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + i * 16 + fr, fq));
+    for (int i = 0; i < TH; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + i * 16 + fr, fq));
 #pragma unroll
     for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BK>(wn0 + j * 16 + fr, fq));
     if (pre) al.issue(p, kbeg + (kt + 2) * BK, nxt, wid);
@@ -882,7 +885,8 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
     bar();
     // ---- phase b
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + 64 + i * 16 + fr, fq));
+    for (int i = 0; i < TH; ++i)
+      af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + (TH + i) * 16 + fr, fq));
     if (kt + 1 < nk) {
       if (pre) wait_vm_rt(AL::L);
       else wait_vm<0>();
@@ -892,7 +896,7 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
     mfma_block(1);
     bar();
   }
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -917,12 +921,12 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
     return;
   }
   // epilogue in two 128-row passes (one per wave group) through a [128][BN + 8] fp16 LDS tile:
-  // h = half(acc + bias) -> per-column amax (rows_per_sample % 128 == 0) -> (+GEGLU) (+residual)
+  // h = half(acc + bias) -> per-column amax (rows_per_sample % WM == 0) -> (+GEGLU) (+residual)
   constexpr int LP = BN + 8;
   f16* ct = smem;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    if (wr == pass) {
+    if (grp == pass) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int nl = wn0 + j * 16 + fq * 4;
@@ -933,8 +937,8 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
         float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const int ml = i * 16 + fr;
-          const bool ok = m0 + wm0 + ml < p.M && col_ok;
+          const int ml = wm0 - pass * 128 + i * 16 + fr;  // row within this pass's 128
+          const bool ok = m0 + pass * 128 + ml < p.M && col_ok;
           f16x4 h;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1231,8 +1235,8 @@ static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register
 extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
                  (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
-                 variant == 201 || (variant >= 300 && variant <= 302),
-             "qd_gemm_force: -1, 0..3, 100 + DMA variant, 200/201 halo conv, 300-302 ping-pong");
+                 variant == 201 || (variant >= 300 && variant <= 304),
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant, 200/201 halo conv, 300-304 ping-pong");
   g_force = variant;
   return 0;
 }
@@ -1281,10 +1285,12 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         best.kps = nc / sp;
       }
     }
-  } else if (g_force >= 300 && g_force <= 302 && !quant_w) {
-    // ping-pong 256 x {256, 320, 192} tile: wave rows 128 (amax needs whole-sample wave tiles)
-    const int bnp = g_force == 300 ? 256 : g_force == 301 ? 320 : 192;
-    if (!amax || rows_per_sample % 128 == 0) {
+  } else if (g_force >= 300 && g_force <= 304 && !quant_w) {
+    // ping-pong 256 x {256, 320, 192} tiles (2x4 waves, wave rows 128) and 256 x {160, 128}
+    // (4x2 waves, wave rows 64); amax needs whole-sample wave tiles
+    static const int kBn[] = {256, 320, 192, 160, 128};
+    const int bnp = kBn[g_force - 300];
+    if (!amax || rows_per_sample % (bnp >= 192 ? 128 : 64) == 0) {
       best = {3, 256, bnp, 0, 1, K};
       const long tiles_mn = (long)((M + 255) / 256) * ((N + bnp - 1) / bnp);
       for (int sp = 2; sp <= 32 && !geglu && K % 32 == 0; ++sp) {
@@ -1355,9 +1361,11 @@ template <int AMODE, bool SPLIT>
 static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t st) {
   if (pl.kind == 3) {
     const int nwg = ((p.M + 255) / 256) * ((p.N + pl.bn - 1) / pl.bn) * p.splits;
-    if (pl.bn == 256) k_gemm_pp<256, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
-    else if (pl.bn == 320) k_gemm_pp<320, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
-    else k_gemm_pp<192, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    if (pl.bn == 256) k_gemm_pp<256, 2, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    else if (pl.bn == 320) k_gemm_pp<320, 2, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    else if (pl.bn == 192) k_gemm_pp<192, 2, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    else if (pl.bn == 160) k_gemm_pp<160, 4, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
+    else k_gemm_pp<128, 4, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
   } else if (pl.kind == 2) {
     const int nwg = (p.M / 256) * (p.N / pl.bn) * p.splits;
     if (pl.bn == 160) k_conv_halo<160><<<nwg, 512, 0, st>>>(p);

@@ -660,7 +660,9 @@ __global__ void k_temb(const float* __restrict__ ts, const int* __restrict__ ste
   const int half_dim = dim / 2;
   if (i >= b * half_dim) return;
   const int row = i / half_dim, k = i % half_dim;
-  const float t = ts[step_idx ? step_idx[0] : 0];
+  // flip bit 1: row r embeds ts[r] (SDXL add_time_proj over the flattened time_ids)
+  const float t = (flip & 2) ? ts[row] : ts[step_idx ? step_idx[0] : 0];
+  flip &= 1;
   const float ex = (-9.210340371976184f * (float)k) / ((float)half_dim - shift);  // -ln(1e4)*k/(h-s)
   const float arg = t * expf(ex);
   const float sv = sinf(arg), cv = cosf(arg);
@@ -731,6 +733,85 @@ __global__ void k_cfg_ddim(f16* __restrict__ lat, const f16* __restrict__ uo, in
 }
 
 __global__ void k_step_inc(int* step_idx) { step_idx[0] += 1; }
+
+// ---------------------------------------------------------------------------------------
+// CFG + EulerDiscreteScheduler.step (epsilon prediction, s_churn = 0) and the next step's
+// scale_model_input, in diffusers' op order with the torch-CPU scalar semantics above:
+//   eps   = u + g * (c - u)                                (fp16 ops)
+//   x     = float(latents)                                 (sample.to(float32))
+//   pred  = x - float(half(half(sigma) * eps))             (0-d sigma_hat first operand: fp16)
+//   deriv = (x - pred) / sigma ; prev = x + deriv * (sigma_next - sigma)    (fp32)
+//   lat   = half(prev) ; next_in = half(float(lat) / dscale[i + 1]) for both CFG halves
+// dscale[i] = (sigma_i ** 2 + 1) ** 0.5 (fp32, host table: scale_model_input's divisor).
+// ---------------------------------------------------------------------------------------
+__global__ void k_cfg_euler_discrete(f16* __restrict__ lat, const f16* __restrict__ uo, int b, long l, float g,
+                                     const float* __restrict__ sig, const float* __restrict__ dsc,
+                                     const int* __restrict__ step_idx, f16* __restrict__ next_in, int c, int cp) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)b * l) return;
+  const int ch = e % cp;
+  const int si = step_idx[0];
+  f16 out = (f16)0.f;
+  if (ch < c) {
+    const long bi = e / l, off = e % l;
+    const float u = (float)uo[bi * l + off];
+    const float cc = (float)uo[((long)b + bi) * l + off];
+    const f16 diff = (f16)(cc - u);
+    const f16 gd = (f16)(g * (float)diff);
+    const f16 eps = (f16)(u + (float)gd);
+    const float sigma = sig[si];
+    const float x = (float)lat[e];
+    const float pred = x - (float)(f16)((float)(f16)sigma * (float)eps);
+    const float deriv = (x - pred) / sigma;
+    const float prev = x + deriv * (sig[si + 1] - sigma);
+    out = (f16)prev;
+  }
+  lat[e] = out;
+  if (next_in) {
+    const f16 sc = ch < c ? (f16)((float)out / dsc[si + 1]) : (f16)0.f;
+    next_in[e] = sc;
+    next_in[(long)b * l + e] = sc;
+  }
+}
+
+extern "C" int qd_cfg_euler_discrete_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
+                                          const float* sigmas, const float* dscale, int* step_idx, void* next_in,
+                                          int c, int c_pad, void* stream) {
+  QD_REQUIRE(latents && unet_out && sigmas && dscale && step_idx, "null pointer");
+  QD_REQUIRE(c_pad >= c && l % c_pad == 0, "bad channel padding");
+  hipStream_t st = S(stream);
+  k_cfg_euler_discrete<<<grid1((long)b * l), 256, 0, st>>>((f16*)latents, (const f16*)unet_out, b, l, guidance,
+                                                           sigmas, dscale, step_idx, (f16*)next_in, c, c_pad);
+  k_step_inc<<<1, 1, 0, st>>>(step_idx);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// x = half(float(x) * mul) then (optional) y = half(float(x) / div) into both CFG halves of y:
+// EulerDiscrete prepare_latents (latents * init_noise_sigma, a 0-d fp32 second operand) and the
+// first step's scale_model_input.  Channels >= c (padding) stay zero.
+__global__ void k_scale_latents(f16* __restrict__ x, long n, float mul, float div, long half_off,
+                                f16* __restrict__ y, int c, int cp) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const bool ok = (e % cp) < c;
+  const f16 v = ok ? (f16)((float)x[e] * mul) : (f16)0.f;
+  x[e] = v;
+  if (y) {
+    const f16 s = ok ? (f16)((float)v / div) : (f16)0.f;
+    y[e] = s;
+    y[half_off + e] = s;
+  }
+}
+
+extern "C" int qd_scale_latents(void* latents, int64_t n, float mul, float div, void* next_in, int c, int c_pad,
+                                void* stream) {
+  QD_REQUIRE(latents && c_pad >= c && n % c_pad == 0, "bad args");
+  if (n == 0) return 0;
+  k_scale_latents<<<grid1(n), 256, 0, S(stream)>>>((f16*)latents, n, mul, div, n, (f16*)next_in, c, c_pad);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int qd_cfg_ddim_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
                                 const float* alpha_t, const float* alpha_prev, int* step_idx,

@@ -162,7 +162,7 @@ def conv_weight_khwc(w, ci_pad):
 # candidates reduce fixed-order fp32 slabs (deterministic for a given choice).
 # QD_GEMM_TUNE=0 disables the search (library planner only).
 REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
-DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 300, 301, 302)  # LDS-DMA variants (fp16 weights; 3xx ping-pong 256-row)
+DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 300, 301, 302, 303, 304)  # LDS-DMA variants (fp16 weights; 3xx ping-pong 256-row)
 HALO_VARIANTS = (200, 201)  # 3x3 conv with the activation halo staged once per channel chunk
 _TUNE = {}
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
@@ -475,10 +475,12 @@ def attention(q, k, v, heads, out=None, b=None):
     return out
 
 
-def timestep_embedding(timesteps_f32, step_idx, b, dim, flip_sin_to_cos=True, shift=0.0, out=None):
+def timestep_embedding(timesteps_f32, step_idx, b, dim, flip_sin_to_cos=True, shift=0.0, out=None, per_row=False):
+    """per_row: row r embeds timesteps_f32[r] (b values) instead of timesteps_f32[step_idx]."""
     o = out if out is not None else _empty((b, dim), torch.float16, timesteps_f32.device)
-    _lib.call("qd_timestep_embedding", _p(timesteps_f32), _p(step_idx), b, dim, 1 if flip_sin_to_cos else 0,
-              float(shift), _p(o), _stream())
+    flags = (1 if flip_sin_to_cos else 0) | (2 if per_row else 0)
+    _lib.call("qd_timestep_embedding", _p(timesteps_f32), _p(step_idx), b, dim, flags, float(shift), _p(o),
+              _stream())
     return o
 
 
@@ -592,6 +594,28 @@ def cfg_euler_step(latents, model_out, guidance, sigmas, step_idx, next_in=None)
         raise ValueError("model output must be [2B, ...] of the latents' shape")
     _lib.call("qd_cfg_euler_step", _p(latents), _p(model_out), b, l, float(guidance), _p(sigmas), _p(step_idx),
               _p(next_in), _stream())
+    return latents
+
+
+def cfg_euler_discrete_step(latents, unet_out, guidance, sigmas, dscale, step_idx, next_in=None, c=None):
+    """CFG + EulerDiscreteScheduler.step; latents NHWC [B, H, W, Cp] updated in place, next_in
+    receives the next step's scale_model_input of them (both CFG halves)."""
+    _chk(latents, "latents")
+    _chk(unet_out, "unet_out")
+    b = latents.shape[0]
+    cp = latents.shape[-1]
+    l = latents.numel() // b
+    _lib.call("qd_cfg_euler_discrete_step", _p(latents), _p(unet_out), b, l, float(guidance), _p(sigmas),
+              _p(dscale), _p(step_idx), _p(next_in), c or cp, cp, _stream())
+    return latents
+
+
+def scale_latents(latents, mul, div=None, next_in=None, c=None):
+    """latents = half(latents * mul); next_in = [half(latents / div)] * 2 (NHWC, Cp channels)."""
+    _chk(latents, "latents")
+    cp = latents.shape[-1]
+    _lib.call("qd_scale_latents", _p(latents), latents.numel(), float(mul), float(div or 1.0), _p(next_in),
+              c or cp, cp, _stream())
     return latents
 
 

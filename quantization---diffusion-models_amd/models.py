@@ -15,7 +15,7 @@ import torch
 
 from .base import QUANTISABLE_COMPONENTS, BaseAWQForDiffusion
 from .calib import synthetic_calibration_set
-from .pipeline import FlowMatchDenoiseLoop, synthetic_text_embeddings
+from .pipeline import EulerDiscreteDenoiseLoop, FlowMatchDenoiseLoop, synthetic_text_embeddings
 from .pipeline_io import load_config
 from .unet import BasicTransformerBlock
 
@@ -134,12 +134,73 @@ class StableDiffusion1_x(_DiffusionAdapter):
 
 
 class StableDiffusionXL(_DiffusionAdapter):
+    """SDXL adapter (models/StableDiffusionXL.py); generate() drives diffusers'
+    StableDiffusionXLPipeline loop - EulerDiscreteScheduler, guidance 5.0, the "text_time"
+    additional conditioning (pooled text embeddings + time_ids) - on device."""
+
     def checkQuantStatus(self, quantUnet=True, quantTextEncoder=False, quantVAE=False, quantTransformer=True):
         if quantTransformer:
             raise Exception("There is no Transformer in this Diffusion Model")
 
     def get_quantized_components(self):
         return self.quantizable_components
+
+    def _xl_conditioning(self, prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
+                         pooled_prompt_embeds, negative_pooled_prompt_embeds, height, width, original_size,
+                         crops_coords_top_left, target_size):
+        cfg = self.pipeline.unet.config
+        dev = self.pipeline.device
+        pooled_dim = cfg.projection_class_embeddings_input_dim - 6 * cfg.addition_time_embed_dim
+        ctx = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds)
+        b = ctx.shape[0] // 2
+        if pooled_prompt_embeds is None:
+            prompts = [prompt] * b if isinstance(prompt, str) else list(prompt or [f"prompt{i}" for i in range(b)])
+            pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in prompts], seq_len=1,
+                                                             dim=pooled_dim, device=dev)[:, 0]
+        if negative_pooled_prompt_embeds is None:
+            neg = negative_prompt if negative_prompt is not None else ""
+            negs = [neg] * b if isinstance(neg, str) else list(neg)
+            negative_pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in negs], seq_len=1,
+                                                                      dim=pooled_dim, device=dev)[:, 0]
+        text = torch.cat([negative_pooled_prompt_embeds.to(dev), pooled_prompt_embeds.to(dev)]).to(torch.float16)
+        # StableDiffusionXLPipeline._get_add_time_ids: original_size + crops_coords_top_left + target_size
+        ids = list(original_size or (height, width)) + list(crops_coords_top_left) + list(target_size or (height, width))
+        time_ids = torch.tensor([ids] * (2 * b), dtype=torch.float32)
+        return ctx, text.contiguous(), time_ids
+
+    def get_loop(self, batch, height, width, steps, guidance, use_graph=True):
+        key = (batch, height, width, steps, float(guidance), use_graph)
+        if key not in self._loops:
+            self._loops[key] = EulerDiscreteDenoiseLoop(self.pipeline.unet, batch, height, width, steps, guidance,
+                                                        device=self.pipeline.device, use_graph=use_graph,
+                                                        sched_cfg=self.pipeline.scheduler_config)
+        return self._loops[key]
+
+    @torch.no_grad()
+    def generate(self, prompt=None, height=1024, width=1024, num_inference_steps=50, guidance_scale=5.0,
+                 negative_prompt=None, num_images_per_prompt=1, generator=None, device="cpu", lat=None,
+                 output_type=None, prompt_embeds=None, negative_prompt_embeds=None, pooled_prompt_embeds=None,
+                 negative_pooled_prompt_embeds=None, original_size=None, crops_coords_top_left=(0, 0),
+                 target_size=None, use_graph=True, **kwargs):
+        """base.py:828-850 for StableDiffusionXLPipeline (its default guidance 5.0; the reference
+        passes 50 steps) -> the device Euler-discrete loop; returns latents [B, 4, h, w] fp16."""
+        if self.pipeline is None:
+            raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
+        if output_type not in (None, "latent"):
+            raise NotImplementedError("VAE decoding is not part of this build (SURVEY.md §8f); use output_type='latent'")
+        ctx, text, time_ids = self._xl_conditioning(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
+                                                    pooled_prompt_embeds, negative_pooled_prompt_embeds, height, width,
+                                                    original_size, crops_coords_top_left, target_size)
+        if num_images_per_prompt > 1:
+            b0, r = ctx.shape[0] // 2, num_images_per_prompt
+            rep = lambda t: torch.cat([t[:b0].repeat_interleave(r, 0), t[b0:].repeat_interleave(r, 0)])
+            ctx, text, time_ids = rep(ctx), rep(text), rep(time_ids)
+        b = ctx.shape[0] // 2
+        cin = self.pipeline.unet.config.in_channels
+        if lat is None:
+            lat = torch.randn((b, cin, height // 8, width // 8), generator=generator, dtype=torch.float32).to(torch.float16)
+        loop = self.get_loop(b, height, width, num_inference_steps, guidance_scale, use_graph)
+        return loop.run(lat.to(self.pipeline.device), ctx, text, time_ids)
 
 
 class StableDiffusion3_5(_DiffusionAdapter):

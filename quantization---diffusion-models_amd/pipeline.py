@@ -15,7 +15,8 @@ import torch
 
 from . import arena as A
 from . import kernels as K
-from .scheduler import DDIMConfig, FlowMatchConfig, ddim_tables, flowmatch_tables
+from .scheduler import (DDIMConfig, EulerDiscreteConfig, FlowMatchConfig, ddim_tables, euler_discrete_tables,
+                        flowmatch_tables)
 
 C_PAD = 8
 
@@ -211,6 +212,89 @@ class FlowMatchDenoiseLoop(DenoiseLoop):
             self.capture()
             if latents is not None:
                 self.set_inputs(latents, ctx, pooled)
+        for _ in range(self.steps):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.step()
+        return self.latents_nchw()
+
+
+class EulerDiscreteDenoiseLoop(DenoiseLoop):
+    """The SDXL loop (diffusers StableDiffusionXLPipeline.__call__ with its EulerDiscreteScheduler):
+    latents * init_noise_sigma, then per step scale_model_input (x / sqrt(sigma^2 + 1)) ->
+    UNet(x, t, prompt_embeds, added_cond_kwargs={text_embeds, time_ids}) -> CFG -> Euler step.
+    The additional "text_time" embedding input [text_embeds | Timesteps(time_ids)] is
+    step-invariant and built once per generate on device."""
+
+    def __init__(self, unet, batch, height=1024, width=1024, num_inference_steps=50, guidance_scale=5.0,
+                 device="cuda", use_graph=True, sched_cfg=EulerDiscreteConfig(), ctx_len=77):
+        super().__init__(unet, batch, height, width, num_inference_steps, guidance_scale, device, use_graph,
+                         sched_cfg, ctx_len)
+        cfg = unet.config
+        if cfg.addition_embed_type != "text_time":
+            raise ValueError("the SDXL loop needs a UNet with addition_embed_type='text_time'")
+        ts, sig, dsc, init = euler_discrete_tables(num_inference_steps, sched_cfg)
+        self.timesteps = ts
+        self.ts_f32 = ts.to(self.device)
+        self.sigmas = sig.to(self.device)
+        self.dscale = dsc.to(self.device)
+        self.dscale0 = float(dsc[0])
+        self.init_sigma = float(init)
+        self.time_dim = cfg.addition_time_embed_dim
+        self.text_dim = cfg.projection_class_embeddings_input_dim - 6 * self.time_dim
+        f16 = dict(dtype=torch.float16, device=self.device)
+        self.add_emb = torch.zeros(2 * batch, cfg.projection_class_embeddings_input_dim, **f16)
+
+    @torch.no_grad()
+    def set_inputs(self, latents, ctx, text_embeds=None, time_ids=None):
+        """latents [B, 4, h, w]; ctx [2B, 77, D]; text_embeds [2B, pooled dim]; time_ids [2B, 6]
+        (uncond first, as diffusers concatenates them)."""
+        if latents.shape != (self.B, self.cin, self.h, self.w):
+            raise ValueError(f"latents must be {(self.B, self.cin, self.h, self.w)}, got {tuple(latents.shape)}")
+        if ctx.shape != self.ctx.shape:
+            raise ValueError(f"context must be {tuple(self.ctx.shape)}, got {tuple(ctx.shape)}")
+        if text_embeds is None or tuple(text_embeds.shape) != (2 * self.B, self.text_dim):
+            raise ValueError(f"text_embeds must be {(2 * self.B, self.text_dim)}")
+        if time_ids is None or tuple(time_ids.shape) != (2 * self.B, 6):
+            raise ValueError(f"time_ids must be {(2 * self.B, 6)}")
+        lat = latents.to(device=self.device, dtype=torch.float16).contiguous()
+        K.nchw_to_nhwc(lat, C_PAD, out=self.lat)
+        K.scale_latents(self.lat, self.init_sigma, self.dscale0, next_in=self.next_in, c=self.cin)
+        self.ctx.copy_(ctx)
+        tid = time_ids.to(device=self.device, dtype=torch.float32).reshape(-1).contiguous()
+        temb = K.timestep_embedding(tid, None, tid.numel(), self.time_dim, flip_sin_to_cos=self.unet.config.flip_sin_to_cos,
+                                    shift=float(self.unet.config.freq_shift), per_row=True)
+        te = text_embeds.to(device=self.device, dtype=torch.float16).contiguous()
+        K.concat_c(te, temb.view(2 * self.B, 6 * self.time_dim), out=self.add_emb)
+        self.step_idx.zero_()
+        fresh = self.unet.prepare_context(self.ctx)
+        if self.ctx_kv is None:
+            self.ctx_kv = fresh
+        else:
+            for key, (k, v) in fresh.items():
+                self.ctx_kv[key][0].copy_(k)
+                self.ctx_kv[key][1].copy_(v)
+
+    @torch.no_grad()
+    def step(self, frozen=False):
+        with A.using(self.arena, frozen=frozen):
+            K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
+                                 shift=float(self.unet.config.freq_shift), out=self.temb_in)
+            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv, add_emb_in=self.add_emb)
+            K.cfg_euler_discrete_step(self.lat, out, self.guidance, self.sigmas, self.dscale, self.step_idx,
+                                      self.next_in, c=self.cin)
+        self.last_out = out
+        return out
+
+    @torch.no_grad()
+    def run(self, latents=None, ctx=None, text_embeds=None, time_ids=None):
+        if latents is not None:
+            self.set_inputs(latents, ctx, text_embeds, time_ids)
+        if self.use_graph and self.graph is None:
+            self.capture()
+            if latents is not None:
+                self.set_inputs(latents, ctx, text_embeds, time_ids)
         for _ in range(self.steps):
             if self.graph is not None:
                 self.graph.replay()

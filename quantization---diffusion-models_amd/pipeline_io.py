@@ -6,8 +6,8 @@ contain 'unet' / 'text_encoder' / 'vae' / 'transformer', StableDiffusion1_x.py:1
 StableDiffusion3_5.py:17-31), ``to(device)`` and ``save_pretrained``.  Weights load from a local
 diffusers directory (``model_index.json`` + ``unet/`` or ``transformer/`` ``config.json`` +
 ``diffusion_pytorch_model.safetensors``) - there is no network - or are synthesized
-(``synthetic:sd15`` / ``synthetic:sdxl`` / ``synthetic:tiny`` / ``synthetic:sd35`` /
-``synthetic:sd35-tiny``) with the real shapes and N(0, 1/fan_in) values.
+(``synthetic:sd15`` / ``synthetic:sdxl`` / ``synthetic:tiny`` / ``synthetic:sdxl-tiny`` /
+``synthetic:sd35`` / ``synthetic:sd35-tiny``) with the real shapes and N(0, 1/fan_in) values.
 """
 import json
 import os
@@ -15,13 +15,14 @@ import os
 import torch
 
 from .mmdit import SD35_LARGE, MMDiTConfig, SD3Transformer2DModel, tiny_mmdit_config
-from .scheduler import DDIMConfig, FlowMatchConfig
-from .unet import SD15, SDXL, UNet2DConditionModel, UNetConfig, tiny_config
+from .scheduler import DDIMConfig, EulerDiscreteConfig, FlowMatchConfig
+from .unet import SD15, SDXL, UNet2DConditionModel, UNetConfig, tiny_config, tiny_sdxl_config
 
 SYNTHETIC = {
     "synthetic:sd15": ("StableDiffusionPipeline", SD15),
     "synthetic:sdxl": ("StableDiffusionXLPipeline", SDXL),
     "synthetic:tiny": ("StableDiffusionPipeline", None),
+    "synthetic:sdxl-tiny": ("StableDiffusionXLPipeline", None),
     "synthetic:sd35": ("StableDiffusion3Pipeline", SD35_LARGE),
     "synthetic:sd35-tiny": ("StableDiffusion3Pipeline", None),
 }
@@ -38,7 +39,8 @@ class QDiffPipeline:
         self.text_encoder = text_encoder
         self.vae = vae
         if scheduler_config is None:
-            scheduler_config = FlowMatchConfig() if transformer is not None else DDIMConfig()
+            scheduler_config = (FlowMatchConfig() if transformer is not None else
+                                EulerDiscreteConfig() if class_name == "StableDiffusionXLPipeline" else DDIMConfig())
         self.scheduler_config = scheduler_config
         self.class_name = class_name
         self.config = config or {"_class_name": class_name}
@@ -68,7 +70,8 @@ class QDiffPipeline:
         name = self.denoiser_name
         os.makedirs(os.path.join(save_dir, name), exist_ok=True)
         if name == "unet":
-            index = {"unet": ["diffusers", "UNet2DConditionModel"], "scheduler": ["diffusers", "DDIMScheduler"]}
+            sched = "EulerDiscreteScheduler" if self.class_name == "StableDiffusionXLPipeline" else "DDIMScheduler"
+            index = {"unet": ["diffusers", "UNet2DConditionModel"], "scheduler": ["diffusers", sched]}
             cls = "UNet2DConditionModel"
         else:
             index = {"transformer": ["diffusers", "SD3Transformer2DModel"],
@@ -110,7 +113,8 @@ def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16):
     cls = cfg["_class_name"]
     mmdit = cls in MMDIT_PIPELINES
     if model_path in SYNTHETIC:
-        mcfg = SYNTHETIC[model_path][1] or (tiny_mmdit_config() if mmdit else tiny_config())
+        mcfg = SYNTHETIC[model_path][1] or (tiny_mmdit_config() if mmdit else
+                                            tiny_sdxl_config() if cls == "StableDiffusionXLPipeline" else tiny_config())
         if mmdit:
             # built and drawn on the target device (a full SD3.5-Large is 8 B parameters)
             with torch.device(device):

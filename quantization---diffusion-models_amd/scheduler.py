@@ -1,5 +1,6 @@
 """Scheduler tables for the device loops: DDIM (diffusers DDIMScheduler, SD1.5
-scheduler_config) and flow-match Euler (FlowMatchEulerDiscreteScheduler, SD3 / SD3.5).
+scheduler_config), Euler discrete (EulerDiscreteScheduler, the SDXL base scheduler_config) and
+flow-match Euler (FlowMatchEulerDiscreteScheduler, SD3 / SD3.5).
 
 Only the per-step constants are computed here (host setup, as diffusers does); the step itself
 is the fused ``qd_cfg_ddim_step`` kernel.  SD1.5 config: beta_start 0.00085, beta_end 0.012,
@@ -63,3 +64,26 @@ def ddim_tables(num_inference_steps, cfg: DDIMConfig = DDIMConfig()):
     a_t = torch.stack([ac[int(t)] for t in ts])
     a_p = torch.stack([ac[int(t) - ratio] if int(t) - ratio >= 0 else final for t in ts])
     return torch.from_numpy(ts), a_t.float(), a_p.float()
+
+
+@dataclass
+class EulerDiscreteConfig(DDIMConfig):
+    """EulerDiscreteScheduler of the SDXL base pipeline: the SD1.5 beta schedule, "leading"
+    timestep spacing with steps_offset 1, epsilon prediction, linear sigma interpolation."""
+
+
+def euler_discrete_tables(num_inference_steps, cfg: EulerDiscreteConfig = EulerDiscreteConfig()):
+    """(timesteps f32 [S], sigmas f32 [S + 1], dscale f32 [S + 1], init_noise_sigma) of
+    EulerDiscreteScheduler.set_timesteps: sigma(t) = sqrt((1 - acp) / acp) at the leading-spaced
+    timesteps (np.interp at integer t), a trailing 0; dscale = (sigma ** 2 + 1) ** 0.5 is
+    scale_model_input's divisor; init_noise_sigma = (max sigma ** 2 + 1) ** 0.5 ("leading")."""
+    ac = alphas_cumprod(cfg)
+    ratio = cfg.num_train_timesteps // num_inference_steps
+    ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.float32)
+    ts += cfg.steps_offset
+    sig_all = np.array(((1 - ac) / ac) ** 0.5)
+    sig = np.interp(ts, np.arange(0, len(sig_all)), sig_all)
+    sigmas = torch.from_numpy(np.concatenate([sig, [0.0]]).astype(np.float32))
+    dscale = (sigmas ** 2 + 1) ** 0.5
+    init = (sigmas.max() ** 2 + 1) ** 0.5
+    return torch.from_numpy(ts), sigmas, dscale, init

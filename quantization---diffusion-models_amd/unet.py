@@ -90,6 +90,19 @@ def tiny_config(**kw):
     return UNetConfig(**base)
 
 
+def tiny_sdxl_config(**kw):
+    """A small SDXL-shaped config for parity tests: no attention at the top level, linear
+    proj_in / proj_out, a 2-deep transformer stack, per-level heads, and the "text_time"
+    additional embedding (pooled text 64 + 6 time ids x 32)."""
+    base = dict(block_out_channels=(64, 128), down_block_types=("DownBlock2D", "CrossAttnDownBlock2D"),
+                up_block_types=("CrossAttnUpBlock2D", "UpBlock2D"), cross_attention_dim=64,
+                attention_head_dim=(2, 4), transformer_layers_per_block=(1, 2), use_linear_projection=True,
+                sample_size=16, norm_num_groups=32, addition_embed_type="text_time", addition_time_embed_dim=32,
+                projection_class_embeddings_input_dim=64 + 6 * 32)
+    base.update(kw)
+    return UNetConfig(**base)
+
+
 # ------------------------------------------------------------------ module tree (diffusers names)
 class ResnetBlock2D(nn.Module):
     def __init__(self, cin, cout, temb, groups, eps):

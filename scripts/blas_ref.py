@@ -29,7 +29,7 @@ for (m, n, k) in ((8192, 9728, 2432), (8192, 2432, 9728), (4096, 7296, 2432), (3
     w = (torch.randn(n, k, device=dev) / k ** 0.5).half()
     f = 2 * m * n * k
     row = []
-    for v in (100, 101, 103, 106, 109, 300, 301, 302):
+    for v in (100, 101, 103, 106, 109, 300, 301, 302, 303, 304):
         K.force_gemm(v)
         try:
             ms = t(lambda: K.linear(a, w, "f16"))

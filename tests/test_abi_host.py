@@ -164,3 +164,35 @@ def test_pipeline_files_roundtrip(tmp_path):
         assert k == k2 and torch.equal(a, b)
     with pytest.raises(FileNotFoundError):
         load_pipeline(str(tmp_path / "nope"), device="cpu")
+
+
+def test_euler_discrete_tables_match_oracle():
+    from oracle.unet_ref import euler_tables
+    from qdiff.scheduler import euler_discrete_tables
+    for n in (4, 30, 50):
+        ts, sig, dsc, init = euler_discrete_tables(n)
+        ots, osig, oinit = euler_tables(n)
+        assert torch.equal(ts, ots) and torch.equal(sig, osig) and init.item() == oinit.item()
+        assert ts[0].item() == 1000 // n * (n - 1) + 1 and sig[-1].item() == 0.0 and len(sig) == n + 1
+        assert torch.equal(dsc, (osig ** 2 + 1) ** 0.5)
+    # SDXL base at 50 steps: sigma_max = sqrt((1 - acp[981]) / acp[981]) ~ 13.12
+    _, sig, _, init = euler_discrete_tables(50)
+    assert 13.0 < sig[0].item() < 13.3 and abs(init.item() - (sig[0].item() ** 2 + 1) ** 0.5) < 1e-4
+
+
+def test_sdxl_tiny_tree_and_oracle_euler_runs():
+    from oracle.unet_ref import RefUNet, denoise_euler, euler_tables
+    from qdiff.unet import UNet2DConditionModel, tiny_sdxl_config
+    cfg = tiny_sdxl_config()
+    u = UNet2DConditionModel(cfg).half().init_synthetic(0)
+    keys = set(u.state_dict())
+    assert "add_embedding.linear_1.weight" in keys and "down_blocks.1.attentions.0.transformer_blocks.1.ff.net.2.bias" in keys
+    assert u.state_dict()["add_embedding.linear_1.weight"].shape == (256, 64 + 6 * 32)
+    cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(cfg).items()}
+    r = RefUNet(cd, dict(u.state_dict()))
+    g = torch.Generator().manual_seed(0)
+    add = r.add_embeds(torch.randn(2, 64, generator=g).half(), torch.tensor([[128.0, 128, 0, 0, 128, 128]] * 2))
+    ts, sig, init = euler_tables(2)
+    out = denoise_euler(r, torch.randn(1, 4, 16, 16, generator=g).half(), torch.randn(2, 77, 64, generator=g).half(),
+                        add, ts, sig, init)
+    assert out.shape == (1, 4, 16, 16) and torch.isfinite(out.float()).all()

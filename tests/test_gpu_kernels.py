@@ -376,7 +376,7 @@ def forced_gemm():
     kernels.force_gemm(None)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 114)) + [200, 201, 300, 301, 302])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 114)) + [200, 201, 300, 301, 302, 303, 304])
 def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     """Every kernel family / tile (register-staged and LDS-DMA) on ragged shapes: rows past M,
     conv halo, stride 2, fused 2x upsample, the 4-channel conv_in (any-Ci decode), K tails,
@@ -506,7 +506,7 @@ def test_conv_halo_kernel(variant, forced_gemm, dev):
         assert torch.allclose(amax.view(n, cout).cpu(), pre.abs().amax(dim=(2, 3)), rtol=2e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 100, 106, 300, 301])
+@pytest.mark.parametrize("variant", [-1, 0, 100, 106, 300, 301, 303])
 def test_linear_gelu_tanh_epilogue(variant, forced_gemm, dev):
     """SD3 FeedForward net.0: half(gelu_tanh(half(x W^T + b))) fused into the GEMM epilogue (also
     through the split-K reduce: K = 4096 at small M)."""
