@@ -39,14 +39,20 @@ def parse():
     ap.add_argument("--denoise-steps", type=int, default=50)
     ap.add_argument("--mode", default=None, choices=["w8a8-sq", "w8a8", "w4a16", "fp16"],
                     help="default: w8a8-sq (sd15), w4a16 (sd35, SURVEY config C5)")
-    ap.add_argument("--model", default="sd15", choices=["sd15", "sd35"],
-                    help="sd35: SD3.5-Large MMDiT, 1024^2, 1 prompt per GPU (config C5) - a secondary line")
+    ap.add_argument("--model", default="sd15", choices=["sd15", "sdxl", "sd35"],
+                    help="secondary lines: sdxl = SDXL W8A8 1024^2, 2 prompts per GPU (config C4); "
+                         "sd35 = SD3.5-Large W4A16 1024^2, 1 prompt per GPU (config C5)")
     ap.add_argument("--calib-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
     if a.mode is None:
-        a.mode = "w4a16" if a.model == "sd35" else "w8a8-sq"
+        a.mode = {"sd35": "w4a16", "sdxl": "w8a8"}.get(a.model, "w8a8-sq")
+    if a.model == "sdxl":
+        if a.res == 512:
+            a.res = 1024
+        if a.batch == 4:
+            a.batch = 2
     if a.model == "sd35":
         if a.mode == "w8a8-sq":
             ap.error("SmoothQuant has no SD3.5 block mapping in the reference")
@@ -75,6 +81,16 @@ def mmdit_gflop_per_sample(cfg, s, sc):
 
 
 def build_model(args, dev):
+    if args.model == "sdxl":
+        from qdiff.models import StableDiffusionXL
+        model = StableDiffusionXL.from_pretrained("synthetic:sdxl", device=dev, seed=0)
+        if args.mode == "w8a8-sq":
+            model.quantize(quant_config=dict(QCFG[args.mode]), quantType="sq", quantUnet=True,
+                           calibration=dict(n_samples=args.batch, batch_size=args.batch,
+                                            num_inference_steps=args.calib_steps, height=args.res, width=args.res))
+        elif args.mode != "fp16":
+            model.quantize(quant_config=dict(QCFG[args.mode]), quantUnet=True)
+        return model
     if args.model == "sd35":
         from qdiff.models import StableDiffusion3_5
         model = StableDiffusion3_5.from_pretrained("synthetic:sd35", device=dev, seed=0)
@@ -95,12 +111,12 @@ def build_model(args, dev):
     return model
 
 
-def dominant_kernel_roofline(dev, iters=20):
-    """Time the largest conv implicit GEMM of the SD1.5 UNet at CFG batch 8 (down/up block 0
-    conv 320->320 3x3 @ 64x64: M = 32768, N = 320, K = 2880) with HIP events on its stream."""
+def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320):
+    """Time the largest conv implicit GEMM of the UNet (SD1.5 at CFG batch 8: down/up block 0
+    conv 320->320 3x3 @ 64x64, M = 32768, N = 320, K = 2880; SDXL at CFG batch 4: the same conv
+    at 128x128, M = 65536) with HIP events on its stream."""
     import torch
     from qdiff import kernels as K
-    n, h, w, c = 8, 64, 64, 320
     g = torch.Generator(device="cpu").manual_seed(0)
     x = torch.randn(n, h, w, c, generator=g).half().to(dev)
     wt = (torch.randn(c, 3, 3, c, generator=g) / 54).half().to(dev)
@@ -118,23 +134,25 @@ def dominant_kernel_roofline(dev, iters=20):
     ms = e0.elapsed_time(e1) / iters
     flops = 2.0 * (n * h * w) * c * (9 * c)
     tflops = flops / (ms * 1e-3) / 1e12
-    choice = _conv_choice()
-    tr = pmc_traffic(choice["variant"] if choice else None)
+    choice = _conv_choice((n, h, w, c))
+    tr = pmc_traffic(choice["variant"] if choice else None) if (n, h, w, c) == (8, 64, 64, 320) else None
     return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": (tr or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": tr,
-            "kernel": "conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880) implicit GEMM",
+            "kernel": f"conv3x3 {c}->{c} @{h}x{w} b{n} (M={n * h * w},N={c},K={9 * c}) implicit GEMM",
             "kernel_choice": choice,
             "avg_us": round(ms * 1e3, 2)}
 
 
-def _conv_choice():
+def _conv_choice(shape=(8, 64, 64, 320)):
     """GEMM family chosen for the dominant conv ((weight op, qd_gemm_force id); >= 100 = LDS-DMA)."""
     from qdiff import kernels as K
-    for key, c in K.gemm_choices().items():
-        if key[:8] == ("conv", 8, 64, 64, 320, 320, 3, 3):
-            fam = "k_conv_halo" if c and c[1] >= 200 else "k_gemm_dma" if c and c[1] >= 100 else "k_gemm"
-            return {"variant": c[1], "family": fam} if c else None
+    n, h, w, c = shape
+    for key, ch in K.gemm_choices().items():
+        if key[:8] == ("conv", n, h, w, c, c, 3, 3):
+            fam = ("k_gemm_pp" if ch and ch[1] >= 300 else "k_conv_halo" if ch and ch[1] >= 200 else
+                   "k_gemm_dma" if ch and ch[1] >= 100 else "k_gemm")
+            return {"variant": ch[1], "family": fam} if ch else None
     return None
 
 
@@ -224,6 +242,8 @@ def main():
     log(f"model built + quantized ({args.model} {args.mode})")
     if args.model == "sd35":
         return main_sd35(args, model, rank, world, dev, log)
+    if args.model == "sdxl":
+        return main_sdxl(args, model, rank, world, dev, log)
     B = args.batch
     hw = args.res // 8
     loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.5, use_graph=True)
@@ -424,6 +444,95 @@ def main_sd35(args, model, rank, world, dev, log):
             log("cpu baseline ...")
             line["cpu_baseline"] = cpu_baseline_sd35(min(args.cpu_threads, len(os.sched_getaffinity(0))), cfg, s, sc,
                                                      args.denoise_steps)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+SDXL_TFLOP_PER_SAMPLE = 6.76   # SDXL 1024^2 UNet eval, 88 % quantizable GEMM
+
+
+def main_sdxl(args, model, rank, world, dev, log):
+    """SDXL W8A8 1024^2 (SURVEY config C4: batch 16 on 8 GPUs = 2 prompts per GPU), 50
+    EulerDiscrete steps at guidance 5.0, text_time conditioning, graph per step."""
+    import torch
+    import torch.distributed as dist
+    from qdiff import dist as qdist
+    from qdiff.pipeline import synthetic_text_embeddings
+    cfg = model.pipeline.unet.config
+    B = args.batch
+    hw = args.res // 8
+    pooled = cfg.projection_class_embeddings_input_dim - 6 * cfg.addition_time_embed_dim
+    loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 5.0, use_graph=True)
+    full_ctx = torch.empty(2 * B * world, 77, cfg.cross_attention_dim, dtype=torch.float16, device=dev)
+    full_text = torch.empty(2 * B * world, pooled, dtype=torch.float16, device=dev)
+    if rank == 0:
+        prompts = [f"a photograph of synthetic scene {i}" for i in range(B * world)]
+        negs = [""] * (B * world)
+        full_ctx.copy_(torch.cat([synthetic_text_embeddings(negs, dim=cfg.cross_attention_dim, device=dev),
+                                  synthetic_text_embeddings(prompts, dim=cfg.cross_attention_dim, device=dev)]))
+        full_text.copy_(torch.cat([
+            synthetic_text_embeddings([f"{p}\x00pooled" for p in negs], seq_len=1, dim=pooled, device=dev)[:, 0],
+            synthetic_text_embeddings([f"{p}\x00pooled" for p in prompts], seq_len=1, dim=pooled, device=dev)[:, 0]]))
+    time_ids = torch.tensor([[args.res, args.res, 0, 0, args.res, args.res]] * (2 * B), dtype=torch.float32)
+    g = torch.Generator().manual_seed(42 + rank)
+    lat = torch.randn(B, 4, hw, hw, generator=g).half().to(dev)
+
+    def one_step():
+        qdist.broadcast_context(full_ctx, 0)
+        qdist.broadcast_context(full_text, 0)
+        out = loop.run(lat, qdist.shard_context(full_ctx, rank, world), qdist.shard_context(full_text, rank, world),
+                       time_ids)
+        return qdist.gather_latents(out, 0)
+
+    for _ in range(args.warmup):
+        one_step()
+    log("warmup done")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    value = B * world * args.steps / dt
+    if rank == 0:
+        assert out is not None and torch.isfinite(out.float()).all(), "non-finite latents"
+        log(f"timed {args.steps} steps: {dt:.3f}s")
+        path_tflops = value * args.denoise_steps * 2 * SDXL_TFLOP_PER_SAMPLE
+        line = {
+            "metric": f"images/sec SDXL {args.mode.upper()} {args.res}x{args.res} {args.denoise_steps}-step",
+            "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+            "data": "synthetic (random-init SDXL UNet weights N(0,1/fan_in), synthetic text embeddings and latents)",
+            "config": {"workload": f"SDXL UNet {args.mode} fake-quant, {args.res}x{args.res}, {B} prompts/GPU "
+                                   f"(CFG batch {2 * B}), {args.denoise_steps} EulerDiscrete steps, HIP graph per step "
+                                   f"(SURVEY config C4)",
+                       "global_batch": B * world, "seq_len": 77, "parallelism": f"dp{world}"},
+            "roofline": dominant_kernel_roofline(dev, n=2 * B, h=hw, w=hw, c=cfg.block_out_channels[0]),
+            "path_roofline": {"achieved": round(path_tflops / world, 1), "peak": PEAK_F16_TFLOPS,
+                              "unit": "TFLOP/s per GPU", "frac": round(path_tflops / world / PEAK_F16_TFLOPS, 4),
+                              "flop_per_image": round(2 * args.denoise_steps * SDXL_TFLOP_PER_SAMPLE * 1e12)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline ...")
+            base = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))
+            # the SD1.5 sample's per-image seconds scaled by the FLOP ratio of one SDXL image
+            per_image = base["seconds_per_image"] * (2 * args.denoise_steps * SDXL_TFLOP_PER_SAMPLE * 1e12) / \
+                (2 * 50 * UNET_GFLOP_PER_SAMPLE * 1e9)
+            line["cpu_baseline"] = {"value": round(1.0 / per_image, 10), "unit": "images/s", "cores": base["cores"],
+                                    "kind": "port", "sample": base["sample"] + "; scaled to one SDXL 1024^2 image by "
+                                    "the FLOP ratio (6.76 TFLOP per SDXL eval vs 0.803 for SD1.5)",
+                                    "seconds_per_image": round(per_image, 1)}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
