@@ -6,6 +6,8 @@
 // tests/test_gpu_quant.py compares them bit-for-bit with tests/golden/fake_quant_golden.npz.
 #include "common.h"
 
+#include <cstdlib>
+
 #include <atomic>
 #include <cstring>
 
@@ -102,13 +104,26 @@ __global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, 
   }
 }
 
-// launch geometry of k_colmax_nhwc: 16 rows per thread while the grid keeps >= 512 blocks
+// launch geometry of k_colmax_nhwc: up to 64 rows per thread while the grid keeps >= 128
+// blocks.  Each block ends in one atomic max per channel, and same-address device atomics
+// serialise (per-XCD L2s: they resolve beyond L2), so the row splits per sample - the atomic
+// chain length per address - are kept short: measured (rocprofv3, scripts/colmax_sweep.sh)
+// 16.4 -> 8.4 us at [8, 64x64, 320] and 16.4 -> 5.2 us at [8, 16x16, 1280] against the old
+// >= 512-block geometry.  QD_COLMAX_MINBLK / QD_COLMAX_MAXRPT: sweep-only overrides.
 static void colmax_launch(const f16* x, const f16* x2, int c1, int n, long hw, int c, float* amax, hipStream_t st) {
+  static const int minblk = [] {
+    const char* e = getenv("QD_COLMAX_MINBLK");
+    return e ? atoi(e) : 128;
+  }();
+  static const int maxrpt = [] {
+    const char* e = getenv("QD_COLMAX_MAXRPT");
+    return e ? atoi(e) : 64;
+  }();
   const int chunks = c / 8;
   const int bx = chunks < 64 ? chunks : 64, by = 256 / bx;
   const int gx = (chunks + bx - 1) / bx;
-  long rps = (long)by * 16;
-  while (rps > by && (long)gx * n * ((hw + rps - 1) / rps) < 512) rps /= 2;
+  long rps = (long)by * maxrpt;
+  while (rps > by && (long)gx * n * ((hw + rps - 1) / rps) < minblk) rps /= 2;
   k_colmax_nhwc<<<dim3(gx, n, (unsigned)((hw + rps - 1) / rps)), dim3(bx, by), 0, st>>>(x, x2, c1, (int)hw, c,
                                                                                       (int)rps, amax);
 }
