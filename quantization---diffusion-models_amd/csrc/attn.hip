@@ -302,7 +302,7 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, hipStream_t st) {
   constexpr int NB = DP <= 96 ? 2 : 1;
   const float sl2 = scale * 1.4426950408889634f;
-  // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1); unset: heuristic
+  // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2); unset: heuristic
   static const int forced = [] {
     const char* e = getenv("QD_ATTN_CFG");
     return e ? atoi(e) : 0;
@@ -317,14 +317,26 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   }
+  if (forced == 5) {
+    k_attn<DP, DV, NB, 4, 2><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+    return;
+  }
   if (forced == 3) {
     k_attn<DP, DV, NB, 4, 1><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   }
   // long sequences: 8 waves x 2 query groups (256 queries) share each staged K/V tile while the
-  // grid still holds >= 2 blocks per CU; then 8 x 1 (128 queries); 4 x 1 on short ones
-  if (sq >= 512 && DP <= 96 && (long)((sq + 255) / 256) * b * heads >= 512) {
+  // grid still holds >= 2 blocks per CU; then 8 x 1 (128 queries); 4 x 1 on short ones.
+  // head_dim 49..64 (SD3.5 / SDXL): 4 waves x 2 groups (accumulators partly in AGPRs, 2 blocks
+  // per CU) - scripts/attn_sweep.sh: 626 -> 543 us on SD3.5-L's joint attention, 272 -> 234 us
+  // on SDXL's 64x64 level; at head_dim 40 (SD1.5) 8 x 2 stays ahead (304 vs 370 us).
+  if (sq >= 512 && DV > 48 && DV <= 80) {
+    const int grid = ((sq + 127) / 128) * b * heads;
+    k_attn<DP, DV, NB, 4, 2><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+  } else if (sq >= 512 && DP <= 96 && (long)((sq + 255) / 256) * b * heads >= 512) {
     const int grid = ((sq + 255) / 256) * b * heads;
     k_attn<DP, DV, NB, 8, 2><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
                                                   (f16*)o, ldo, heads, sq, skv, d, sl2);

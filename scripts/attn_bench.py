@@ -8,7 +8,8 @@ from qdiff import kernels as K
 
 dev = "cuda:0"
 for (b, s, skv, heads, d, ld) in ((8, 4096, 4096, 8, 40, 960), (8, 1024, 1024, 10, 64, 1920), (2, 4429, 4429, 38, 64, 7296),
-                                  (8, 4096, 77, 8, 40, 320)):
+                                  (8, 4096, 77, 8, 40, 320), (8, 1024, 1024, 8, 80, 1920), (8, 256, 256, 8, 160, 3840),
+                                  (4, 4096, 4096, 10, 64, 1920), (4, 1024, 1024, 20, 64, 3840)):
     c = heads * d
     x = torch.randn(b, s, ld, device=dev).half()
     kv = torch.randn(b, skv, ld, device=dev).half()

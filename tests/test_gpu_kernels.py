@@ -246,7 +246,7 @@ def test_gemm_plans_split_k_for_small_m():
 # ------------------------------------------------------------------ attention
 @pytest.mark.parametrize("b,heads,sq,skv,d", [(2, 8, 256, 256, 40), (2, 8, 64, 77, 80), (1, 8, 128, 77, 160),
                                               (2, 5, 200, 200, 64), (1, 2, 4096, 4096, 40), (4, 8, 4000, 333, 40),
-                                              (4, 8, 4096, 1024, 80)])
+                                              (4, 8, 4096, 1024, 80), (2, 4, 1024, 1024, 64), (1, 3, 600, 333, 64)])
 def test_attention(b, heads, sq, skv, d, dev):
     k = K()
     g = torch.Generator().manual_seed(sq + skv + d)
