@@ -13,7 +13,10 @@ Also reported (rank 0):
   cpu_baseline  the reference's CPU path restated by the oracle (torch-CPU fp16 ops, W8A8
                 fake-quant) timed on this box's host cores on a bounded sample (one op of each
                 FLOP class; see cpu_baseline())
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Secondary lines (same JSON contract): --model sdxl (SURVEY config C4: SDXL W8A8 1024^2, 2
+prompts per GPU, 50 EulerDiscrete steps) and --model sd35 (config C5: SD3.5-Large W4A16 g128
+1024^2, 1 prompt per GPU, flow-match Euler).
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model sd15|sdxl|sd35]
 """
 import argparse
 import json
