@@ -162,11 +162,38 @@ class RefMMDiT:
         co = None if pre else self.lin(p + ".to_add_out", co)
         return self.lin(p + ".to_out.0", ho), co
 
+    def self_attn(self, p, nx):
+        """diffusers Attention + AttnProcessor2_0 (MMDiT-X attn2): image tokens only."""
+        b = nx.shape[0]
+        heads = self.cfg["num_attention_heads"]
+        d = self.cfg["attention_head_dim"]
+
+        def heads_view(t):
+            return t.view(b, -1, heads, d).transpose(1, 2)
+
+        q = heads_view(self.lin(p + ".to_q", nx))
+        k = heads_view(self.lin(p + ".to_k", nx))
+        v = heads_view(self.lin(p + ".to_v", nx))
+        if self.cfg.get("qk_norm") == "rms_norm":
+            q, k = self.rms(p + ".norm_q", q), self.rms(p + ".norm_k", k)
+        o = self.ops.scaled_dot_product_attention(q, k, v, dropout_p=0.0, is_causal=False)
+        o = o.transpose(1, 2).reshape(b, -1, heads * d).to(q.dtype)
+        return self.lin(p + ".to_out.0", o)
+
     def block(self, i, h, ctx, temb_silu):
+        """diffusers JointTransformerBlock.forward; blocks listed in dual_attention_layers
+        (SD3.5-Medium MMDiT-X) take SD35AdaLayerNormZeroX's 9 chunks and the attn2 residual."""
         p = f"transformer_blocks.{i}"
         pre = i == self.cfg["num_layers"] - 1
-        sh_msa, sc_msa, g_msa, sh_mlp, sc_mlp, g_mlp = self.lin(p + ".norm1.linear", temb_silu).chunk(6, dim=1)
-        nh = self.ln(h) * (1 + sc_msa[:, None]) + sh_msa[:, None]
+        dual = i in tuple(self.cfg.get("dual_attention_layers") or ())
+        e1 = self.lin(p + ".norm1.linear", temb_silu)
+        if dual:
+            sh_msa, sc_msa, g_msa, sh_mlp, sc_mlp, g_mlp, sh_msa2, sc_msa2, g_msa2 = e1.chunk(9, dim=1)
+        else:
+            sh_msa, sc_msa, g_msa, sh_mlp, sc_mlp, g_mlp = e1.chunk(6, dim=1)
+        ln_h = self.ln(h)
+        nh = ln_h * (1 + sc_msa[:, None]) + sh_msa[:, None]
+        nh2 = ln_h * (1 + sc_msa2[:, None]) + sh_msa2[:, None] if dual else None
         e2 = self.lin(p + ".norm1_context.linear", temb_silu)
         if pre:
             cscale, cshift = e2.chunk(2, dim=1)
@@ -176,6 +203,8 @@ class RefMMDiT:
             nc = self.ln(ctx) * (1 + c_sc_msa[:, None]) + c_sh_msa[:, None]
         ao, co = self.attn(p + ".attn", nh, nc, pre)
         h = h + g_msa.unsqueeze(1) * ao
+        if dual:
+            h = h + g_msa2.unsqueeze(1) * self.self_attn(p + ".attn2", nh2)
         nh = self.ln(h) * (1 + sc_mlp[:, None]) + sh_mlp[:, None]
         h = h + g_mlp.unsqueeze(1) * self.ff(p + ".ff", nh)
         if pre:

@@ -69,6 +69,9 @@ class MMDiTConfig:
 # SD3.5-Large (stable-diffusion-3.5-large transformer/config.json) and SD3-Medium
 SD35_LARGE = MMDiTConfig()
 SD3_MEDIUM = MMDiTConfig(num_layers=24, num_attention_heads=24, caption_projection_dim=1536, qk_norm=None)
+# SD3.5-Medium (MMDiT-X): blocks 0-12 carry the second, image-only self-attention
+SD35_MEDIUM = MMDiTConfig(num_layers=24, num_attention_heads=24, caption_projection_dim=1536, pos_embed_max_size=384,
+                          dual_attention_layers=tuple(range(13)))
 
 
 def tiny_mmdit_config(**kw):
@@ -141,6 +144,17 @@ class AdaLayerNormZero(nn.Module):
         self.norm = nn.LayerNorm(dim, elementwise_affine=False, eps=1e-6)
 
 
+class SD35AdaLayerNormZeroX(nn.Module):
+    """diffusers SD35AdaLayerNormZeroX (MMDiT-X blocks): one linear to 9 * dim, chunked as
+    shift | scale | gate for msa, mlp and the second (image-only) attention msa2."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.silu = nn.SiLU()
+        self.linear = nn.Linear(dim, 9 * dim)
+        self.norm = nn.LayerNorm(dim, elementwise_affine=False, eps=1e-6)
+
+
 class AdaLayerNormContinuous(nn.Module):
     def __init__(self, dim, cond_dim):
         super().__init__()
@@ -182,6 +196,26 @@ class JointAttention(nn.Module):
             raise NotImplementedError(f"qk_norm={qk_norm!r}")
 
 
+class SelfAttention(nn.Module):
+    """diffusers Attention(query_dim=dim, out_dim=dim, bias=True, qk_norm) driven by
+    AttnProcessor2_0: the MMDiT-X blocks' image-only ``attn2``."""
+
+    def __init__(self, dim, heads, head_dim, qk_norm):
+        super().__init__()
+        inner = heads * head_dim
+        self.heads = heads
+        self.to_q = nn.Linear(dim, inner)
+        self.to_k = nn.Linear(dim, inner)
+        self.to_v = nn.Linear(dim, inner)
+        self.to_out = nn.ModuleList([nn.Linear(inner, dim), nn.Dropout(0.0)])
+        if qk_norm == "rms_norm":
+            self.norm_q, self.norm_k = RMSNorm(head_dim), RMSNorm(head_dim)
+        elif qk_norm is None:
+            self.norm_q = self.norm_k = None
+        else:
+            raise NotImplementedError(f"qk_norm={qk_norm!r}")
+
+
 class GELU(nn.Module):
     def __init__(self, dim, inner):
         super().__init__()
@@ -197,12 +231,14 @@ class FeedForward(nn.Module):
 
 
 class JointTransformerBlock(nn.Module):
-    def __init__(self, dim, heads, head_dim, context_pre_only, qk_norm):
+    def __init__(self, dim, heads, head_dim, context_pre_only, qk_norm, use_dual_attention=False):
         super().__init__()
         self.context_pre_only = context_pre_only
-        self.norm1 = AdaLayerNormZero(dim)
+        self.use_dual_attention = use_dual_attention
+        self.norm1 = SD35AdaLayerNormZeroX(dim) if use_dual_attention else AdaLayerNormZero(dim)
         self.norm1_context = AdaLayerNormContinuous(dim, dim) if context_pre_only else AdaLayerNormZero(dim)
         self.attn = JointAttention(dim, heads, head_dim, context_pre_only, qk_norm)
+        self.attn2 = SelfAttention(dim, heads, head_dim, qk_norm) if use_dual_attention else None
         self.norm2 = nn.LayerNorm(dim, elementwise_affine=False, eps=1e-6)
         self.ff = FeedForward(dim)
         if context_pre_only:
@@ -216,8 +252,6 @@ class JointTransformerBlock(nn.Module):
 class SD3Transformer2DModel(nn.Module):
     def __init__(self, cfg: MMDiTConfig = SD35_LARGE):
         super().__init__()
-        if cfg.dual_attention_layers:
-            raise NotImplementedError("SD3.5-Medium dual-attention (MMDiT-X) blocks are not part of this build")
         if cfg.caption_projection_dim != cfg.inner_dim:
             raise ValueError("caption_projection_dim must equal heads * head_dim (joint attention)")
         self.config = cfg
@@ -227,7 +261,7 @@ class SD3Transformer2DModel(nn.Module):
         self.context_embedder = nn.Linear(cfg.joint_attention_dim, cfg.caption_projection_dim)
         self.transformer_blocks = nn.ModuleList([
             JointTransformerBlock(c, cfg.num_attention_heads, cfg.attention_head_dim, i == cfg.num_layers - 1,
-                                  cfg.qk_norm) for i in range(cfg.num_layers)])
+                                  cfg.qk_norm, i in cfg.dual_attention_layers) for i in range(cfg.num_layers)])
         self.norm_out = AdaLayerNormContinuous(c, c)
         self.proj_out = nn.Linear(c, cfg.patch_size * cfg.patch_size * cfg.out_channels)
 
@@ -440,12 +474,38 @@ def _ff(ff, x):
     return run_linear(ff.net[2], f)
 
 
+def self_attn_fwd(attn, nx, n, s):
+    """diffusers Attention + AttnProcessor2_0 (the MMDiT-X ``attn2``) on nx [n*s, C]: to_q | to_k
+    | to_v stacked into one [n, s, 3C] buffer, RMSNorm qk-norm in place, attention over the
+    image tokens only, to_out.  Returns [n*s, C]."""
+    c = nx.shape[1]
+    heads = attn.heads
+    d = c // heads
+    op = _stacked_operand(attn, "_qd_qkv", [attn.to_q, attn.to_k, attn.to_v])
+    if op is not None:
+        w, fmt, scl, g, b, wf, _ = op
+        J = K.linear(nx, w, fmt, scl, g, bias=b, weight_f16=wf)
+    else:
+        J = A.empty((n * s, 3 * c), torch.float16, nx.device)
+        for j, l in enumerate((attn.to_q, attn.to_k, attn.to_v)):
+            K.copy_rows(run_linear(l, nx), J[:, j * c:(j + 1) * c])
+    if attn.norm_q is not None:
+        K.rmsnorm_heads(J, n * s, heads, d, 3 * c, _f16(attn.norm_q.weight), attn.norm_q.eps)
+        K.rmsnorm_heads(J[:, c:], n * s, heads, d, 3 * c, _f16(attn.norm_k.weight), attn.norm_k.eps)
+    J = J.view(n, s, 3 * c)
+    o = K.attention(J[:, :, :c], J[:, :, c:2 * c], J[:, :, 2 * c:], heads)   # [n, s, C]
+    return run_linear(attn.to_out[0], o.reshape(n * s, c))
+
+
 def joint_block_fwd(blk, h, cs, n, s, sc, mods):
     """diffusers JointTransformerBlock.forward on token-major streams h [n*s, C], cs [n*sc, C];
-    returns (h, cs) (cs None after the context_pre_only block)."""
+    returns (h, cs) (cs None after the context_pre_only block).  MMDiT-X blocks
+    (use_dual_attention) add h += gate_msa2 * attn2(norm(h_in) * (1 + scale_msa2) + shift_msa2)
+    after the joint attention's residual, norm taken of the block's INPUT h (SD35AdaLayerNormZeroX)."""
     c = h.shape[1]
-    m = mods[id(blk.norm1)]      # shift_msa | scale_msa | gate_msa | shift_mlp | scale_mlp | gate_mlp
+    m = mods[id(blk.norm1)]      # shift_msa | scale_msa | gate_msa | shift_mlp | scale_mlp | gate_mlp [| msa2 x3]
     nx = K.adaln(h, s, shift=m[:, :c], scale=m[:, c:2 * c])
+    nx2 = K.adaln(h, s, shift=m[:, 6 * c:7 * c], scale=m[:, 7 * c:8 * c]) if blk.use_dual_attention else None
     mc = mods[id(blk.norm1_context)]
     if blk.context_pre_only:     # AdaLayerNormContinuous: scale | shift
         nc = K.adaln(cs, sc, shift=mc[:, c:2 * c], scale=mc[:, :c])
@@ -455,6 +515,8 @@ def joint_block_fwd(blk, h, cs, n, s, sc, mods):
     J = joint_qkv(attn, nx, nc, n, s, sc)
     o = K.attention(J[:, :, :c], J[:, :, c:2 * c], J[:, :, 2 * c:], attn.heads)   # [n, s + sc, C]
     h = K.gated_residual(h, _joint_rows_out(attn.to_out[0], o, n, 0, s), m[:, 2 * c:3 * c], s)
+    if nx2 is not None:
+        h = K.gated_residual(h, self_attn_fwd(blk.attn2, nx2, n, s), m[:, 8 * c:9 * c], s)
     nx = K.adaln(h, s, shift=m[:, 3 * c:4 * c], scale=m[:, 4 * c:5 * c])
     h = K.gated_residual(h, _ff(blk.ff, nx), m[:, 5 * c:6 * c], s)
     if blk.context_pre_only:

@@ -7,14 +7,14 @@ StableDiffusion3_5.py:17-31), ``to(device)`` and ``save_pretrained``.  Weights l
 diffusers directory (``model_index.json`` + ``unet/`` or ``transformer/`` ``config.json`` +
 ``diffusion_pytorch_model.safetensors``) - there is no network - or are synthesized
 (``synthetic:sd15`` / ``synthetic:sdxl`` / ``synthetic:tiny`` / ``synthetic:sdxl-tiny`` /
-``synthetic:sd35`` / ``synthetic:sd35-tiny``) with the real shapes and N(0, 1/fan_in) values.
+``synthetic:sd35`` / ``synthetic:sd35-medium`` / ``synthetic:sd35-tiny`` / ``synthetic:sd35m-tiny``) with the real shapes and N(0, 1/fan_in) values.
 """
 import json
 import os
 
 import torch
 
-from .mmdit import SD35_LARGE, MMDiTConfig, SD3Transformer2DModel, tiny_mmdit_config
+from .mmdit import SD35_LARGE, SD35_MEDIUM, MMDiTConfig, SD3Transformer2DModel, tiny_mmdit_config
 from .scheduler import DDIMConfig, EulerDiscreteConfig, FlowMatchConfig
 from .unet import SD15, SDXL, UNet2DConditionModel, UNetConfig, tiny_config, tiny_sdxl_config
 
@@ -25,6 +25,9 @@ SYNTHETIC = {
     "synthetic:sdxl-tiny": ("StableDiffusionXLPipeline", None),
     "synthetic:sd35": ("StableDiffusion3Pipeline", SD35_LARGE),
     "synthetic:sd35-tiny": ("StableDiffusion3Pipeline", None),
+    "synthetic:sd35-medium": ("StableDiffusion3Pipeline", SD35_MEDIUM),
+    # SD3.5-Medium-shaped tiny MMDiT-X: dual attention in blocks 0-1 of 3 (block 2 is context_pre_only)
+    "synthetic:sd35m-tiny": ("StableDiffusion3Pipeline", tiny_mmdit_config(num_layers=3, dual_attention_layers=(0, 1))),
 }
 MMDIT_PIPELINES = ("StableDiffusion3Pipeline",)
 
@@ -119,7 +122,7 @@ def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16):
             # built and drawn on the target device (a full SD3.5-Large is 8 B parameters)
             with torch.device(device):
                 net = SD3Transformer2DModel(mcfg).to(dtype)
-            big = SYNTHETIC[model_path][1] is not None and torch.device(device).type == "cuda"
+            big = not model_path.endswith("-tiny") and torch.device(device).type == "cuda"
             net.init_synthetic(seed, rng_device=device if big else "cpu")
         else:
             net = UNet2DConditionModel(mcfg).to(dtype)

@@ -229,6 +229,55 @@ def test_sd35_large_width_two_blocks_512():
     assert mx32 <= 0.02 and mean32 <= 0.004, (mx32, mean32)
 
 
+@pytest.mark.parametrize("qc", [None,
+                                dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
+                                dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True)])
+def test_tiny_mmdit_x_eval_matches_oracle(qc):
+    """SD3.5-Medium-shaped MMDiT-X (dual attention in blocks 0-1 of 3: SD35AdaLayerNormZeroX's
+    9C adaLN, image-only attn2 with RMSNorm qk-norm) vs the oracle, CFG batch 2, odd context."""
+    model = _model("synthetic:sd35m-tiny", seed=2)
+    tr = model.pipeline.transformer
+    cfg = tr.config
+    assert tr.transformer_blocks[0].attn2 is not None and tr.transformer_blocks[2].attn2 is None
+    sd = {k: v.detach().cpu() for k, v in tr.state_dict().items()}
+    if qc is not None:
+        model.quantize(quant_config=dict(qc), quantTransformer=True)
+    x, enc, pooled = _inputs(cfg, 21, b=2, sc=37)
+    got = _one_eval(model, x, 641.5, enc, pooled)
+    assert torch.isfinite(got).all()
+    q = None if qc is None else dict(qc)
+    ref = RefMMDiT(_cfgdict(cfg), sd, q).forward(x, 641.5, enc, pooled)
+    ref32 = RefMMDiT(_cfgdict(cfg), sd, q, variant="fp32").forward(x, 641.5, enc, pooled)
+    _check_parity(got, ref, ref32, f"tiny MMDiT-X eval {qc}")
+
+
+@pytest.mark.timeout(600)
+def test_sd35_medium_width_dual_blocks_512():
+    """SD3.5-Medium width (C = 1536, 24 heads x 64, pos_embed_max_size 384) with 2 of its
+    blocks, both MMDiT-X (dual attention), 512^2 latents, 333-token context, W4A16 g128,
+    CFG batch 2, against the fp32 oracle (bound of the SD3.5-L width case)."""
+    import dataclasses as dc
+    from qdiff.mmdit import SD35_MEDIUM, SD3Transformer2DModel
+    from qdiff.models import StableDiffusion3_5
+    from qdiff.pipeline_io import QDiffPipeline
+    cfg = dc.replace(SD35_MEDIUM, num_layers=2, sample_size=64, dual_attention_layers=(0, 1))
+    with torch.device(DEV):
+        tr = SD3Transformer2DModel(cfg).half()
+    tr.init_synthetic(9, rng_device=DEV)
+    sd = {k: v.detach().cpu() for k, v in tr.state_dict().items()}
+    model = StableDiffusion3_5(QDiffPipeline(transformer=tr, class_name="StableDiffusion3Pipeline"),
+                               "StableDiffusion3Pipeline", False, {}, None)
+    qc = dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False)
+    model.quantize(quant_config=dict(qc), quantTransformer=True)
+    x, enc, pooled = _inputs(cfg, 14, b=1, sc=333)
+    got = _one_eval(model, x, 811.0, enc, pooled)
+    ref32 = RefMMDiT(_cfgdict(cfg), sd, qc, variant="fp32").forward(x, 811.0, enc, pooled)
+    mx32, mean32 = _rel_errs(got, ref32)
+    print(f"SD3.5-M width, 2 dual blocks, W4A16: gpu-vs-fp32 max {mx32:.4g} mean {mean32:.4g}")
+    assert torch.isfinite(got).all()
+    assert mx32 <= 0.02 and mean32 <= 0.004, (mx32, mean32)
+
+
 def test_quantized_buffers_bit_exact_and_output_quant_names():
     from oracle.unet_ref import quantize_state_dict
     from qdiff.fake_quant import WxAxLinear

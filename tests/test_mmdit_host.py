@@ -83,12 +83,13 @@ def test_oracle_euler_step_formula():
     assert (out - ref).abs().max() < 0.02 * ref.abs().max()
 
 
-def test_oracle_variants_agree_unquantized():
+@pytest.mark.parametrize("dual", [(), (0, 1)])
+def test_oracle_variants_agree_unquantized(dual):
     """Without activation quantization the oracle's fp16 and fp32 variants stay within a few ulp
-    of each other on the tiny MMDiT (sanity of the restatement's op order)."""
+    of each other on the tiny MMDiT (sanity of the restatement's op order); dual = MMDiT-X blocks."""
     from oracle.mmdit_ref import RefMMDiT
     from qdiff.mmdit import SD3Transformer2DModel, tiny_mmdit_config
-    cfg = tiny_mmdit_config()
+    cfg = tiny_mmdit_config(num_layers=3, dual_attention_layers=dual) if dual else tiny_mmdit_config()
     t = SD3Transformer2DModel(cfg).half().init_synthetic(0)
     sd = dict(t.state_dict())
     cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(cfg).items()}
@@ -100,6 +101,58 @@ def test_oracle_variants_agree_unquantized():
     b = RefMMDiT(cd, sd, variant="fp32").forward(x, 1000.0, enc, pooled).float()
     assert a.shape == (2, 16, 16, 16) and torch.isfinite(a).all()
     assert (a - b).abs().max() < 0.02 * a.abs().max()
+
+
+def test_sd35_medium_tree():
+    """SD3.5-Medium (MMDiT-X): blocks 0-12 carry SD35AdaLayerNormZeroX (9C adaLN) and an
+    image-only attn2 (to_q/k/v/out + RMSNorm qk-norm).  2,243,171,520 parameters = SD3-Medium's
+    2,028,328,000 + 13 x (4 attn2 linears + 3C extra adaLN rows) + the qk-norm weights."""
+    from qdiff.base import load_quantized_modules
+    from qdiff.fake_quant import WxAxLinear
+    from qdiff.mmdit import SD35_MEDIUM, tiny_mmdit_config, SD3Transformer2DModel
+    m = _meta(SD35_MEDIUM)
+    assert sum(p.numel() for p in m.parameters()) == 2_243_171_520
+    assert sum(isinstance(x, nn.Linear) for x in m.modules()) == 23 * 14 + 11 + 7 + 13 * 4
+    sd = m.state_dict()
+    assert sd["transformer_blocks.12.norm1.linear.weight"].shape == (9 * 1536, 1536)
+    assert sd["transformer_blocks.13.norm1.linear.weight"].shape == (6 * 1536, 1536)
+    assert "transformer_blocks.12.attn2.norm_k.weight" in sd and "transformer_blocks.13.attn2.to_q.weight" not in sd
+    # reference naming rule: attn2.to_q / to_k / to_v do not contain "q_proj" -> no output quant
+    t = SD3Transformer2DModel(tiny_mmdit_config(num_layers=3, dual_attention_layers=(0, 1)))
+    load_quantized_modules(t, bitWidth=4, group_size=128, act_bits=8)
+    oq = sorted(n for n, x in t.named_modules() if isinstance(x, WxAxLinear) and x.output_quant_name != "None")
+    assert oq == sorted(f"transformer_blocks.{i}.attn.add_{p}_proj" for i in range(3) for p in "qkv")
+
+
+def test_oracle_dual_block_with_silent_attn2_equals_plain_block():
+    """Oracle self-consistency of the MMDiT-X restatement: with attn2.to_out zeroed the attn2
+    residual adds exact zeros, so the dual model equals the plain model holding the first 6C
+    adaLN rows, bit for bit."""
+    from oracle.mmdit_ref import RefMMDiT
+    from qdiff.mmdit import SD3Transformer2DModel, tiny_mmdit_config
+    cd_ = tiny_mmdit_config(num_layers=3, dual_attention_layers=(0, 1))
+    cp_ = tiny_mmdit_config(num_layers=3)
+    t = SD3Transformer2DModel(cd_).half().init_synthetic(4)
+    sd = dict(t.state_dict())
+    c = cd_.inner_dim
+    for i in (0, 1):
+        sd[f"transformer_blocks.{i}.attn2.to_out.0.weight"] = torch.zeros_like(sd[f"transformer_blocks.{i}.attn2.to_out.0.weight"])
+    plain = {k: v for k, v in sd.items() if ".attn2." not in k}
+    for i in (0, 1):
+        for w in ("weight", "bias"):
+            plain[f"transformer_blocks.{i}.norm1.linear.{w}"] = sd[f"transformer_blocks.{i}.norm1.linear.{w}"][:6 * c]
+    assert set(plain) == set(SD3Transformer2DModel(cp_).state_dict())
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 16, 16, 16, generator=g).half()
+    enc = torch.randn(2, 24, 64, generator=g).half()
+    pooled = torch.randn(2, 64, generator=g).half()
+    asd = lambda cfg: {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(cfg).items()}
+    a = RefMMDiT(asd(cd_), sd).forward(x, 700.0, enc, pooled)
+    b = RefMMDiT(asd(cp_), plain).forward(x, 700.0, enc, pooled)
+    assert torch.equal(a, b)
+    # and the attn2 branch is live when its weights are not zero
+    sd2 = dict(t.state_dict())
+    assert not torch.equal(RefMMDiT(asd(cd_), sd2).forward(x, 700.0, enc, pooled), a)
 
 
 def test_mmdit_pipeline_files_roundtrip(tmp_path):
