@@ -30,6 +30,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace qd;
 
@@ -1377,6 +1378,156 @@ static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t 
   else launch_fmt<64, 64, AMODE, SPLIT>(p, fmt, st);
 }
 
+// ---- skinny-M GEMV (M <= 4) ------------------------------------------------------------
+// The SD3 stacked adaLN projection (M = CFG batch 2, N = 1.1 M rows of int4 codes, K 2432) and
+// the per-step time-embedding linears are weight-stream (HBM) bound: a 64x64 MFMA tile wastes
+// 62 of its 64 rows and reaches ~1 TB/s.  Here each wave owns 4 consecutive output rows at a
+// time (grid-stride), its lanes stride over 32-element k chunks (16 B of int4 codes, 32 B of
+// int8, 64 B of fp16 per chunk and row, 4 rows' loads in flight), the activation chunks a lane
+// needs stay in registers for the whole kernel, and a butterfly reduces each (row, m) dot.
+// Dequant is the tile loaders' half(q * s) and the epilogue rounds like gemm_epilogue
+// (half(acc + bias) -> GELU-tanh -> + residual); only the fp32 summation order differs.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+
+template <int BFMT>
+struct GemvChunk {
+  static constexpr int NV = BFMT == QD_WFMT_F16 ? 4 : BFMT == QD_WFMT_I8 ? 2 : 1;  // 16-B loads
+  i32x4 v[NV];
+  float s;
+  __device__ __forceinline__ void load(const GemmArgs& p, long n, int c) {
+    const int k0 = c * 32;
+    const i32x4* src;
+    if constexpr (BFMT == QD_WFMT_F16) src = reinterpret_cast<const i32x4*>((const f16*)p.b + n * p.K + k0);
+    else if constexpr (BFMT == QD_WFMT_I8) src = reinterpret_cast<const i32x4*>((const int8_t*)p.b + n * p.K + k0);
+    else src = reinterpret_cast<const i32x4*>((const uint8_t*)p.b + n * (p.K / 2) + k0 / 2);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = __builtin_nontemporal_load(src + q);
+    s = BFMT == QD_WFMT_F16 ? 0.f : (float)p.bscale[n * (p.K / p.group) + k0 / p.group];
+  }
+  // weight k0 + e as the tile GEMM's fp16 operand
+  __device__ __forceinline__ void decode(f16 (&w)[32]) const {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int wd[4] = {v[q][0], v[q][1], v[q][2], v[q][3]};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if constexpr (BFMT == QD_WFMT_F16) {
+          w[q * 8 + 2 * d] = __builtin_bit_cast(f16, (unsigned short)(wd[d] & 0xffff));
+          w[q * 8 + 2 * d + 1] = __builtin_bit_cast(f16, (unsigned short)((unsigned)wd[d] >> 16));
+        } else if constexpr (BFMT == QD_WFMT_I8) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[q * 16 + d * 4 + e] = (f16)((float)(int)(int8_t)((wd[d] >> (8 * e)) & 0xff) * s);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int nib = (wd[d] >> (4 * e)) & 0xf;
+            w[d * 8 + e] = (f16)((float)(nib >= 8 ? nib - 16 : nib) * s);
+          }
+        }
+      }
+    }
+  }
+};
+
+template <int BFMT, int MM, int CPL>
+__global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
+  constexpr int R = 4;
+  const int lane = threadIdx.x & 63;
+  const int nch = p.K / 32;
+  f16x8 a[MM][CPL][4];
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        a[m][j][q] = (m < p.M && c < nch) ? *reinterpret_cast<const f16x8*>(p.a + (long)m * p.lda + c * 32 + q * 8)
+                                          : f16x8{};
+    }
+  const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
+  const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
+  const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+  const long nwaves = (long)gridDim.x * 4;
+  for (long n0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R; n0 < p.N; n0 += nwaves * R) {
+    float acc[R][MM];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int m = 0; m < MM; ++m) acc[r][m] = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) {
+        GemvChunk<BFMT> ch[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) ch[r].load(p, n0 + r, c);   // N % 8 == 0: n0 + r < N
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          f16 w[32];
+          ch[r].decode(w);
+#pragma unroll
+          for (int e = 0; e < 32; e += 2) {
+            const f16x2 w2 = {w[e], w[e + 1]};
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+              const f16x2 a2 = {a[m][j][e >> 3][e & 7], a[m][j][e >> 3][(e & 7) + 1]};
+              acc[r][m] = __builtin_amdgcn_fdot2(a2, w2, acc[r][m], false);   // v_dot2_f32_f16
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        float v = acc[r][m];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == r * MM + m && m < p.M) {
+          const long n = n0 + r;
+          f16 h = (f16)(v + (has_bias ? (float)p.bias[n] : 0.f));
+          if (gtanh) h = (f16)gelu_tanh_f((float)h);
+          if (has_res) h = (f16)((float)h + (float)p.res[(long)m * p.ldy + n]);
+          p.y[(long)m * p.ldy + n] = h;
+        }
+      }
+  }
+}
+
+// chunks per lane the register-resident activation allows (0: not a GEMV shape)
+static int gemv_cpl(const GemmArgs& p) {
+  if (p.M < 1 || p.M > 4 || (p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU)) || p.K % 32) return 0;
+  const int cpl = (p.K / 32 + 63) / 64;
+  const int mm = p.M <= 2 ? 2 : 4;
+  const int cap = mm == 2 ? 4 : 2;   // MM * CPL * 16 activation VGPRs <= 128
+  return cpl <= cap ? (cpl <= 1 ? 1 : cpl <= 2 ? 2 : 4) : 0;
+}
+
+template <int BFMT, int MM>
+static void launch_gemv_cpl(const GemmArgs& p, int cpl, int nwg, hipStream_t st) {
+  if (cpl == 1) k_gemv<BFMT, MM, 1><<<nwg, 256, 0, st>>>(p);
+  else if (cpl == 2) k_gemv<BFMT, MM, 2><<<nwg, 256, 0, st>>>(p);
+  else if constexpr (MM == 2) k_gemv<BFMT, MM, 4><<<nwg, 256, 0, st>>>(p);
+}
+
+template <int BFMT>
+static void launch_gemv_fmt(const GemmArgs& p, int cpl, hipStream_t st) {
+  // one 4-row group per wave per pass; cap the grid at 8 waves per SIMD-slot's worth of CUs
+  const long groups = (p.N + 3) / 4;
+  const int nwg = (int)std::min<long>((groups + 3) / 4, 256L * 16);
+  if (p.M <= 2) launch_gemv_cpl<BFMT, 2>(p, cpl, nwg, st);
+  else launch_gemv_cpl<BFMT, 4>(p, cpl, nwg, st);
+}
+
+static void launch_gemv(const GemmArgs& p, int fmt, int cpl, hipStream_t st) {
+  if (fmt == QD_WFMT_F16) launch_gemv_fmt<QD_WFMT_F16>(p, cpl, st);
+  else if (fmt == QD_WFMT_I8) launch_gemv_fmt<QD_WFMT_I8>(p, cpl, st);
+  else launch_gemv_fmt<QD_WFMT_I4>(p, cpl, st);
+}
+
 static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 ? (long)pl.splits * M * N : 0; }
 
 template <int AMODE>
@@ -1478,7 +1629,10 @@ extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w
   p.b_bytes = (unsigned)(wfmt == QD_WFMT_F16 ? (long)N * K * 2 : wfmt == QD_WFMT_I8 ? (long)N * K : (long)N * K / 2);
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
-  run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
+  static const bool gemv_off = getenv("QD_NO_GEMV") != nullptr;  // A/B switch: tile GEMM for every M
+  const int cpl = gemv_off ? 0 : gemv_cpl(p);
+  if (cpl) launch_gemv(p, wfmt, cpl, S(stream));
+  else run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();
   return 0;
 }

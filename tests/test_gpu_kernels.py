@@ -163,6 +163,35 @@ def test_linear_formats(M, N, Kd, fmt, dev):
     assert ((y - yf).abs() <= tol).all(), (y - yf).abs().max().item()
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,Kd", [(4864, 2432), (1280, 320), (64, 4096), (8, 64), (640, 8192), (1536, 192)])
+@pytest.mark.parametrize("fmt", ["f16", "i8", "i4"])
+def test_linear_skinny_m_gemv(M, N, Kd, fmt, dev):
+    """M <= 4 runs the skinny-M GEMV (k_gemv: weight-stream bound, register-resident activations)
+    where K / 32 chunks fit its register budget (M 3-4 at K 8192 falls back to the tile GEMM):
+    same dequant and epilogue rounding as the tile kernels, fp32 sums in another order."""
+    k = K()
+    g = torch.Generator().manual_seed(7 * M + N + Kd)
+    x = torch.randn(M, Kd, generator=g).half()
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half()
+    b = torch.randn(N, generator=g).half()
+    res = torch.randn(M, N, generator=g).half()
+    bits = {"f16": 8, "i8": 8, "i4": 4}[fmt]
+    gs = FQ.shrink_group(Kd, 128) if Kd % 32 == 0 else Kd
+    codes, scales, wdq = k.weight_quant(w.to(dev), gs, bits)
+    op, sc, grp = {"f16": (wdq, None, 0), "i8": (codes, scales, gs), "i4": (k.pack_int4(codes), scales, gs)}[fmt]
+    y = k.linear(x.to(dev), op, fmt, sc, grp, bias=b.to(dev), residual=res.to(dev)).cpu().float()
+    pre = (x.float() @ wdq.cpu().float().t() + b.float()).half().float()
+    yf = (pre + res.float()).half().float()
+    tol = ulp16(pre) + ulp16(yf) + 1e-3
+    assert ((y - yf).abs() <= tol).all(), (y - yf).abs().max().item()
+    yt = k.linear(x.to(dev), op, fmt, sc, grp, bias=b.to(dev), gelu_tanh=True).cpu().float()
+    ref_t = torch.nn.functional.gelu(pre, approximate="tanh").half().float()
+    # a 1-ulp move of pre moves gelu_tanh(pre) by at most ~1.13 ulp(pre), then one more rounding
+    tol_t = 1.2 * ulp16(pre) + ulp16(ref_t) + 1e-3
+    assert ((yt - ref_t).abs() <= tol_t).all(), (yt - ref_t).abs().max().item()
+
+
 @pytest.mark.parametrize("M,I,Kd,fmt", [(256, 1280, 320, "f16"), (1000, 640, 640, "i8"), (64, 2560, 1280, "i4")])
 def test_linear_geglu_epilogue(M, I, Kd, fmt, dev):
     k = K()
