@@ -1435,6 +1435,8 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
   constexpr int R = 4;
   const int lane = threadIdx.x & 63;
   const int nch = p.K / 32;
+  // int4: the activations are kept as (k, k + 4) pairs, the order the packed nibble decode
+  // below produces weights in; other formats keep k order
   f16x8 a[MM][CPL][4];
 #pragma unroll
   for (int m = 0; m < MM; ++m)
@@ -1442,9 +1444,12 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
     for (int j = 0; j < CPL; ++j) {
       const int c = lane + 64 * j;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        a[m][j][q] = (m < p.M && c < nch) ? *reinterpret_cast<const f16x8*>(p.a + (long)m * p.lda + c * 32 + q * 8)
-                                          : f16x8{};
+      for (int q = 0; q < 4; ++q) {
+        const f16x8 v = (m < p.M && c < nch) ? *reinterpret_cast<const f16x8*>(p.a + (long)m * p.lda + c * 32 + q * 8)
+                                             : f16x8{};
+        if constexpr (BFMT == QD_WFMT_I4) a[m][j][q] = __builtin_shufflevector(v, v, 0, 4, 1, 5, 2, 6, 3, 7);
+        else a[m][j][q] = v;
+      }
     }
   const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
@@ -1465,6 +1470,29 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
         for (int r = 0; r < R; ++r) ch[r].load(p, n0 + r, c);   // N % 8 == 0: n0 + r < N
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+          if constexpr (BFMT == QD_WFMT_I4) {
+            // packed decode: (nib ^ 8) | 0x6400 is the fp16 1024 + q + 8, minus 1032 = q exactly;
+            // v_pk_mul_f16 by s rounds q * s (exact in fp32) once, as the tile loader's
+            // half((float)q * s).  Lanes of a pair are k = 8d + t and 8d + t + 4.
+            const f16 sh = (f16)ch[r].s;
+            const f16x2 s2 = {sh, sh};
+            const f16x2 off = {(f16)1032.f, (f16)1032.f};
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const unsigned u = (unsigned)ch[r].v[0][d] ^ 0x88888888u;
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                const f16x2 q2 = __builtin_bit_cast(f16x2, ((u >> (4 * t)) & 0x000F000Fu) | 0x64006400u) - off;
+                const f16x2 w2 = q2 * s2;
+#pragma unroll
+                for (int m = 0; m < MM; ++m) {
+                  const f16x2 a2 = {a[m][j][d][2 * t], a[m][j][d][2 * t + 1]};
+                  acc[r][m] = __builtin_amdgcn_fdot2(a2, w2, acc[r][m], false);
+                }
+              }
+            }
+            continue;
+          }
           f16 w[32];
           ch[r].decode(w);
 #pragma unroll
