@@ -108,7 +108,9 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
  * wfmt: QD_WFMT_*; wscale [N][K/group] fp16 for I8/I4.  lda/ldy in elements.
- * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32). */
+ * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32).
+ * M <= 4 without AMAX / GEGLU runs a weight-stream GEMV (same dequant and epilogue rounding;
+ * environment QD_NO_GEMV, read at the first call, keeps the tile GEMM for every M). */
 int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
                   const void* wscale, int group, const void* bias, const void* residual,
                   void* y, int N, int ldy, int epi, float* amax, int rows_per_sample,
