@@ -1430,6 +1430,46 @@ struct GemvChunk {
   }
 };
 
+// one 32-element k chunk of one weight row against the lane's activation slot j
+template <int BFMT, int MM, int CPL>
+__device__ __forceinline__ void gemv_dot(const GemvChunk<BFMT>& ch, const f16x8 (&a)[MM][CPL][4], int j,
+                                         float (&out)[MM]) {
+    if constexpr (BFMT == QD_WFMT_I4) {
+      // packed decode: (nib ^ 8) | 0x6400 is the fp16 1024 + q + 8, minus 1032 = q exactly;
+      // v_pk_mul_f16 by s rounds q * s (exact in fp32) once, as the tile loader's
+      // half((float)q * s).  Lanes of a pair are k = 8d + t and 8d + t + 4.
+      const f16 sh = (f16)ch.s;
+      const f16x2 s2 = {sh, sh};
+      const f16x2 off = {(f16)1032.f, (f16)1032.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const unsigned u = (unsigned)ch.v[0][d] ^ 0x88888888u;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f16x2 q2 = __builtin_bit_cast(f16x2, ((u >> (4 * t)) & 0x000F000Fu) | 0x64006400u) - off;
+          const f16x2 w2 = q2 * s2;
+#pragma unroll
+          for (int m = 0; m < MM; ++m) {
+            const f16x2 a2 = {a[m][j][d][2 * t], a[m][j][d][2 * t + 1]};
+            out[m] = __builtin_amdgcn_fdot2(a2, w2, out[m], false);
+          }
+        }
+      }
+      return;
+    }
+    f16 w[32];
+    ch.decode(w);
+#pragma unroll
+    for (int e = 0; e < 32; e += 2) {
+      const f16x2 w2 = {w[e], w[e + 1]};
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        const f16x2 a2 = {a[m][j][e >> 3][e & 7], a[m][j][e >> 3][(e & 7) + 1]};
+        out[m] = __builtin_amdgcn_fdot2(a2, w2, out[m], false);   // v_dot2_f32_f16
+      }
+    }
+}
+
 template <int BFMT, int MM, int CPL>
 __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
   constexpr int R = 4;
@@ -1470,40 +1510,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
         for (int r = 0; r < R; ++r) ch[r].load(p, n0 + r, c);   // N % 8 == 0: n0 + r < N
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if constexpr (BFMT == QD_WFMT_I4) {
-            // packed decode: (nib ^ 8) | 0x6400 is the fp16 1024 + q + 8, minus 1032 = q exactly;
-            // v_pk_mul_f16 by s rounds q * s (exact in fp32) once, as the tile loader's
-            // half((float)q * s).  Lanes of a pair are k = 8d + t and 8d + t + 4.
-            const f16 sh = (f16)ch[r].s;
-            const f16x2 s2 = {sh, sh};
-            const f16x2 off = {(f16)1032.f, (f16)1032.f};
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              const unsigned u = (unsigned)ch[r].v[0][d] ^ 0x88888888u;
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                const f16x2 q2 = __builtin_bit_cast(f16x2, ((u >> (4 * t)) & 0x000F000Fu) | 0x64006400u) - off;
-                const f16x2 w2 = q2 * s2;
-#pragma unroll
-                for (int m = 0; m < MM; ++m) {
-                  const f16x2 a2 = {a[m][j][d][2 * t], a[m][j][d][2 * t + 1]};
-                  acc[r][m] = __builtin_amdgcn_fdot2(a2, w2, acc[r][m], false);
-                }
-              }
-            }
-            continue;
-          }
-          f16 w[32];
-          ch[r].decode(w);
-#pragma unroll
-          for (int e = 0; e < 32; e += 2) {
-            const f16x2 w2 = {w[e], w[e + 1]};
-#pragma unroll
-            for (int m = 0; m < MM; ++m) {
-              const f16x2 a2 = {a[m][j][e >> 3][e & 7], a[m][j][e >> 3][(e & 7) + 1]};
-              acc[r][m] = __builtin_amdgcn_fdot2(a2, w2, acc[r][m], false);   // v_dot2_f32_f16
-            }
-          }
+          gemv_dot<BFMT, MM, CPL>(ch[r], a, j, acc[r]);
         }
       }
     }
