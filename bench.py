@@ -221,8 +221,27 @@ def cpu_baseline(threads):
             "seconds_per_image": round(per_image, 1)}
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` run directly (not under torchrun): this parent never touches the GPU;
+    it starts N ranks (one process per GPU) through torch.distributed.run on 127.0.0.1 and exits
+    with their status (non-zero if any rank failed)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
     import qdiff_boot  # noqa: F401
@@ -230,8 +249,9 @@ def main():
     from qdiff.pipeline import synthetic_text_embeddings
 
     rank, world, local = qdist.init_from_env()
-    if world != args.gpus and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: run `python bench.py --gpus N` "
+                         "(it launches the N ranks itself) or torchrun with --nproc-per-node N")
     n_gpus = world
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
@@ -265,6 +285,12 @@ def main():
         out = loop.run(lat, ctx)
         return qdist.gather_latents(out, 0)
 
+    def warm_eager():
+        loop.set_inputs(lat, qdist.shard_context(full_ctx, rank, world))
+        loop.step()
+
+    if world > 1:
+        qdist.share_gemm_table(warm_eager, rank, world)
     for _ in range(args.warmup):
         one_step()
     log("warmup done")
@@ -405,6 +431,12 @@ def main_sd35(args, model, rank, world, dev, log):
         out = loop.run(lat, qdist.shard_context(full_ctx, rank, world), qdist.shard_context(full_pooled, rank, world))
         return qdist.gather_latents(out, 0)
 
+    def warm_eager():
+        loop.set_inputs(lat, qdist.shard_context(full_ctx, rank, world), qdist.shard_context(full_pooled, rank, world))
+        loop.step()
+
+    if world > 1:
+        qdist.share_gemm_table(warm_eager, rank, world)
     for _ in range(args.warmup):
         one_step()
     log("warmup done")
@@ -489,6 +521,13 @@ def main_sdxl(args, model, rank, world, dev, log):
                        time_ids)
         return qdist.gather_latents(out, 0)
 
+    def warm_eager():
+        loop.set_inputs(lat, qdist.shard_context(full_ctx, rank, world), qdist.shard_context(full_text, rank, world),
+                        time_ids)
+        loop.step()
+
+    if world > 1:
+        qdist.share_gemm_table(warm_eager, rank, world)
     for _ in range(args.warmup):
         one_step()
     log("warmup done")

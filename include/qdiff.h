@@ -83,7 +83,8 @@ int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, 
  * (fake_quant.py:21-105).  w is [rows, cols] fp16 (a 4-D conv weight is [Co*Ci*kh, kw]);
  * groups of `group` consecutive elements along cols (group == cols for per_channel;
  * per_tensor: group = rows*cols with rows = 1).  Any of codes (int8 [rows, cols]),
- * scales (fp16 [rows, cols/group]) and w_dq (fp16 [rows, cols]) may be NULL. */
+ * scales (fp16 [rows, cols/group]) and w_dq (fp16 [rows, cols]) may be NULL.  n_bits in
+ * [2, 16] as the reference accepts any width; codes must be NULL above 8 bits. */
 int qd_weight_quant(const void* w, int rows, int cols, int group, int n_bits, int8_t* codes,
                     void* scales, void* w_dq, void* stream);
 /* pack int8 codes in [-8, 7] to int4, 2 per byte along cols (cols even). */

@@ -120,6 +120,13 @@ class RefUNet:
         else:
             self.sd, self.flags = sd, {}
         self.hooks = None  # optional {linear name: callable(x)} for calibration
+        # optional {layer name: (input, output)} of every conv / linear / norm / SDPA call:
+        # the teacher-forced per-layer parity test feeds each GPU layer these inputs
+        self.record = None
+
+    def _rec(self, name, *tensors):
+        if self.record is not None:
+            self.record[name] = tuple(t.detach().clone() for t in tensors)
 
     # ---- layers
     def lin(self, name, x):
@@ -129,6 +136,7 @@ class RefUNet:
         f = self.flags.get(name)
         if f and f["out_quant"]:
             y = FT.per_token(y, f["a_bit"])
+        self._rec(name, x, y)
         return y
 
     def conv(self, name, x, stride=1, padding=None):
@@ -137,11 +145,13 @@ class RefUNet:
             padding = w.shape[-1] // 2
         f = self.flags.get(name)
         quant = f is not None and f["quant"]
+        x_in = x
         if quant:
             x = self._act(f, x)
         y = self.ops.conv2d(x, w, self.sd.get(name + ".bias"), stride, padding)
         if quant:
             y = self._act(f, y)
+        self._rec(name, x_in, y)
         return y
 
     def _act(self, f, x):
@@ -150,10 +160,14 @@ class RefUNet:
         return FT.ACT[f["act"]](x, f["a_bit"])
 
     def gn(self, name, x, groups, eps):
-        return self.ops.group_norm(x, groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)
+        y = self.ops.group_norm(x, groups, self.sd[name + ".weight"], self.sd[name + ".bias"], eps)
+        self._rec(name, x, y)
+        return y
 
     def ln(self, name, x):
-        return self.ops.layer_norm(x, (x.shape[-1],), self.sd[name + ".weight"], self.sd[name + ".bias"], 1e-5)
+        y = self.ops.layer_norm(x, (x.shape[-1],), self.sd[name + ".weight"], self.sd[name + ".bias"], 1e-5)
+        self._rec(name, x, y)
+        return y
 
     # ---- blocks
     def resnet(self, p, x, temb):
@@ -179,6 +193,9 @@ class RefUNet:
         v = v.view(b, -1, heads, d).transpose(1, 2)
         o = self.ops.scaled_dot_product_attention(q, k, v, dropout_p=0.0, is_causal=False)
         o = o.transpose(1, 2).reshape(b, -1, heads * d).to(q.dtype)
+        if self.record is not None:
+            self._rec(p + ".sdpa", q.transpose(1, 2).reshape(b, -1, heads * d), k.transpose(1, 2).reshape(b, -1, heads * d),
+                      v.transpose(1, 2).reshape(b, -1, heads * d), o)
         return self.lin(p + ".to_out.0", o)
 
     def block(self, p, t, ctx, heads):

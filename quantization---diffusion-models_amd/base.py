@@ -223,15 +223,21 @@ class BaseAWQForDiffusion(nn.Module):
         sd = load_file(os.path.join(model_path, sub, "diffusion_pytorch_model.safetensors"))
         net.load_state_dict({k: v.to(device) for k, v in sd.items()}, strict=True)
         cpath = os.path.join(model_path, sub, "qdiff_codes.safetensors")
-        if os.path.exists(cpath):
-            codes = load_file(cpath)
-            for name, m in net.named_modules():
-                if isinstance(m, WxAxLinear) and f"{name}.qcodes" in codes:
-                    g, nb = codes[f"{name}.qmeta"].tolist()
-                    m.qcodes = codes[f"{name}.qcodes"].to(device)
-                    m.qscales = codes[f"{name}.qscales"].to(device)
-                    m.qgroup, m.n_bits_W = g, nb
-                    m.qfmt = "i4" if nb <= 4 else "i8"
+        codes = load_file(cpath) if os.path.exists(cpath) else {}
+        for name, m in net.named_modules():
+            if not isinstance(m, WxAxLinear):
+                continue
+            if f"{name}.qcodes" in codes:
+                g, nb = codes[f"{name}.qmeta"].tolist()
+                m.qcodes = codes[f"{name}.qcodes"].to(device)
+                m.qscales = codes[f"{name}.qscales"].to(device)
+                m.qgroup, m.n_bits_W = g, nb
+                m.qfmt = "i4" if nb <= 4 else "i8"
+                m._codes_ver = (m.weight.data_ptr(), m.weight._version)
+            else:
+                # a reference-written checkpoint holds only the dequantized fp16 buffers: re-derive
+                # the integer codes and keep them only if they reproduce the buffer bit for bit
+                rederive_codes(m, qc["bits"], qc["group_size"])
         if sub == "transformer":
             pipe = QDiffPipeline(transformer=net, class_name=cls_name, config={"_class_name": cls_name})
         else:
@@ -246,6 +252,25 @@ class BaseAWQForDiffusion(nn.Module):
             obj._loops = {}
         obj.quantized_components = comps
         return obj
+
+
+@torch.no_grad()
+def rederive_codes(m, n_bits, group_size):
+    """Integer codes of a loaded WxAxLinear whose checkpoint stored only ``weight`` (the
+    reference's format, base.py:530-582): RTN of the dequantized buffer with the same bits and
+    group (shrink rule included).  Attached only when dequantizing them gives back exactly the
+    stored buffer, so the GEMM operand is unchanged; otherwise the fp16 buffer stays the operand."""
+    from .fake_quant import quantize_weight_absmax_codes, shrink_group
+    if n_bits > 8 or m.in_features % 64 != 0:
+        return False
+    try:
+        g = shrink_group(m.in_features, group_size) if group_size > 0 else m.in_features
+    except ZeroDivisionError:
+        return False
+    codes, scales, wdq, g = quantize_weight_absmax_codes(m.weight, n_bits, g)
+    if not torch.equal(wdq.view(torch.int16), m.weight.view(torch.int16)):
+        return False
+    return m.set_codes(codes, scales, g, n_bits)
 
 
 def load_quantized_modules(module, bitWidth=4, group_size=128, act_bits=16, full_config=None):

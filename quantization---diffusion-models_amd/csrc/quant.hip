@@ -415,7 +415,10 @@ __global__ void __launch_bounds__(256) k_weight_tensor_apply(const f16* __restri
 extern "C" int qd_weight_quant(const void* w, int rows, int cols, int group, int n_bits,
                                int8_t* codes, void* scales, void* w_dq, void* stream) {
   QD_REQUIRE(w, "null weight");
-  QD_REQUIRE(n_bits >= 2 && n_bits <= 8, "weight n_bits must be in [2, 8] for int8 codes");
+  // the reference's quantize_weight_* accept any width (fake_quant.py:21-105); integer codes
+  // exist only up to 8 bits, wider widths produce the dequantized fp16 weight only
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "weight n_bits must be in [2, 16]");
+  QD_REQUIRE(n_bits <= 8 || !codes, "integer codes need n_bits <= 8 (pass codes = NULL for wider widths)");
   QD_REQUIRE(rows >= 0 && cols > 0 && group > 0, "bad shape");
   const long count = (long)rows * cols;
   if (count == 0) return 0;
@@ -666,8 +669,11 @@ __global__ void k_smooth_scales(const float* __restrict__ wmax, const f16* __res
   if (i >= c) return;
   const float cl = clamp_min_f16();
   const float ws = fmaxf(wmax[i], cl);  // exact fp16 value
-  const f16 num = (f16)powf((float)act[i], ea);
-  const f16 den = (f16)powf(ws, eb);
+  // pow in f64, rounded to f32 then fp16: torch's Half pow(Scalar) result on these inputs
+  // (oracle/fake_quant_np.py smooth_scales, pinned to the reference's smooth_ln_fcs golden);
+  // an f32 powf differs from it by 1 fp16 ulp on a few channels
+  const f16 num = (f16)(float)pow((double)(float)act[i], (double)ea);
+  const f16 den = (f16)(float)pow((double)ws, (double)eb);
   const float s = fmaxf((float)(f16)((float)num / (float)den), cl);
   scales[i] = (f16)s;
   lnw[i] = (f16)((float)lnw[i] / s);

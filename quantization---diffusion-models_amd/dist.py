@@ -33,10 +33,20 @@ def shard_range(total, rank, world):
     return start, start + base + (1 if rank < extra else 0)
 
 
+def _host_staged():
+    """gloo (CPU tests, several ranks sharing one GPU) moves HIP tensors through host memory."""
+    return dist.get_backend() != "nccl"
+
+
 def broadcast_context(ctx, src=0):
     """Broadcast the text-embedding batch from `src` (in place).  No-op at world size 1."""
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.broadcast(ctx, src)
+        if ctx.is_cuda and _host_staged():
+            h = ctx.cpu()
+            dist.broadcast(h, src)
+            ctx.copy_(h)
+        else:
+            dist.broadcast(ctx, src)
     return ctx
 
 
@@ -49,9 +59,33 @@ def gather_latents(lat, dst=0):
         out = [torch.empty_like(lat) for _ in range(world)]
         dist.all_gather(out, lat)
         return torch.cat(out) if dist.get_rank() == dst else None
-    out = [torch.empty_like(lat) for _ in range(world)] if dist.get_rank() == dst else None
-    dist.gather(lat, out, dst)
-    return torch.cat(out) if dist.get_rank() == dst else None
+    src = lat.cpu() if lat.is_cuda else lat
+    out = [torch.empty_like(src) for _ in range(world)] if dist.get_rank() == dst else None
+    dist.gather(src, out, dst)
+    if dist.get_rank() != dst:
+        return None
+    return torch.cat(out).to(lat.device)
+
+
+def share_gemm_table(warm_eager, rank=None, world=None):
+    """Rank 0 tunes every GEMM shape of the step (`warm_eager()`: one eager step, no collectives)
+    and broadcasts its kernel table; the other ranks install it before their own warm-up, so all
+    ranks run the same kernel variants and compute bit-identical results for identical inputs
+    (the tuner times candidates, and split-K / halo candidates change the fp32 summation order).
+    Returns the shared table."""
+    from . import kernels as K
+    rank = dist.get_rank() if rank is None else rank
+    world = dist.get_world_size() if world is None else world
+    if world <= 1:
+        warm_eager()
+        return K.export_table()
+    if rank == 0:
+        warm_eager()
+    box = [K.export_table() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    if rank != 0:
+        K.import_table(box[0])
+    return box[0]
 
 
 def shard_context(full_ctx, rank, world):

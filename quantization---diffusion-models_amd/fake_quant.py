@@ -61,7 +61,9 @@ def quantize_weight_absmax_codes(w, n_bits=8, group_size=0):
     if w2.dim() != 2 or (group_size <= 0 and w.dim() != 2):
         raise AssertionError("w.dim() == 2")  # fake_quant.py:41
     codes, scales, wdq = K.weight_quant(w2, g, n_bits)
-    return codes.reshape(shape), scales.reshape(*shape[:-1], shape[-1] // g), wdq.reshape(shape), g
+    if codes is not None:  # None above 8 bits: dequantized weight only
+        codes = codes.reshape(shape)
+    return codes, scales.reshape(*shape[:-1], shape[-1] // g), wdq.reshape(shape), g
 
 
 @torch.no_grad()
@@ -182,9 +184,21 @@ class WxAxLinear(nn.Module):
 
     # the fused-GEMM weight operand: (tensor, fmt, scales, group)
     def gemm_weight(self):
+        """Integer codes while they still describe ``weight``; after a load_state_dict or an
+        in-place edit of the buffer (data pointer / version changed) the codes are stale and
+        dropped, and the GEMM runs on the fp16 buffer (the reference's own operand)."""
         if self.qcodes is not None:
-            return self.qcodes, self.qfmt, self.qscales, self.qgroup
+            if getattr(self, "_codes_ver", None) == (self.weight.data_ptr(), self.weight._version):
+                return self.qcodes, self.qfmt, self.qscales, self.qgroup
+            self.drop_codes()
         return self.weight, "f16", None, 0
+
+    def drop_codes(self):
+        self.qcodes = None
+        self.qscales = None
+        self.qfmt = "f16"
+        self.qgroup = 0
+        self._codes_ver = None
 
     def set_codes(self, codes, scales, group, n_bits):
         """Attach integer codes for the fused-dequant GEMM (int4 packed when n_bits <= 4)."""
@@ -200,6 +214,7 @@ class WxAxLinear(nn.Module):
         self.qscales = scales.reshape(self.out_features, K_ // group).contiguous()
         self.qgroup = group
         self.n_bits_W = n_bits
+        self._codes_ver = (self.weight.data_ptr(), self.weight._version)
         return True
 
     @torch.no_grad()
@@ -250,7 +265,7 @@ class WxAxLinear(nn.Module):
         else:
             raise ValueError(f"Invalid weight_quant: {weight_quant}")  # fake_quant.py:252-253
         new.weight.copy_(wdq)
-        if codes is not None:
+        if codes is not None and n_bits_W <= 8:
             new.set_codes(codes, scales, g, n_bits_W)
         new.weight_quant_name = weight_quant
         if module.bias is not None:

@@ -125,6 +125,8 @@ def weight_quant(w2d, group, n_bits, want_codes=True, want_scales=True, want_dq=
     """Row-group absmax RTN of a [rows, cols] fp16 weight (fake_quant.py:21-105)."""
     _chk(w2d, "weight")
     rows, cols = w2d.shape
+    if n_bits > 8:
+        want_codes = False  # integer codes exist up to 8 bits; wider widths: dequantized weight only
     codes = torch.empty(rows, cols, dtype=torch.int8, device=w2d.device) if want_codes else None
     ngr = 1 if group > cols else cols // group
     scales = torch.empty(rows, ngr, dtype=torch.float16, device=w2d.device) if want_scales else None
@@ -167,6 +169,54 @@ HALO_VARIANTS = (200, 201)  # 3x3 conv with the activation halo staged once per 
 _TUNE = {}
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
 _OVERRIDE = None  # benchmarking: force every GEMM onto one qd_gemm_force id (see force_gemm)
+
+
+def _tuplify(v):
+    return tuple(_tuplify(e) for e in v) if isinstance(v, list) else v
+
+
+def _listify(v):
+    return [_listify(e) for e in v] if isinstance(v, (tuple, list)) else v
+
+
+def export_table():
+    """The tuned GEMM table as JSON-able [key, choice] pairs (keys are tuples of ints / strs)."""
+    return [[_listify(k), _listify(c)] for k, c in _TUNE.items()]
+
+
+def import_table(entries, overwrite=True):
+    """Install [key, choice] pairs (export_table()'s format): every GEMM whose key is present
+    runs that kernel variant without timing anything, so processes / ranks that share a table
+    compute bit-identical results (split-K and halo candidates change the fp32 summation order)."""
+    n = 0
+    for k, c in entries:
+        key = _tuplify(k)
+        if overwrite or key not in _TUNE:
+            _TUNE[key] = tuple(c) if c is not None else None
+            n += 1
+    return n
+
+
+def save_table(path):
+    import json
+    with open(path, "w") as f:
+        json.dump({"device_arch": device_arch(), "entries": export_table()}, f)
+
+
+def load_table(path, overwrite=True):
+    import json
+    with open(path) as f:
+        d = json.load(f)
+    return import_table(d["entries"], overwrite)
+
+
+# A committed table (tuned on an MI355X by scripts/tune_table.py) makes kernel choices - and
+# therefore results - reproducible across processes; shapes it does not cover are tuned at
+# their first eager call.  QD_GEMM_TABLE=<path> selects another file, QD_GEMM_TABLE=none none.
+_TABLE_PATH = os.environ.get("QD_GEMM_TABLE", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "gemm_table.json"))
+if _TABLE_PATH.lower() != "none" and os.path.exists(_TABLE_PATH):
+    load_table(_TABLE_PATH)
 
 
 def force_gemm(variant=None):
@@ -628,6 +678,9 @@ def channel_absmax_accum(x2d, ws, sum_buf=None, amax_out=None):
 def smooth_fold(ln_weight, ln_bias, fc_weights, act_mean, alpha=0.8):
     """quantizer_SQ.smooth_ln_fcs on device (in place); returns the fp16 scales."""
     c = ln_weight.numel()
+    _chk(ln_weight, "ln weight")  # read as fp16 by the kernel (an fp32 LayerNorm is rejected)
+    if ln_bias is not None:
+        _chk(ln_bias, "ln bias")
     for w in fc_weights:
         _chk(w, "fc weight")
         if w.shape[1] != c:

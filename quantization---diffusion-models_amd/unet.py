@@ -441,8 +441,16 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
     if q:
         n = x.shape[0]
-        amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
-        y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)
+        hh, ww = (2 * x.shape[1], 2 * x.shape[2]) if upsample else (x.shape[1], x.shape[2])
+        ho, wo = (hh + 2 * pad - layer.kernel_size[0]) // stride + 1, (ww + 2 * pad - layer.kernel_size[1]) // stride + 1
+        if (ho * wo) % 64:
+            # the GEMM's amax epilogue needs whole-sample 64-row wave tiles; other output sizes
+            # (never the UNet's: >= 8x8 per sample) reduce the amax in a separate pass
+            y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias)
+            amax = K.act_absmax(y, "per_channel", K.NHWC)
+        else:
+            amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
+            y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)
         if defer and residual is None:
             return y, (amax, q, chan_add)
         return K.fq_finalize(y, amax, q, residual=residual, chan_add=chan_add, out=y)

@@ -50,6 +50,15 @@ def _worker(rank, world, port, q):
             assert torch.equal(out, ref)
         else:
             assert out is None
+        # GEMM table sharing (bench.py before warm-up): rank 0 tunes, every rank ends with its table
+        from qdiff import kernels as K
+        key = ("linear", 4096, 320, 320, 320, 1, 0, ("f16",))
+
+        def warm():
+            K._TUNE[key] = (0, 103)
+
+        shared = qdist.share_gemm_table(warm, rank, world)
+        assert K._TUNE.get(key) == (0, 103) and [list(key[:7]) + [["f16"]], [0, 103]] in shared
         # bench.py timing reduction: MAX over ranks
         t = torch.tensor([1.0 + rank], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -86,3 +95,48 @@ def test_gloo_world2_broadcast_shard_gather():
     for p in procs:
         p.join(timeout=30)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_table_export_import_roundtrip(tmp_path):
+    sys.path.insert(0, ROOT)
+    import json
+    import qdiff_boot  # noqa: F401
+    from qdiff import kernels as K
+    saved = dict(K._TUNE)
+    try:
+        K._TUNE.clear()
+        K._TUNE[("conv", 8, 64, 64, 320, 320, 3, 3, 1, 1, False, 5)] = (0, 200)
+        K._TUNE[("linear", 8, 1280, 320, 320, 1, 0, ("i8", "f16"))] = None
+        blob = json.dumps(K.export_table())
+        K._TUNE.clear()
+        assert K.import_table(json.loads(blob)) == 2
+        assert K._TUNE[("conv", 8, 64, 64, 320, 320, 3, 3, 1, 1, False, 5)] == (0, 200)
+        assert K._TUNE[("linear", 8, 1280, 320, 320, 1, 0, ("i8", "f16"))] is None
+    finally:
+        K._TUNE.clear()
+        K._TUNE.update(saved)
+
+
+def test_bench_gpus_n_launches_n_ranks(monkeypatch):
+    """`python bench.py --gpus N` outside torchrun starts N ranks through torch.distributed.run
+    (127.0.0.1 rendezvous) from a parent that never touches the GPU, and returns their status."""
+    import subprocess
+    sys.path.insert(0, ROOT)
+    import bench
+    calls = []
+
+    def fake_call(cmd, env=None):
+        calls.append((cmd, env))
+        return 3
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "2"])
+    with pytest.raises(SystemExit) as ei:
+        bench.main()
+    assert ei.value.code == 3
+    cmd, env = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[-4:] == ["--gpus", "4", "--steps", "2"]
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert not torch.cuda.is_initialized()

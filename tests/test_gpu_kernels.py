@@ -121,9 +121,11 @@ def test_smooth_fold_and_hook(golden, dev):
     lnb = torch.from_numpy(s["ln_b_in"]).to(dev)
     fcs = [torch.from_numpy(s[f"fc{i}_w_in"]).to(dev) for i in range(3)]
     k.smooth_fold(lnw, lnb, fcs, torch.from_numpy(s["act"]).to(dev), 0.8)
-    # powf on device vs the reference's pow: at most a handful of 1-ulp scale differences
-    nbad = int((lnw.cpu().numpy() != s["ln_w_out"]).sum())
-    assert nbad <= 3, nbad
+    # f64 pow on device, rounded like torch's Half pow: every bit equal to the reference
+    assert same_bits(lnw.cpu().numpy(), s["ln_w_out"])
+    assert same_bits(lnb.cpu().numpy(), s["ln_b_out"])
+    for i in range(3):
+        assert same_bits(fcs[i].cpu().numpy(), s[f"fc{i}_w_out"])
     x = torch.from_numpy(s["hook_x"].reshape(-1, 320)).to(dev)
     ws = torch.empty(320, dtype=torch.float32, device=dev)
     sm = torch.zeros(320, dtype=torch.float32, device=dev)
