@@ -29,6 +29,9 @@ sys.path.insert(0, ROOT)
 
 UNET_GFLOP_PER_SAMPLE = 803.3   # SURVEY.md Appendix B (analytic, SD1.5 512^2)
 PEAK_F16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: dense BF16/FP16 MFMA
+PEAK_I8_TOPS = 5000.0           # MI355X_MICROARCH.md: I8 MFMA = 2x the BF16 rate per clock (dense)
+# int8-eligible (quantized GEMM) and fp16 (attention) FLOP per SD1.5 512^2 image
+SD15_I8_FLOP_PER_IMAGE, SD15_F16_FLOP_PER_IMAGE = 67.72e12, 12.61e12
 PEAK_HBM_GBS = 8000.0
 
 
@@ -40,7 +43,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=4, help="prompts per GPU")
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--denoise-steps", type=int, default=50)
-    ap.add_argument("--mode", default=None, choices=["w8a8-sq", "w8a8", "w4a16", "fp16"],
+    ap.add_argument("--mode", default=None, choices=["w8a8-sq", "w8a8", "w4a16", "fp16", "w8a8-sq-int8", "w8a8-int8"],
                     help="default: w8a8-sq (sd15), w4a16 (sd35, SURVEY config C5)")
     ap.add_argument("--model", default="sd15", choices=["sd15", "sdxl", "sd35"],
                     help="secondary lines: sdxl = SDXL W8A8 1024^2, 2 prompts per GPU (config C4); "
@@ -69,6 +72,9 @@ def parse():
 QCFG = {
     "w8a8-sq": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
     "w8a8": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
+    # the int8-MFMA W8A8 mode: same config, int8 codes on v_mfma_i32_16x16x64_i8
+    "w8a8-sq-int8": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
+    "w8a8-int8": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
     "w4a16": dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
 }
 
@@ -102,22 +108,23 @@ def build_model(args, dev):
         return model
     from qdiff.models import StableDiffusion1_x
     model = StableDiffusion1_x.from_pretrained("synthetic:sd15", device=dev, seed=0)
-    sd_cpu = None
     if args.mode != "fp16":
         qc = dict(QCFG[args.mode])
-        if args.mode == "w8a8-sq":
-            model.quantize(quant_config=qc, quantType="sq", quantUnet=True,
+        i8 = args.mode.endswith("-int8")
+        if args.mode.startswith("w8a8-sq"):
+            model.quantize(quant_config=qc, quantType="sq", quantUnet=True, int8_mfma=i8,
                            calibration=dict(n_samples=args.batch, batch_size=args.batch,
                                             num_inference_steps=args.calib_steps))
         else:
-            model.quantize(quant_config=qc, quantUnet=True)
+            model.quantize(quant_config=qc, quantUnet=True, int8_mfma=i8)
     return model
 
 
-def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320):
+def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320, int8=False):
     """Time the largest conv implicit GEMM of the UNet (SD1.5 at CFG batch 8: down/up block 0
     conv 320->320 3x3 @ 64x64, M = 32768, N = 320, K = 2880; SDXL at CFG batch 4: the same conv
-    at 128x128, M = 65536) with HIP events on its stream."""
+    at 128x128, M = 65536) with HIP events on its stream.  int8: the int8-MFMA mode's kernel
+    (qd_conv2d_i8 on per-sample int8 codes) against the int8 MFMA peak."""
     import torch
     from qdiff import kernels as K
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -125,33 +132,46 @@ def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320):
     wt = (torch.randn(c, 3, 3, c, generator=g) / 54).half().to(dev)
     b = torch.zeros(c, dtype=torch.float16, device=dev)
     amax = torch.empty(n * c, dtype=torch.float32, device=dev)
+    if int8:
+        xq, sa = K.quant_samples_i8(x)
+        wq, sw16, _ = K.weight_quant(wt.view(c, -1).contiguous(), 9 * c, 8, want_dq=False)
+        wq, sw = wq.view(c, 3, 3, c), sw16.float().view(-1).contiguous()
+        run = lambda: K.conv2d_i8(xq, sa, wq, sw, c, 1, 1, bias=b)
+    else:
+        run = lambda: K.conv2d_nhwc(x, wt, c, 1, 1, bias=b, amax=amax)
     for _ in range(3):
-        K.conv2d_nhwc(x, wt, c, 1, 1, bias=b, amax=amax)
+        run()
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(iters):
-        K.conv2d_nhwc(x, wt, c, 1, 1, bias=b, amax=amax)
+        run()
     e1.record(st)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
     flops = 2.0 * (n * h * w) * c * (9 * c)
     tflops = flops / (ms * 1e-3) / 1e12
-    choice = _conv_choice((n, h, w, c))
-    tr = pmc_traffic(choice["variant"] if choice else None) if (n, h, w, c) == (8, 64, 64, 320) else None
-    return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": (tr or {}).get("hbm_bytes_per_launch"),
+    peak = PEAK_I8_TOPS if int8 else PEAK_F16_TFLOPS
+    choice = _conv_choice((n, h, w, c), "conv_i8" if int8 else "conv")
+    tr = pmc_traffic(choice["variant"] if choice else None) if (n, h, w, c) == (8, 64, 64, 320) and not int8 else None
+    return {"bound": "mfma", "achieved": round(tflops, 1), "peak": peak, "unit": "TOP/s" if int8 else "TFLOP/s",
+            "frac": round(tflops / peak, 4), "traffic": (tr or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": tr,
-            "kernel": f"conv3x3 {c}->{c} @{h}x{w} b{n} (M={n * h * w},N={c},K={9 * c}) implicit GEMM",
+            "kernel": f"conv3x3 {c}->{c} @{h}x{w} b{n} (M={n * h * w},N={c},K={9 * c}) implicit GEMM"
+                      + (" int8 x int8 -> int32 (v_mfma_i32_16x16x64_i8)" if int8 else ""),
             "kernel_choice": choice,
             "avg_us": round(ms * 1e3, 2)}
 
 
-def _conv_choice(shape=(8, 64, 64, 320)):
+def _conv_choice(shape=(8, 64, 64, 320), kind="conv"):
     """GEMM family chosen for the dominant conv ((weight op, qd_gemm_force id); >= 100 = LDS-DMA)."""
     from qdiff import kernels as K
     n, h, w, c = shape
     for key, ch in K.gemm_choices().items():
+        if kind == "conv_i8":
+            if key[:8] == ("conv_i8", n, h, w, c, c, 3, 3):
+                return {"variant": ch, "family": "k_gemm_dma<I8>"} if ch else None
+            continue
         if key[:8] == ("conv", n, h, w, c, c, 3, 3):
             fam = ("k_gemm_pp" if ch and ch[1] >= 300 else "k_conv_halo" if ch and ch[1] >= 200 else
                    "k_gemm_dma" if ch and ch[1] >= 100 else "k_gemm")
@@ -313,22 +333,32 @@ def main():
     if rank == 0:
         assert out is not None and torch.isfinite(out.float()).all(), "non-finite latents"
         log(f"timed {args.steps} steps: {dt:.3f}s")
-        roof = dominant_kernel_roofline(dev)
+        int8 = args.mode.endswith("-int8")
+        roof = dominant_kernel_roofline(dev, int8=int8)
         evals_per_s = value * args.denoise_steps  # UNet evals per image per step: 50 steps at CFG batch 2
         path_tflops = evals_per_s * 2 * UNET_GFLOP_PER_SAMPLE / 1e3
+        # north_star's target metric: images/s against the int8-blended bound of one GPU
+        # (int8-eligible GEMM FLOP at the int8 peak + attention FLOP at the fp16 peak)
+        t_min = SD15_I8_FLOP_PER_IMAGE / (PEAK_I8_TOPS * 1e12) + SD15_F16_FLOP_PER_IMAGE / (PEAK_F16_TFLOPS * 1e12)
         line = {
             "metric": "images/sec SD1.5 W8A8 512x512 50-step",
             "value": round(value, 4), "unit": "images/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+            "scaling": "weak", "vs_baseline": None, "dtype": "i8 (int32 accumulate) + f16" if int8 else "f16",
             "data": "synthetic (random-init SD1.5 UNet weights N(0,1/fan_in), synthetic text embeddings and latents)",
-            "config": {"workload": f"SD1.5 UNet {args.mode} fake-quant, {args.res}x{args.res}, {B} prompts/GPU "
+            "config": {"workload": f"SD1.5 UNet {args.mode} {'int8-MFMA' if int8 else 'fake-quant'}, "
+                                   f"{args.res}x{args.res}, {B} prompts/GPU "
                                    f"(CFG batch {2 * B}), {args.denoise_steps} DDIM steps, HIP graph per step",
                        "global_batch": B * world, "seq_len": 77, "parallelism": f"dp{world}"},
             "roofline": roof,
             "path_roofline": {"achieved": round(path_tflops / world, 1), "peak": PEAK_F16_TFLOPS,
                               "unit": "TFLOP/s per GPU", "frac": round(path_tflops / world / PEAK_F16_TFLOPS, 4),
                               "flop_per_image": 2 * args.denoise_steps * UNET_GFLOP_PER_SAMPLE * 1e9},
+            "int8_blended_roofline": {"achieved": round(value / world, 4), "bound": round(1.0 / t_min, 2),
+                                      "unit": "images/s per GPU", "frac": round(value / world * t_min, 4),
+                                      "target_frac": 0.40,
+                                      "basis": "67.72 TFLOP int8-eligible @ 5.0 POPS + 12.61 TFLOP attention @ 2.5 PF "
+                                               "per 512^2 image (SURVEY 8d)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")

@@ -148,6 +148,49 @@ int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n
                    const void* residual, const void* chan_add, int chan_add_ld, void* out,
                    void* stream);
 
+/* ---------------- int8-MFMA W8A8 mode ------------------------------------------------ */
+/* The reference's W8A8 is fake-quant (fp16 F.linear / F.conv2d on dequantized operands,
+ * fake_quant.py:223, 339) with granularities that vary along K (conv weights per (Co, Ci, kh),
+ * activations per (n, c): fake_quant.py:86-93, 123-131), so an integer dot product cannot
+ * reproduce it.  This mode re-granularizes to what factors out of the dot product and computes
+ * on v_mfma_i32_16x16x64_i8: weights per output channel, activations per token (linear) or per
+ * sample (conv), codes from the reference's RTN recipe (fake_quant.py:44-46: s = half(half(amax)
+ * / 127), q = rint(half(x / s))), exact int32 sums, then y = half(((float)acc * sa) * sw + bias)
+ * and the same epilogue flags as the fp16 GEMM.  Tolerance vs the fake-quant path: DESIGN.md. */
+/* int8 codes of each row of x [rows][ldx] (c values, dynamic per token) -> y [rows][ldy],
+ * scales[rows] fp32 (the fp16 scale widened). */
+int qd_quant_rows_i8(const void* x, long rows, int c, int ldx, int8_t* y, int ldy, float* scales, void* stream);
+/* int8 codes of n samples of per_sample contiguous values each (one scale per sample: the
+ * conv-input granularity of this mode) -> y, scales[n]; amax_ws fp32 [n] workspace, zeroed by the
+ * call unless amax_zeroed (a pooled buffer zeroed once per step). */
+int qd_quant_samples_i8(const void* x, int n, long per_sample, int8_t* y, float* scales, float* amax_ws,
+                        int amax_zeroed, void* stream);
+/* y[M, N] = (x_i8[M, K] . w_i8[N, K]^T) * sa[m] * sw[n] (+ epilogue), K % 64 == 0, lda % 16 == 0;
+ * sa fp32 [M], sw fp32 [N] (16-B aligned).  Epilogue flags / rows_per_sample / workspace as
+ * qd_linear_fwd (workspace size: qd_gemm_i8_workspace).  qd_gemm_force 110..113 picks the tile. */
+int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                 const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                 int rows_per_sample, float* ws, long ws_elems, void* stream);
+/* NHWC implicit-GEMM conv on int8 codes: x_i8 [N, H, W, Ci_pad] (Ci_pad % 64 == 0), one scale
+ * per sample sa[N]; w_i8 [Co][kh][kw][Ci_pad], sw[Co]; geometry / epilogue as qd_conv2d_fwd. */
+int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w, int ci, int ci_pad, const void* wt,
+                 const float* sw, int co, int kh, int kw, int stride, int pad, int upsample2x, const void* bias,
+                 const void* residual, void* y, int epi, float* amax, float* ws, long ws_elems, void* stream);
+/* fp32 elements of split-K workspace qd_linear_i8 / qd_conv2d_i8 plan for this shape (K = codes
+ * per row; conv: M = N*Ho*Wo, K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo). */
+long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, int epi);
+/* qd_groupnorm / qd_groupnorm_fq_in whose output is written as the int8 codes of the conv that
+ * consumes it (one scale per sample, scales[n] fp32) instead of fp16: the fp16 GroupNorm(+SiLU)
+ * value is formed exactly as qd_groupnorm does, then coded (= qd_quant_samples_i8 of it) in the
+ * same pass.  x2 (concat) and in_amax / cadd (virtual finalized input) as the fp16 entry points;
+ * ws: qd_groupnorm_workspace(). */
+int qd_groupnorm_i8(const void* x, const void* x2, int c1, const float* in_amax, int in_bits, const void* cadd,
+                    int cadd_ld, int n, int hw, int c, int groups, float eps, const void* gamma, const void* beta,
+                    int silu, int8_t* y8, float* scales, float* ws, void* stream);
+/* qd_layernorm with per-row int8 output (= qd_quant_rows_i8 of the fp16 LayerNorm output). */
+int qd_layernorm_i8(const void* x, int rows, int c, float eps, const void* gamma, const void* beta, int8_t* y8,
+                    float* scales, void* stream);
+
 /* ---------------- normalisation / activations (diffusers UNet ops, fp16 I/O) --------- */
 /* GroupNorm(groups, eps, affine) on NHWC [N, HW, C] (+ SiLU) (+ per-(n, c) fake-quant of the
  * result with q_bits, i.e. the input quant of the conv that consumes it, fused because a

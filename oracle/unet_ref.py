@@ -19,12 +19,15 @@ import torch.nn.functional as F
 
 from . import fake_quant_np as FQ
 from . import fake_quant_torch as FT
+from . import int8_ref as I8
+
+I8_MIN_ROWS = 64  # the product's rule: linears with fewer input rows keep the fp16 MFMA (unet.py)
 
 F16 = torch.float16
 
 
 # ------------------------------------------------------------------ weight quantization
-def quantize_state_dict(sd, qc, backend="torch"):
+def quantize_state_dict(sd, qc, backend="torch", skip=()):
     """Return (qsd, flags): fake-quantized fp16 weights and per-layer activation flags.
 
     qc keys (AwqConfig): w_bit, a_bit, q_group_size, weight_quant_type, weight_quant_conv_type,
@@ -44,6 +47,14 @@ def quantize_state_dict(sd, qc, backend="torch"):
             continue
         name = key[: -len(".weight")]
         child = name.split(".")[-1]
+        if name in skip:  # int8-mode layer: its weight is already the per-channel int8 dequant
+            if w.dim() == 2:
+                flags[name] = {"kind": "linear", "out_quant": "k_proj" in child or "v_proj" in child or
+                               "q_proj" in child, "a_bit": qc["a_bit"]}
+            else:
+                flags[name] = {"kind": "conv", "act": qc.get("act_quant_conv_type", "per_channel"), "quant": False,
+                               "a_bit": qc["a_bit"]}
+            continue
         w = w.to(F16).contiguous()
         if w.dim() == 2:
             wt = qc.get("weight_quant_type", "group")
@@ -110,15 +121,21 @@ class RefUNet:
     implementation (MFMA) computes.  The spread between the two variants measures how much the
     fake-quant network amplifies ulp-level differences (tests/test_gpu_unet.py)."""
 
-    def __init__(self, cfg, sd, qc=None, variant="half"):
-        """cfg: dict of UNetConfig fields; sd: {key: fp16 cpu tensor}; qc: AwqConfig dict or None."""
+    def __init__(self, cfg, sd, qc=None, variant="half", int8=False):
+        """cfg: dict of UNetConfig fields; sd: {key: fp16 cpu tensor}; qc: AwqConfig dict or None.
+        int8=True: the int8-MFMA W8A8 mode (oracle/int8_ref.py) on every eligible layer."""
         self.cfg = cfg
         self.ops = _Fp32Ops if variant == "fp32" else F
         sd = {k: v.detach().to("cpu", F16).contiguous() for k, v in sd.items()}
+        self.i8 = {}
+        if int8:
+            sd = self._int8_weights(sd)
         if qc is not None:
-            self.sd, self.flags = quantize_state_dict(sd, qc)
+            self.sd, self.flags = quantize_state_dict(sd, qc, skip=set(self.i8))
         else:
             self.sd, self.flags = sd, {}
+        for name in self.i8:
+            self.flags[name] = dict(self.flags.get(name, {}), int8=True)
         self.hooks = None  # optional {linear name: callable(x)} for calibration
         # optional {layer name: (input, output)} of every conv / linear / norm / SDPA call:
         # the teacher-forced per-layer parity test feeds each GPU layer these inputs
@@ -128,10 +145,48 @@ class RefUNet:
         if self.record is not None:
             self.record[name] = tuple(t.detach().clone() for t in tensors)
 
+    def _int8_weights(self, sd):
+        """Per-output-channel int8 codes of every eligible layer (the product's rule: linear
+        K % 64 == 0; conv Ci_pad % 64 == 0 and Co % 8 == 0); the state dict gets their
+        dequantized values (the buffers the product's modules hold in this mode)."""
+        out = dict(sd)
+        for key, w in sd.items():
+            if not key.endswith(".weight") or w.dim() not in (2, 4):
+                continue
+            name = key[: -len(".weight")]
+            if w.dim() == 2:
+                if w.shape[1] % 64:
+                    continue
+                q, sc = I8.weight_rows_i8(w.numpy())
+                self.i8[name] = ("linear", q, sc)
+                out[key] = torch.from_numpy(I8.weight_rows_dequant(w.numpy()))
+            else:
+                co, ci, kh, kw = w.shape
+                if ((ci + 7) // 8 * 8) % 64 or co % 8:
+                    continue
+                wk = w.numpy().transpose(0, 2, 3, 1).reshape(co, -1)
+                q, sc = I8.weight_rows_i8(wk)
+                deq = I8.weight_rows_dequant(wk).reshape(co, kh, kw, ci)
+                self.i8[name] = ("conv", q.reshape(co, kh, kw, ci).transpose(0, 3, 1, 2).copy(), sc)
+                out[key] = torch.from_numpy(deq.transpose(0, 3, 1, 2).copy())
+        return out
+
     # ---- layers
     def lin(self, name, x):
         if self.hooks is not None and name in self.hooks:
             self.hooks[name](x)
+        i8 = self.i8.get(name)
+        if i8 is not None and x.numel() // x.shape[-1] >= I8_MIN_ROWS:
+            x2 = x.reshape(-1, x.shape[-1]).numpy()
+            xq, sa = I8.quant_rows_i8(x2)
+            b = self.sd.get(name + ".bias")
+            y = torch.from_numpy(I8.linear_i8(xq, sa, i8[1], i8[2], None if b is None else b.numpy()))
+            y = y.view(*x.shape[:-1], -1)
+            f = self.flags.get(name)
+            if f and f.get("out_quant"):
+                y = FT.per_token(y, f["a_bit"])
+            self._rec(name, x, y)
+            return y
         y = self.ops.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias"))
         f = self.flags.get(name)
         if f and f["out_quant"]:
@@ -143,6 +198,13 @@ class RefUNet:
         w = self.sd[name + ".weight"]
         if padding is None:
             padding = w.shape[-1] // 2
+        i8 = self.i8.get(name)
+        if i8 is not None:
+            xq, sa = I8.quant_samples_i8(x.numpy())
+            b = self.sd.get(name + ".bias")
+            y = torch.from_numpy(I8.conv2d_i8(xq, sa, i8[1], i8[2], None if b is None else b.numpy(), stride, padding))
+            self._rec(name, x, y)
+            return y
         f = self.flags.get(name)
         quant = f is not None and f["quant"]
         x_in = x

@@ -60,12 +60,19 @@ SIGNATURES = {
     "qd_copy_rows": [P, I, P, I, I64, I, I64, I64, P],
     "qd_unpatchify": [P, I, I, I, I, I, P, P],
     "qd_cfg_euler_step": [P, P, I, I64, F, P, P, P, P],
+    "qd_quant_rows_i8": [P, ctypes.c_long, I, I, P, I, P, P],
+    "qd_quant_samples_i8": [P, I, ctypes.c_long, P, P, P, I, P],
+    "qd_linear_i8": [P, P, I, I, I, P, P, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
+    "qd_conv2d_i8": [P, P, I, I, I, I, I, P, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
+    "qd_groupnorm_i8": [P, P, I, P, I, P, I, I, I, I, I, F, P, P, I, P, P, P, P],
+    "qd_layernorm_i8": [P, I, I, F, P, P, P, P, P],
 }
 
 # size queries (no status code)
 QUERIES = {
     "qd_gemm_workspace": ([I, I, I, I, I, I], ctypes.c_long),
     "qd_groupnorm_workspace": ([I, I, I, I], I),
+    "qd_gemm_i8_workspace": ([I, I, I, I, I], ctypes.c_long),
 }
 
 _lib = None

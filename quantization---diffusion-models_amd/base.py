@@ -83,8 +83,10 @@ class BaseAWQForDiffusion(nn.Module):
                  quantText=True, quantVisionProjection=False, quantTextProjection=False, quantUnet=False,
                  quantTextEncoder=False, quantVAE=False, quantTransformer=False, diffusion_model=True,
                  codeBookQuantInd=False, debugPlot=False, debugAttentionMap=False, debugSavePath="",
-                 calibration=None, **kwargs):
-        """base.py:215-528.  quantType 'awq' = RTN swap; 'sq' = SmoothQuant fold + swap."""
+                 calibration=None, int8_mfma=False, **kwargs):
+        """base.py:215-528.  quantType 'awq' = RTN swap; 'sq' = SmoothQuant fold + swap.
+        int8_mfma=True (this build, w_bit 8): the int8-MFMA W8A8 mode instead of the reference's
+        fake-quant arithmetic (re-granularized, tolerance-based parity)."""
         if quant_act and quant_config.get("version", "fake_act").lower() != "fake_act":
             print("With activation quantization set to True, you can only use the fake quant kernel fake_act! "
                   "Changing to that....")
@@ -97,7 +99,7 @@ class BaseAWQForDiffusion(nn.Module):
                       quant_act=quant_act, apply_clip=apply_clip, applyScale=applyScale, samples=samples,
                       calib_data_type=calib_data_type, blocksize=blocksize, quantUnet=quantUnet,
                       quantTextEncoder=quantTextEncoder, quantVAE=quantVAE, quantTransformer=quantTransformer,
-                      diffusion_model=True, codeBookQuantInd=codeBookQuantInd)
+                      diffusion_model=True, codeBookQuantInd=codeBookQuantInd, int8_mfma=int8_mfma)
         args = (self, None, None, qc.quantize_act, qc.weight_quant_conv_type, qc.weight_quant_type,
                 qc.act_quant_conv_type, qc.act_quant_conv_group_size, qc.w_bit, qc.wv_bit, qc.a_bit,
                 qc.q_group_size, qc.zero_point, qc.version, calib_data, split, text_column, duo_scaling)
@@ -109,6 +111,7 @@ class BaseAWQForDiffusion(nn.Module):
             raise NotImplementedError("Only awq and sq are supported for now.")
         self.quantizer.quantize(debugSavePath, debugPlot)
         self.is_quantized = True
+        self.int8_mfma = bool(int8_mfma)
         self._loops = {}
 
     # ---------------------------------------------------------------- generate

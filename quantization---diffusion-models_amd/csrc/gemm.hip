@@ -58,6 +58,15 @@ struct GemmArgs {
   float* part;
   int splits, kps;  // K per split (multiple of 64)
   unsigned a_bytes, b_bytes;
+  // int8 x int8 path (qd_linear_i8 / qd_conv2d_i8): A and B are int8 codes addressed through a
+  // "half view" (K, lda and Cip halved: two codes per fp16 slot), so the LDS-DMA loaders move
+  // them unchanged; the MFMA is v_mfma_i32_16x16x64_i8 and the int32 sums are scaled in the
+  // epilogue: y = half(((float)acc * sa[row]) * sw[col] + bias).  Split-K slabs hold the int32
+  // partial sums (exact), so every tile / split choice gives bit-identical outputs.
+  const float* sa;  // activation scale per row (sa_rps == 0) or per sa_rps consecutive rows
+  int sa_rps;
+  const float* sw;  // weight scale per output column (16-B aligned)
+  int i8;
 };
 
 constexpr int BK = 64;
@@ -293,6 +302,38 @@ __device__ __forceinline__ float rowgroup_max(float v) {
   v = fmaxf(v, __shfl_xor(v, 4, 64));
   v = fmaxf(v, __shfl_xor(v, 8, 64));
   return v;
+}
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// int8 path: C^T fragments of int32 sums -> scaled fp32 (or the raw int32 bits for a split-K slab)
+template <int TM, int TN, bool SPLIT>
+__device__ __forceinline__ void i8_scale(const GemmArgs& p, const i32x4 (&acc)[TM][TN], f32x4 (&out)[TM][TN], int m0,
+                                         int n0, int wm0, int wn0) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) out[i][j] = __builtin_bit_cast(f32x4, acc[i][j]);
+  } else {
+    float sa[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = min(m0 + wm0 + i * 16 + fr, p.M - 1);
+      sa[i] = p.sa[p.sa_rps ? m / p.sa_rps : m];
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn0 + j * 16 + fq * 4;
+      const f32x4 sw = n < p.N ? *reinterpret_cast<const f32x4*>(p.sw + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[i][j][r] = ((float)acc[i][j][r] * sa[i]) * sw[r];
+    }
+  }
 }
 
 // ---- shared epilogue ----------------------------------------------------------------------
@@ -641,7 +682,7 @@ constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt, int bkt = 64) {
              : 1;
 }
 
-template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT>
+template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false>
 __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
     k_gemm_dma(GemmArgs p) {
   constexpr int NT = 64 * WGM * WGN;
@@ -651,6 +692,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   constexpr int LDSZ = dma_lds_halves(BM, BN, ST, BKT);
   constexpr int KSUB = BKT / 32;  // 32-deep MFMA slices per stage
   static_assert(PIPE == 0 || (ST >= 3 && BKT == 64), "split-phase pipeline needs >= 3 stages of 64");
+  static_assert(!I8 || (BKT == 32 && PIPE == 0), "int8: one 64-code MFMA k-slice per 64-B LDS row");
   using AL = ADma<BM, NT, AMODE, BKT>;
   using BL = BDma<BN, NT, BKT>;
   __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
@@ -679,10 +721,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   bl.init(p, n0, wid);
 
   f32x4 acc[TM][TN];
+  i32x4 iacc[I8 ? TM : 1][I8 ? TN : 1];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) {
+      acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (I8) iacc[i][j] = (i32x4){0, 0, 0, 0};
+    }
 
   const int nk = (kend - kbeg + BKT - 1) / BKT;
 #pragma unroll
@@ -709,8 +755,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (I8)
+          iacc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, bf[j]),
+                                                             __builtin_bit_cast(i32x4, af[i]), iacc[i][j], 0, 0, 0);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      }
 #endif
   };
   auto sync = [&](int ahead) {  // own loads of the awaited tile landed, `ahead` later tiles in flight
@@ -767,6 +818,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if constexpr (I8) i8_scale<TM, TN, SPLIT>(p, iacc, acc, m0, n0, wm0, wn0);
   gemm_epilogue<BM, BN, NT, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
@@ -1160,12 +1212,34 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
       off[rr] = (long)m * p.N + n;
       s[rr] = *reinterpret_cast<const f32x4*>(p.part + off[rr]);
     }
-    for (int k = 1; k < p.splits; ++k) {
-      f32x4 t[RPT];
+    if (p.i8) {
+      // int32 partial sums (exact, any split order), then the int8 path's scaling
+      i32x4 si[RPT];
 #pragma unroll
-      for (int rr = 0; rr < RPT; ++rr) t[rr] = *reinterpret_cast<const f32x4*>(p.part + k * mn + off[rr]);
+      for (int rr = 0; rr < RPT; ++rr) si[rr] = __builtin_bit_cast(i32x4, s[rr]);
+      for (int k = 1; k < p.splits; ++k) {
+        i32x4 t[RPT];
 #pragma unroll
-      for (int rr = 0; rr < RPT; ++rr) s[rr] += t[rr];
+        for (int rr = 0; rr < RPT; ++rr) t[rr] = *reinterpret_cast<const i32x4*>(p.part + k * mn + off[rr]);
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) si[rr] += t[rr];
+      }
+      const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) {
+        const int m = min(mb + rg * RPT + rr, p.M - 1);
+        const float sa = p.sa[p.sa_rps ? m / p.sa_rps : m];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[rr][r] = ((float)si[rr][r] * sa) * sw[r];
+      }
+    } else {
+      for (int k = 1; k < p.splits; ++k) {
+        f32x4 t[RPT];
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) t[rr] = *reinterpret_cast<const f32x4*>(p.part + k * mn + off[rr]);
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) s[rr] += t[rr];
+      }
     }
 #pragma unroll
     for (int rr = 0; rr < RPT; ++rr) {
@@ -1237,7 +1311,7 @@ extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
                  (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
                  variant == 201 || (variant >= 300 && variant <= 304),
-             "qd_gemm_force: -1, 0..3, 100 + DMA variant, 200/201 halo conv, 300-304 ping-pong");
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113), 200/201 halo conv, 300-304 ping-pong");
   g_force = variant;
   return 0;
 }
@@ -1724,6 +1798,194 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
     run_gemm<AM_CONV>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
   } else {
     run_gemm<AM_CONV_ANY>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
+  }
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- int8 x int8 GEMM / conv (the int8-MFMA W8A8 mode) --------------------------------------
+// The reference's W8A8 is fake-quant (fp16 F.linear / F.conv2d on dequantized values,
+// fake_quant.py:223, 339); its granularities (conv weights per (Co, Ci, kh), activations per
+// (n, c)) vary along the reduction, so no integer dot product reproduces it.  This mode
+// re-granularizes to what factors out of an integer dot: weights per output channel (conv: over
+// (kh, kw, Ci); linear: over K), activations per token (linear) or per sample (conv), codes from
+// the reference's own RTN recipe, and runs v_mfma_i32_16x16x64_i8 (2x the fp16 MFMA rate) on the
+// LDS-DMA pipeline with 64-B rows (one 64-code MFMA k-slice per stage).  Exact int32
+// accumulation: every variant / split gives the same bits.
+template <int V, int AMODE, bool SPLIT>
+static void launch_i8_v(const GemmArgs& p, hipStream_t st) {
+  constexpr DmaVar d = kDmaC[V];
+  static_assert(d.bkt == 32 && d.pipe == 0, "int8 variants use the 64-B row layout");
+  const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
+  k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT, true><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+}
+
+template <int AMODE, bool SPLIT>
+static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
+  switch (var) {
+    case 10: launch_i8_v<10, AMODE, SPLIT>(p, st); break;
+    case 12: launch_i8_v<12, AMODE, SPLIT>(p, st); break;
+    case 13: launch_i8_v<13, AMODE, SPLIT>(p, st); break;
+    default: launch_i8_v<11, AMODE, SPLIT>(p, st); break;
+  }
+}
+
+// variant: qd_gemm_force 110..113 (DMA variants 10-13, the 64-B-row family), else a default by
+// N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
+static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu) {
+  int var = N % 160 == 0 ? 10 : 11;
+  if (g_force >= 110 && g_force <= 113) var = g_force - 100;
+  if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
+  if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
+  const DmaVar& d = kDmaC[var];
+  Plan pl{1, d.bm, d.bn, var, 1, Kh};
+  const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
+  const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
+  const int per_cu = std::max(1, std::min(by_lds, by_waves));
+  for (int sp = 2; sp <= 32 && !geglu && Kh % 32 == 0; ++sp) {
+    if ((Kh / 32) % sp != 0 || Kh / sp < 256) continue;
+    if (tiles_mn * sp > 256L * per_cu) break;
+    pl.splits = sp;
+    pl.kps = Kh / sp;
+  }
+  return pl;
+}
+
+template <int AMODE>
+static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
+  Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0);
+  if (pl.splits > 1 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N))) {
+    pl.splits = 1;
+    pl.kps = p.K;
+  }
+  p.splits = pl.splits;
+  p.kps = pl.kps;
+  if (pl.splits == 1) {
+    launch_i8<AMODE, false>(p, pl.var, st);
+  } else {
+    p.part = ws;
+    launch_i8<AMODE, true>(p, pl.var, st);
+    const int gx = (p.N + 255) / 256;
+    if ((long)gx * ((p.M + 15) / 16) >= 512) k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
+    else k_splitk_reduce<1><<<dim3(gx, (p.M + 3) / 4), 256, 0, st>>>(p);
+  }
+}
+
+static int check_i8(const GemmArgs& p) {
+  QD_REQUIRE(p.a && p.b && p.y && p.sa && p.sw, "null pointer");
+  QD_REQUIRE(p.M >= 0 && p.N > 0 && p.K > 0, "bad GEMM shape");
+  QD_REQUIRE(p.N % 8 == 0 && p.ldy % 8 == 0, "N and ldy must be multiples of 8");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(p.sw) & 15) == 0, "sw must be 16-B aligned");
+  QD_REQUIRE(!(p.epi & QD_EPI_RESIDUAL) || p.res, "residual epilogue without residual");
+  QD_REQUIRE(!(p.epi & QD_EPI_AMAX) || (p.amax && p.rows_per_sample > 0 && p.rows_per_sample % 64 == 0),
+             "amax epilogue needs rows_per_sample % 64 == 0");
+  QD_REQUIRE(!(p.epi & QD_EPI_GEGLU) || (!(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL)) && p.N % 32 == 0),
+             "GEGLU epilogue: N % 32 == 0, no residual / amax");
+  QD_REQUIRE(!(p.epi & QD_EPI_GELU_TANH) || !(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL | QD_EPI_GEGLU)),
+             "GELU-tanh epilogue: no residual / amax / GEGLU");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
+  QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
+  QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
+  QD_REQUIRE((double)p.N * p.K * 2 < 2147483648.0, "weight exceeds the 2 GiB buffer-addressing range");
+  return 0;
+}
+
+extern "C" long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, int epi) {
+  const Plan pl = plan_i8(M, N, K / 2, rows_per_sample, (epi & QD_EPI_AMAX) != 0, (epi & QD_EPI_GEGLU) != 0);
+  return split_ws_elems(pl, M, N);
+}
+
+extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                            const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                            int rows_per_sample, float* ws, long ws_elems, void* stream) {
+  QD_REQUIRE(K % 64 == 0 && K > 0, "int8 GEMM needs K % 64 == 0");
+  QD_REQUIRE(lda >= K && lda % 16 == 0, "int8 GEMM needs lda >= K, lda % 16 == 0");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
+             "x and w must be 16-B aligned");
+  GemmArgs p{};
+  p.a = (const f16*)x;
+  p.lda = lda / 2;
+  p.b = w;
+  p.bias = (const f16*)bias;
+  p.res = (const f16*)residual;
+  p.y = (f16*)y;
+  p.ldy = ldy;
+  p.amax = amax;
+  p.rows_per_sample = rows_per_sample;
+  p.M = M;
+  p.N = N;
+  p.K = K / 2;
+  p.epi = epi;
+  p.sa = sa;
+  p.sa_rps = 0;
+  p.sw = sw;
+  p.i8 = 1;
+  int rc = check_i8(p);
+  if (rc) return rc;
+  QD_REQUIRE(ldy >= ((epi & QD_EPI_GEGLU) ? N / 2 : N), "bad ldy");
+  QD_REQUIRE((double)M * lda < 2147483648.0, "activation exceeds the 2 GiB buffer-addressing range");
+  if (M == 0) return 0;
+  p.a_bytes = (unsigned)((long)(M - 1) * lda + K);
+  p.b_bytes = (unsigned)((long)N * K);
+  if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))
+    qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
+  run_i8<AM_LINEAR>(p, ws, ws_elems, S(stream));
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w, int ci, int ci_pad, const void* wt,
+                            const float* sw, int co, int kh, int kw, int stride, int pad, int upsample2x,
+                            const void* bias, const void* residual, void* y, int epi, float* amax, float* ws,
+                            long ws_elems, void* stream) {
+  QD_REQUIRE(ci_pad % 64 == 0 && ci_pad >= ci, "int8 conv needs ci_pad % 64 == 0");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(wt) & 15) == 0,
+             "x and w must be 16-B aligned");
+  GemmArgs p{};
+  const int H = upsample2x ? 2 * h : h, W = upsample2x ? 2 * w : w;
+  const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
+  p.a = (const f16*)x;
+  p.b = wt;
+  p.bias = (const f16*)bias;
+  p.res = (const f16*)residual;
+  p.y = (f16*)y;
+  p.ldy = co;
+  p.amax = amax;
+  p.rows_per_sample = Ho * Wo;
+  p.M = n * Ho * Wo;
+  p.N = co;
+  p.K = kh * kw * ci_pad / 2;
+  p.H = H;
+  p.W = W;
+  p.Hs = h;
+  p.Ws = w;
+  p.Cip = ci_pad / 2;
+  p.Ho = Ho;
+  p.Wo = Wo;
+  p.kh = kh;
+  p.kw = kw;
+  p.stride = stride;
+  p.pad = pad;
+  p.ups = upsample2x;
+  p.epi = epi;
+  p.sa = sa;
+  p.sa_rps = Ho * Wo;  // one activation scale per sample
+  p.sw = sw;
+  p.i8 = 1;
+  int rc = check_i8(p);
+  if (rc) return rc;
+  QD_REQUIRE(stride >= 1 && pad >= 0 && Ho > 0 && Wo > 0, "bad conv geometry");
+  QD_REQUIRE(!upsample2x || stride == 1, "upsample fusion needs stride 1");
+  QD_REQUIRE((double)n * h * w * ci_pad < 2147483648.0, "activation exceeds the 2 GiB buffer-addressing range");
+  if (p.M == 0) return 0;
+  p.a_bytes = (unsigned)((long)n * h * w * ci_pad);
+  p.b_bytes = (unsigned)((long)co * kh * kw * ci_pad);
+  if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED)) qd_zero_f32(amax, (size_t)n * co, S(stream));
+  if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && !upsample2x) {
+    p.lda = ci_pad / 2;
+    run_i8<AM_LINEAR>(p, ws, ws_elems, S(stream));
+  } else {
+    run_i8<AM_CONV>(p, ws, ws_elems, S(stream));
   }
   QD_CHECK_LAUNCH();
   return 0;

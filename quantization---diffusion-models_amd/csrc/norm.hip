@@ -149,13 +149,14 @@ __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
 
 template <int XF>
 __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg, int rows_per_block,
-                                                  float4* __restrict__ part) {
+                                                  float4* __restrict__ part, float* __restrict__ amax_n) {
   __shared__ float2 red[256][8];
   const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
   const int chunk = blockIdx.x * bx + tx;
   const bool active = chunk * 8 < c;
   const int ch = chunk * 8;
   const long n = blockIdx.y;
+
   const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
   float s1[8], s2[8], sh[8], mn[8], mx[8];
   GnXf xf;
@@ -235,7 +236,8 @@ constexpr float SILU_NEG_BOUND = 0.2786f;
 __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, GnIn in, int hw, int c, int cg,
                                                   int Z, float eps, const f16* __restrict__ gamma,
                                                   const f16* __restrict__ beta, int silu, int quant,
-                                                  float2* __restrict__ coef, float* __restrict__ amax) {
+                                                  float2* __restrict__ coef, float* __restrict__ amax,
+                                                  float* __restrict__ amax_n) {
   __shared__ float red[2][4];
   __shared__ float stat[2];
   __shared__ int nflag;
@@ -317,20 +319,45 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     if (t == 0) amax[i] = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));
     __syncthreads();
   }
+  if (amax_n) {
+    // int8 output: this (n, group)'s max over its channels into amax_n[n][group]; the apply pass
+    // takes the max over the groups (no same-address atomics: they serialise across blocks)
+    float m = 0.f;
+    for (int j = t; j < cg; j += 256) m = fmaxf(m, amax[(long)ni * c + g0 + j]);
+    m = wave_max(m);
+    if ((t & 63) == 0) fmx[t >> 6] = m;
+    __syncthreads();
+    if (t == 0) amax_n[blockIdx.x] = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));
+  }
 }
 
 // block (bx, by): thread (tx, ty) owns channel chunk blockIdx.x * bx + tx (8 channels, 16 B) of
 // sample blockIdx.y and rows ty, ty + by, ... of its row range: the per-channel coefficients
 // and fake-quant scales are loaded / computed once per thread, rows stream through.
 // The two sources are both multiples of 8 channels wide (host check).
-template <int XF, int SILU, bool Q>
+// int8 output (the int8-MFMA mode's conv input, one scale per sample): codes
+// rint(half(out / s_n)) with s_n = half(half(max_c amax[n][c]) / 127) written to y8, s_n to sa8[n]
+template <int XF, int SILU, bool Q, bool I8 = false>
 __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int rows_per_block,
                                                   const float2* __restrict__ coef, int qmax,
-                                                  const float* __restrict__ amax, f16* __restrict__ y) {
+                                                  const float* __restrict__ amax, f16* __restrict__ y,
+                                                  const float* __restrict__ amax_n = nullptr,
+                                                  int8_t* __restrict__ y8 = nullptr, float* __restrict__ sa8 = nullptr) {
   const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
   if (chunk * 8 >= c) return;
   const int ch = chunk * 8;
   const long n = blockIdx.y;
+  float s8 = 0.f;
+  double r8 = 0.0;
+  if constexpr (I8) {
+    // amax_n[n][g] (qmax carries the group count here): max over the sample's groups
+    const float* ag = amax_n + n * qmax;
+    float m = 0.f;
+    for (int gi = 0; gi < qmax; ++gi) m = fmaxf(m, ag[gi]);
+    s8 = fq_scale(m, 127);
+    r8 = rcp_exact(s8);
+    if (chunk == 0 && blockIdx.z == 0 && threadIdx.y == 0) sa8[n] = s8;
+  }
   const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
   float2 k[8];
   float sq[8];
@@ -359,6 +386,19 @@ __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int ro
     for (int u = 0; u < 4; ++u) {
       if (rb + u * by >= r1) break;
       const f16x8 w = gn_xf8<XF>(in, v[u], xf);
+      if constexpr (I8) {
+        unsigned lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float val = gn_out((float)w[j], k[j], SILU);
+          const f16 tq = (f16)(float)((double)val * r8);
+          const unsigned q = (unsigned)(uint8_t)(int8_t)__builtin_rintf((float)tq);
+          if (j < 4) lo |= q << (8 * j);
+          else hi |= q << (8 * (j - 4));
+        }
+        *reinterpret_cast<uint2*>(y8 + (n * hw + rb + u * by) * c + ch) = make_uint2(lo, hi);
+        continue;
+      }
       f16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -377,8 +417,10 @@ extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
 }
 
 static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float eps, const void* gamma,
-                         const void* beta, int silu, int q_bits, void* y, float* ws, hipStream_t st) {
-  QD_REQUIRE(in.x && gamma && beta && y && ws, "null pointer");
+                         const void* beta, int silu, int q_bits, void* y, float* ws, hipStream_t st,
+                         int8_t* y8 = nullptr, float* sa8 = nullptr) {
+  QD_REQUIRE(in.x && gamma && beta && (y || y8) && ws, "null pointer");
+  QD_REQUIRE(!y8 || (sa8 && q_bits == 0), "int8 output: scales needed, no fake-quant bits");
   QD_REQUIRE(groups > 0 && c % groups == 0, "groups must divide C");
   QD_REQUIRE(c % 8 == 0, "GroupNorm needs C % 8 == 0");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "workspace must be 16-B aligned");
@@ -390,14 +432,23 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   float4* part = reinterpret_cast<float4*>(ws);
   float2* coef = reinterpret_cast<float2*>(part + (long)n * g.zs * c);
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
+  float* amax_n = y8 ? amax + (long)n * c : nullptr;  // per-(n, group) maxima in the spare n * c floats
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
   const bool xf = in.qmax > 0 || in.cadd;
   const dim3 gs(g.gx, n, g.zs), bs(g.bx, g.bys);
-  if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part);
-  else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part);
+  if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
+  else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
   k_gn_coeff<<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta, silu,
-                                         qmax > 0, coef, amax);
+                                         qmax > 0 || y8, coef, amax, amax_n);
   const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
+  if (y8) {  // (the qmax argument carries the group count of amax_n[n][group])
+    if (xf && silu) k_gn_apply<1, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
+    else if (xf) k_gn_apply<1, 0, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
+    else if (silu) k_gn_apply<0, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
+    else k_gn_apply<0, 0, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
 #define QD_GN_APPLY(XFV, SV, QV) \
   k_gn_apply<XFV, SV, QV><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, qmax, amax, (f16*)y)
   const int sel = (xf ? 4 : 0) | (silu ? 2 : 0) | (qmax > 0 ? 1 : 0);
@@ -425,6 +476,24 @@ extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
 }
 
+extern "C" int qd_groupnorm_i8(const void* x, const void* x2, int c1, const float* in_amax, int in_bits,
+                               const void* cadd, int cadd_ld, int n, int hw, int c, int groups, float eps,
+                               const void* gamma, const void* beta, int silu, int8_t* y8, float* scales, float* ws,
+                               void* stream) {
+  QD_REQUIRE(y8 && scales, "null pointer");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(y8) & 7) == 0, "y8 must be 8-B aligned");
+  if (x2) {
+    QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c && !in_amax && !cadd, "bad concat split / concat with fq_in");
+  } else {
+    c1 = c;
+  }
+  QD_REQUIRE(in_bits == 0 || (in_bits >= 2 && in_bits <= 16 && in_amax), "bad input quant bits / amax");
+  if (cadd_ld <= 0) cadd_ld = c;
+  QD_REQUIRE(!cadd || (cadd_ld >= c && cadd_ld % 8 == 0), "bad cadd leading dim");
+  GnIn in{(const f16*)x, (const f16*)x2, c1, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld};
+  return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, 0, nullptr, ws, S(stream), y8, scales);
+}
+
 extern "C" int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int in_bits, const void* cadd,
                                   int cadd_ld, int n, int hw, int c, int groups, float eps, const void* gamma,
                                   const void* beta, int silu, int q_bits, void* y, float* ws, void* stream) {
@@ -442,10 +511,13 @@ extern "C" int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int i
 // (enough bytes in flight per CU to stream at HBM rate even for C = 320 rows of 640 B); lane l
 // owns the 8-channel chunks l, l + 64, ... of the row.
 // ---------------------------------------------------------------------------------------
-template <int PER, int R>  // 8-channel chunks per lane, rows per wave
+// I8: int8 output with one scale per row (the int8-MFMA mode's linear input, per token):
+// codes rint(half(out / s)), s = half(half(max |out|) / 127) -> y8, s -> sa8[row]
+template <int PER, int R, bool I8 = false>  // 8-channel chunks per lane, rows per wave
 __global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, long rows, int c, float eps,
                                                    const f16* __restrict__ gamma,
-                                                   const f16* __restrict__ beta, f16* __restrict__ y) {
+                                                   const f16* __restrict__ beta, f16* __restrict__ y,
+                                                   int8_t* __restrict__ y8 = nullptr, float* __restrict__ sa8 = nullptr) {
   const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   const int lane = threadIdx.x & 63;
   const int chunks = c >> 3;
@@ -479,6 +551,43 @@ __global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, lo
       }
     }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)c + eps);
+    if constexpr (I8) {
+      f16x8 o[PER];
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int j = lane + i * 64;
+        o[i] = (f16x8){};
+        if (j < chunks) {
+          const f16x8 g = *reinterpret_cast<const f16x8*>(gamma + j * 8);
+          const f16x8 b = *reinterpret_cast<const f16x8*>(beta + j * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            o[i][e] = (f16)fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[e], (float)b[e]);
+            m = fmaxf(m, fabsf((float)o[i][e]));
+          }
+        }
+      }
+      const float s = fq_scale(wave_max(m), 127);
+      const double rs = rcp_exact(s);
+      if (lane == 0) sa8[row0 + r] = s;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int j = lane + i * 64;
+        if (j < chunks) {
+          unsigned lo = 0, hi = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const f16 tq = (f16)(float)((double)(float)o[i][e] * rs);
+            const unsigned qv = (unsigned)(uint8_t)(int8_t)__builtin_rintf((float)tq);
+            if (e < 4) lo |= qv << (8 * e);
+            else hi |= qv << (8 * (e - 4));
+          }
+          *reinterpret_cast<uint2*>(y8 + (row0 + r) * c + j * 8) = make_uint2(lo, hi);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int j = lane + i * 64;
@@ -494,14 +603,34 @@ __global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, lo
   }
 }
 
-template <int PER>
-static void launch_ln(const f16* x, long rows, int c, float eps, const f16* g, const f16* b, f16* y, hipStream_t st) {
+template <int PER, bool I8 = false>
+static void launch_ln(const f16* x, long rows, int c, float eps, const f16* g, const f16* b, f16* y, hipStream_t st,
+                      int8_t* y8 = nullptr, float* sa8 = nullptr) {
   // rows per wave: ~2 KB of loads in flight per wave, while the grid still fills the chip
   int r = std::max(1, 2048 / (c * 2));
   while (r > 1 && (rows + 4L * r - 1) / (4L * r) < 1024) r >>= 1;
-  if (r >= 4) k_layernorm<PER, 4><<<(int)((rows + 15) / 16), 256, 0, st>>>(x, rows, c, eps, g, b, y);
-  else if (r >= 2) k_layernorm<PER, 2><<<(int)((rows + 7) / 8), 256, 0, st>>>(x, rows, c, eps, g, b, y);
-  else k_layernorm<PER, 1><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, eps, g, b, y);
+  if (r >= 4) k_layernorm<PER, 4, I8><<<(int)((rows + 15) / 16), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
+  else if (r >= 2) k_layernorm<PER, 2, I8><<<(int)((rows + 7) / 8), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
+  else k_layernorm<PER, 1, I8><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
+}
+
+extern "C" int qd_layernorm_i8(const void* x, int rows, int c, float eps, const void* gamma, const void* beta,
+                               int8_t* y8, float* scales, void* stream) {
+  QD_REQUIRE(x && gamma && beta && y8 && scales, "null pointer");
+  QD_REQUIRE(c % 8 == 0 && c <= 4096, "LayerNorm needs C % 8 == 0, C <= 4096");
+  QD_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) &
+              15) == 0 && (reinterpret_cast<uintptr_t>(y8) & 7) == 0, "LayerNorm operands must be aligned");
+  if (rows == 0) return 0;
+  const int per = (c / 8 + 63) / 64;
+  hipStream_t st = S(stream);
+  const f16 *xp = (const f16*)x, *g = (const f16*)gamma, *b = (const f16*)beta;
+  if (per <= 1) launch_ln<1, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
+  else if (per <= 2) launch_ln<2, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
+  else if (per <= 3) launch_ln<3, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
+  else if (per <= 4) launch_ln<4, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
+  else launch_ln<8, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
+  QD_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int qd_layernorm(const void* x, int rows, int c, float eps, const void* gamma,

@@ -710,3 +710,151 @@ extern "C" int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const i
   QD_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// int8 activation codes for the int8-MFMA W8A8 mode (qd_linear_i8 / qd_conv2d_i8)
+// ---------------------------------------------------------------------------------------
+// The reference's RTN recipe (fake_quant.py:108-131), keeping the integer instead of the
+// dequantized value: s = half(half(max(amax, 1e-5)) / 127), q = rint(half(x / s)); the scale is
+// stored widened to fp32 for the GEMM epilogue.  |q| <= 127 by construction.
+__device__ __forceinline__ int8_t q_i8(float x, float s, double rs) {
+  const f16 t = (f16)(float)((double)x * rs);  // == (f16)(x / s), fq_apply_r argument (common.h)
+  return (int8_t)__builtin_rintf((float)t);
+}
+
+// per row (dynamic per-token): one wave per row, R rows per wave, the row held in registers
+// (PER 16-B chunks per lane, all rows' loads issued before any reduction): one HBM read + one
+// 1-B/element write, no second pass over the row
+template <int PER, int R>
+__global__ void __launch_bounds__(256) k_quant_rows_i8(const f16* __restrict__ x, long rows, int c, int ldx,
+                                                       int8_t* __restrict__ y, int ldy, float* __restrict__ sa) {
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  const int lane = threadIdx.x & 63;
+  const int chunks = c >> 3;
+  f16x8 v[R][PER];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = lane + i * 64;
+      v[r][i] = (row0 + r < rows && j < chunks) ? *reinterpret_cast<const f16x8*>(x + (row0 + r) * ldx + j * 8)
+                                                : (f16x8){};
+    }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (row0 + r >= rows) break;
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)v[r][i][e]));
+    const float s = fq_scale(wave_max(m), 127);
+    const double rs = rcp_exact(s);
+    if (lane == 0) sa[row0 + r] = s;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = lane + i * 64;
+      if (j < chunks) {
+        unsigned lo = 0, hi = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lo |= (unsigned)(uint8_t)q_i8((float)v[r][i][e], s, rs) << (8 * e);
+          hi |= (unsigned)(uint8_t)q_i8((float)v[r][i][4 + e], s, rs) << (8 * e);
+        }
+        *reinterpret_cast<uint2*>(y + (row0 + r) * ldy + j * 8) = make_uint2(lo, hi);
+      }
+    }
+  }
+}
+
+template <int PER>
+static void launch_rows_i8(const f16* x, long rows, int c, int ldx, int8_t* y, int ldy, float* sa, hipStream_t st) {
+  int r = std::max(1, 2048 / (c * 2));
+  while (r > 1 && (rows + 4L * r - 1) / (4L * r) < 1024) r >>= 1;
+  if (r >= 4) k_quant_rows_i8<PER, 4><<<(int)((rows + 15) / 16), 256, 0, st>>>(x, rows, c, ldx, y, ldy, sa);
+  else if (r >= 2) k_quant_rows_i8<PER, 2><<<(int)((rows + 7) / 8), 256, 0, st>>>(x, rows, c, ldx, y, ldy, sa);
+  else k_quant_rows_i8<PER, 1><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, ldx, y, ldy, sa);
+}
+
+extern "C" int qd_quant_rows_i8(const void* x, long rows, int c, int ldx, int8_t* y, int ldy, float* scales,
+                                void* stream) {
+  QD_REQUIRE(x && y && scales, "null pointer");
+  QD_REQUIRE(c % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && ldx >= c && ldy >= c, "c, ldx, ldy must be multiples of 8");
+  QD_REQUIRE(c <= 8192, "row quantization supports c <= 8192");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 7) == 0, "alignment");
+  if (rows <= 0) return 0;
+  const int per = (c / 8 + 63) / 64;
+  const f16* xp = (const f16*)x;
+  hipStream_t st = S(stream);
+  if (per <= 1) launch_rows_i8<1>(xp, rows, c, ldx, y, ldy, scales, st);
+  else if (per <= 2) launch_rows_i8<2>(xp, rows, c, ldx, y, ldy, scales, st);
+  else if (per <= 4) launch_rows_i8<4>(xp, rows, c, ldx, y, ldy, scales, st);
+  else if (per <= 8) launch_rows_i8<8>(xp, rows, c, ldx, y, ldy, scales, st);
+  else launch_rows_i8<16>(xp, rows, c, ldx, y, ldy, scales, st);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// per sample (conv input): amax over the sample's per_sample values, then the codes
+__global__ void __launch_bounds__(256) k_sample_absmax(const f16* __restrict__ x, long per_sample,
+                                                       float* __restrict__ amax) {
+  __shared__ float red[4];
+  const long n = blockIdx.y;
+  const f16* p = x + n * per_sample;
+  float m = 0.f;
+  const long stride = (long)gridDim.x * 2048;
+  // 4 independent 16-B loads in flight per thread per iteration (clamped, not guarded)
+  for (long i0 = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i0 < per_sample; i0 += 4 * stride) {
+    f16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f16x8*>(p + min(i0 + u * stride, per_sample - 8));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)v[u][j]));  // clamped re-reads are harmless for a max
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_pos(amax + n, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+__global__ void __launch_bounds__(256) k_sample_apply_i8(const f16* __restrict__ x, long per_sample,
+                                                         const float* __restrict__ amax, int8_t* __restrict__ y,
+                                                         float* __restrict__ sa) {
+  const long n = blockIdx.y;
+  const float s = fq_scale(amax[n], 127);
+  const double rs = rcp_exact(s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) sa[n] = s;
+  const f16* p = x + n * per_sample;
+  int8_t* q = y + n * per_sample;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < per_sample; i += (long)gridDim.x * 2048) {
+    const f16x8 v = *reinterpret_cast<const f16x8*>(p + i);
+    unsigned lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo |= (unsigned)(uint8_t)q_i8((float)v[j], s, rs) << (8 * j);
+      hi |= (unsigned)(uint8_t)q_i8((float)v[4 + j], s, rs) << (8 * j);
+    }
+    *reinterpret_cast<uint2*>(q + i) = make_uint2(lo, hi);
+  }
+}
+
+extern "C" int qd_quant_samples_i8(const void* x, int n, long per_sample, int8_t* y, float* scales, float* amax_ws,
+                                   int amax_zeroed, void* stream) {
+  QD_REQUIRE(x && y && scales && amax_ws, "null pointer");
+  QD_REQUIRE(per_sample % 8 == 0, "per-sample size must be a multiple of 8");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 7) == 0, "alignment");
+  if ((long)n * per_sample == 0) return 0;
+  hipStream_t st = S(stream);
+  if (!amax_zeroed) qd_zero_f32(amax_ws, (size_t)n, st);
+  const long ch = (per_sample / 8 + 255) / 256;  // 2048-element blocks per sample
+  const int gx = (int)std::min<long>(std::max<long>(1, 1024 / n), ch);
+  const int gxa = (int)std::min<long>(std::max<long>(1, 512 / n), (ch + 3) / 4);  // 4 loads per thread
+  k_sample_absmax<<<dim3(gxa, n), 256, 0, st>>>((const f16*)x, per_sample, amax_ws);
+  k_sample_apply_i8<<<dim3(gx, n), 256, 0, st>>>((const f16*)x, per_sample, amax_ws, y, scales);
+  QD_CHECK_LAUNCH();
+  return 0;
+}

@@ -167,6 +167,7 @@ class WxAxLinear(nn.Module):
         self.qfmt = "f16"
         self.qgroup = 0
         self.n_bits_W = 16
+        self.int8_mfma = False  # int8-MFMA W8A8 mode (per-row int8 codes x per-token int8 activations)
         self.weight_quant_name = weight_quant
         if act_quant == "per_token":
             self.act_quant_name = "per_token"
@@ -199,6 +200,20 @@ class WxAxLinear(nn.Module):
         self.qfmt = "f16"
         self.qgroup = 0
         self._codes_ver = None
+        self.int8_mfma = False
+
+    def i8_operand(self):
+        """(int8 codes [N, K], fp32 scales [N]) of the int8-MFMA mode, or None when the layer is
+        not in that mode (or its codes went stale)."""
+        if not self.int8_mfma:
+            return None
+        w, fmt, sc, g = self.gemm_weight()
+        if fmt != "i8" or g != self.in_features:
+            return None
+        cache = getattr(self, "_i8_sw", None)
+        if cache is None or cache[0] != (sc.data_ptr(), sc._version):
+            self._i8_sw = ((sc.data_ptr(), sc._version), sc.float().reshape(-1).contiguous())
+        return w, self._i8_sw[1]
 
     def set_codes(self, codes, scales, group, n_bits):
         """Attach integer codes for the fused-dequant GEMM (int4 packed when n_bits <= 4)."""
@@ -227,6 +242,12 @@ class WxAxLinear(nn.Module):
         x2 = q_x.reshape(-1, shape[-1])
         if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0 or x2.data_ptr() % 16 != 0:
             x2 = x2.contiguous()
+        i8 = self.i8_operand()
+        if i8 is not None:
+            xq, sa = K.quant_rows_i8(x2)
+            y = K.linear_i8(xq, sa, i8[0], i8[1], bias=self.bias)
+            y = y.reshape(*shape[:-1], self.out_features)
+            return self.output_quant(y).to(x.dtype)
         w, fmt, sc, g = self.gemm_weight()
         y = K.linear(x2, w, fmt, sc, g, bias=self.bias)
         y = y.reshape(*shape[:-1], self.out_features)
@@ -243,8 +264,11 @@ class WxAxLinear(nn.Module):
     @torch.no_grad()
     def from_float(module, init_only=False, weight_quant="per_channel", act_quant="per_token",
                    quantize_output=False, n_bits_W=8, n_bits_A=16, group_size_W=0, codeBookQuantInd=False,
-                   debugPath=[], debug=False):
-        """fake_quant.py:234-258."""
+                   debugPath=[], debug=False, int8_mfma=False):
+        """fake_quant.py:234-258.  int8_mfma=True (this build's int8-MFMA W8A8 mode): per-row
+        8-bit weight codes (weight_quant forced to per_channel) and per-token int8 activations."""
+        if int8_mfma:
+            weight_quant, n_bits_W = "per_channel", 8
         assert isinstance(module, torch.nn.Linear)
         new = WxAxLinear(module.in_features, module.out_features, module.bias is not None,
                          weight_quant=weight_quant, act_quant=act_quant, quantize_output=quantize_output,
@@ -270,6 +294,7 @@ class WxAxLinear(nn.Module):
         new.weight_quant_name = weight_quant
         if module.bias is not None:
             new.bias.copy_(module.bias.to(torch.float16))
+        new.int8_mfma = bool(int8_mfma) and new.qfmt == "i8"
         return new
 
     def __repr__(self):
@@ -310,6 +335,10 @@ class WxAxConv2d(nn.Module):
         else:
             self.register_buffer("bias", None)
         self.register_buffer("w_khwc", None, persistent=False)
+        # int8-MFMA W8A8 mode: [Co][kh][kw][Ci_pad] int8 codes (one scale per output channel) and
+        # per-sample int8 activations (qd_conv2d_i8); None = the reference's fake-quant path
+        self.register_buffer("i8_w", None, persistent=False)
+        self.register_buffer("i8_sw", None, persistent=False)
         self.weight_quant_name = weight_quant
         if act_quant not in ("per_token", "per_tensor", "per_channel", "per_group"):
             raise ValueError(f"Invalid act_quant: {act_quant}")  # fake_quant.py:316-317
@@ -335,6 +364,36 @@ class WxAxConv2d(nn.Module):
             self._khwc_ver = ver
         return self.w_khwc
 
+    def i8_operand(self):
+        """(int8 codes [Co, kh, kw, Ci_pad], fp32 scales [Co]) of the int8-MFMA mode while they
+        still describe ``weight``, else None."""
+        if self.i8_w is None:
+            return None
+        if getattr(self, "_i8_ver", None) != (self.weight.data_ptr(), self.weight._version):
+            self.i8_w = self.i8_sw = None
+            return None
+        return self.i8_w, self.i8_sw
+
+    @torch.no_grad()
+    def set_int8(self, w_orig):
+        """int8-MFMA mode: per-output-channel RTN codes of the ORIGINAL weight over (kh, kw, Ci)
+        (the fake-quant recipe, fake_quant.py:44-46, at this granularity); ``weight`` becomes
+        their dequantized value so state_dict / the NCHW reference path stay consistent."""
+        co, ci, kh, kw = self.weight.shape
+        cip = self.ci_pad
+        if cip % 64 or co % 8 or self.groups != 1 or self.dilation != (1, 1):
+            return False
+        khwc = K.conv_weight_khwc(w_orig.detach().to(torch.float16).contiguous(), cip)
+        codes, scales, wdq = K.weight_quant(khwc.view(co, -1), kh * kw * cip, 8)
+        self.weight.copy_(wdq.view(co, kh, kw, cip)[..., :ci].permute(0, 3, 1, 2))
+        self.i8_w = codes.view(co, kh, kw, cip).contiguous()
+        self.i8_sw = scales.float().view(-1).contiguous()
+        self._i8_ver = (self.weight.data_ptr(), self.weight._version)
+        self.quantise_act = False
+        self.output_quant_name = "None"
+        self.output_quant = _identity
+        return True
+
     def _check_supported(self):
         if self.groups != 1 or self.dilation != (1, 1):
             raise NotImplementedError("grouped / dilated convolutions are not used by the SD UNets and "
@@ -349,6 +408,11 @@ class WxAxConv2d(nn.Module):
         if x.dtype != torch.float16:
             raise RuntimeError(f"WxAxConv2d expects fp16 input, got {x.dtype}")
         self._check_supported()
+        i8 = self.i8_operand()
+        if i8 is not None:
+            xq, sa = K.quant_samples_i8(K.nchw_to_nhwc(x.contiguous(), self.ci_pad))
+            y = K.conv2d_i8(xq, sa, i8[0], i8[1], self.in_channels, self.stride[0], self.padding[0], bias=self.bias)
+            return K.nhwc_to_nchw(y).to(x.dtype)
         q_x = self.act_quant(x) if self.quantise_act else x
         xh = K.nchw_to_nhwc(q_x.contiguous(), self.ci_pad)
         y = K.conv2d_nhwc(xh, self.gemm_weight(), self.in_channels, self.stride[0], self.padding[0],
@@ -360,8 +424,9 @@ class WxAxConv2d(nn.Module):
     @torch.no_grad()
     def from_float(cls, module, init_only=False, weight_quant="per_tensor", act_quant="per_tensor",
                    act_group_size=1, quantize_output=False, n_bits_W=8, n_bits_A=16, group_size_W=0,
-                   codeBookQuantInd=False, debugPath=[], debug=False):
-        """fake_quant.py:343-382."""
+                   codeBookQuantInd=False, debugPath=[], debug=False, int8_mfma=False):
+        """fake_quant.py:343-382.  int8_mfma=True: the int8-MFMA W8A8 mode where the conv allows
+        it (Ci_pad % 64 == 0, Co % 8 == 0; others keep the reference's fake-quant path)."""
         assert isinstance(module, torch.nn.Conv2d)
         new = cls(module.in_channels, module.out_channels, module.kernel_size, module.stride, module.padding,
                   module.dilation, module.groups, module.bias is not None, act_quant=act_quant,
@@ -385,6 +450,8 @@ class WxAxConv2d(nn.Module):
         new.weight_quant_name = weight_quant
         if module.bias is not None:
             new.bias.copy_(module.bias.to(torch.float16))
+        if int8_mfma and n_bits_W == 8 and new.set_int8(w):
+            new.weight_quant_name = "per_out_channel_int8"
         return new
 
     def __repr__(self):

@@ -396,6 +396,156 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     return out
 
 
+# ---------------------------------------------------------------- int8-MFMA W8A8 mode
+# int8 x int8 GEMMs (qd_linear_i8 / qd_conv2d_i8): exact int32 sums, so every tile variant and
+# split gives identical bits - the tuner below only picks the fastest.
+I8_VARIANTS = (110, 111, 112, 113)   # qd_gemm_force ids: LDS-DMA variants 10-13 (64-B rows)
+
+
+def quant_rows_i8(x2d, out=None, scales=None):
+    """Dynamic per-token int8 codes of x2d [M, K] (row stride may exceed K): (codes [M, K] int8,
+    scales [M] fp32) with the reference's RTN recipe (fake_quant.py:108-118)."""
+    if x2d.dtype != torch.float16 or not x2d.is_cuda or x2d.dim() != 2 or x2d.stride(1) != 1:
+        raise ValueError("x must be a 2-D fp16 HIP tensor with unit column stride")
+    M, Kd = x2d.shape
+    q = out if out is not None else _empty((M, Kd), torch.int8, x2d.device)
+    sa = scales if scales is not None else _empty((M,), torch.float32, x2d.device)
+    _lib.call("qd_quant_rows_i8", _p(x2d), M, Kd, x2d.stride(0), _p(q), q.stride(0), _p(sa), _stream())
+    return q, sa
+
+
+def quant_samples_i8(x, out=None, scales=None):
+    """int8 codes of x [N, ...] with one scale per sample (the conv-input granularity of the
+    int8 mode): (codes int8 of x's shape, scales [N] fp32)."""
+    _chk(x, "x")
+    n = x.shape[0]
+    q = out if out is not None else _empty(x.shape, torch.int8, x.device)
+    sa = scales if scales is not None else _empty((n,), torch.float32, x.device)
+    ws, zeroed = A.zeroed_f32(n, x.device)
+    _lib.call("qd_quant_samples_i8", _p(x), n, x.numel() // max(n, 1), _p(q), _p(sa), _p(ws), 1 if zeroed else 0,
+              _stream())
+    return q, sa
+
+
+def groupnorm_nhwc_i8(x, groups, eps, gamma, beta, silu=False, x2=None, fq_in=None):
+    """groupnorm_nhwc(...) written as int8 codes with one scale per sample (the int8-mode conv
+    input): (codes [N, H, W, C] int8, scales [N] fp32); x2 / fq_in as groupnorm_nhwc."""
+    _chk(x, "x")
+    n = x.shape[0]
+    c1 = x.shape[-1]
+    c = c1 + (x2.shape[-1] if x2 is not None else 0)
+    hw = x.numel() // (n * c1)
+    y8 = _empty((*x.shape[:-1], c), torch.int8, x.device)
+    sa = _empty((n,), torch.float32, x.device)
+    ws = _empty((_lib.load().qd_groupnorm_workspace(n, hw, c, groups),), torch.float32, x.device)
+    amax, bits, cadd, ld = None, 0, None, 0
+    if fq_in is not None:
+        amax, bits, cadd = fq_in
+        if cadd is not None:
+            if cadd.dim() != 2 or cadd.stride(1) != 1 or cadd.dtype != torch.float16:
+                raise ValueError("cadd must be an fp16 [N, C] tensor with unit column stride")
+            ld = cadd.stride(0)
+    if x2 is not None:
+        _chk(x2, "x2")
+    _lib.call("qd_groupnorm_i8", _p(x), _p(x2), c1 if x2 is not None else c, _p(amax), bits, _p(cadd), ld, n, hw, c,
+              groups, float(eps), _p(gamma), _p(beta), 1 if silu else 0, _p(y8), _p(sa), _p(ws), _stream())
+    return y8, sa
+
+
+def layernorm_i8(x, eps, gamma, beta):
+    """layernorm(...) written as per-row int8 codes: (codes [rows, C] int8, scales [rows] fp32)."""
+    _chk(x, "x")
+    c = x.shape[-1]
+    rows = x.numel() // c
+    y8 = _empty((rows, c), torch.int8, x.device)
+    sa = _empty((rows,), torch.float32, x.device)
+    _lib.call("qd_layernorm_i8", _p(x), rows, c, float(eps), _p(gamma), _p(beta), _p(y8), _p(sa), _stream())
+    return y8, sa
+
+
+def _i8_ws(M, N, K, rows_per_sample, epi, device, scratch=False):
+    n = _lib.load().qd_gemm_i8_workspace(M, N, K, rows_per_sample, epi)
+    if n <= 0:
+        return None, 0
+    return (torch.empty(n, dtype=torch.float32, device=device) if scratch else _empty((n,), torch.float32, device)), n
+
+
+def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, rows_per_sample=0, amax_zeroed=False,
+              geglu=False, gelu_tanh=False):
+    """y = half((xq . wq^T) * sa[m] * sw[n] (+ bias)) (+ residual / GEGLU / GELU-tanh / amax as
+    linear()); xq [M, K] int8 codes (row stride % 16 == 0), sa [M] fp32, wq [N, K] int8, sw [N] fp32."""
+    if xq.dtype != torch.int8 or wq.dtype != torch.int8 or not xq.is_cuda:
+        raise ValueError("int8 GEMM operands must be int8 HIP tensors")
+    if xq.dim() != 2 or xq.stride(1) != 1 or not wq.is_contiguous():
+        raise ValueError("xq must be 2-D with unit column stride, wq contiguous")
+    if sa.dtype != torch.float32 or sw.dtype != torch.float32:
+        raise ValueError("sa / sw must be fp32")
+    M, Kd = xq.shape
+    N = wq.shape[0]
+    if out is None:
+        out = _empty((M, N // 2 if geglu else N), torch.float16, xq.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
+          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
+          (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0)
+
+    def launch(c, y, am, ep, scratch):
+        _force(c if _OVERRIDE is None else _OVERRIDE)
+        try:
+            ws, wsn = _i8_ws(M, N, Kd, rows_per_sample, ep, xq.device, scratch)
+            _lib.call("qd_linear_i8", _p(xq), _p(sa), M, Kd, xq.stride(0), _p(wq), _p(sw), _p(bias), _p(residual),
+                      _p(y), N, y.stride(0), ep, _p(am), rows_per_sample, _p(ws), wsn, _stream())
+        finally:
+            _force(-1)
+
+    key = ("linear_i8", M, N, Kd, xq.stride(0), epi & ~EPI_AMAX_ZEROED, rows_per_sample)
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        ta = torch.empty_like(amax) if amax is not None else None
+        c = _choose(key, list(I8_VARIANTS), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else -1, out, amax, epi, False)
+    return out
+
+
+def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, residual=None, out=None, amax=None,
+              amax_zeroed=False):
+    """NHWC implicit-GEMM conv on int8 codes: xq [N, H, W, Cip] int8 (Cip % 64 == 0), sa [N]
+    fp32 (one scale per sample), wq [Co, kh, kw, Cip] int8, sw [Co] fp32."""
+    if xq.dtype != torch.int8 or wq.dtype != torch.int8 or not xq.is_cuda or not xq.is_contiguous():
+        raise ValueError("int8 conv operands must be contiguous int8 HIP tensors")
+    n, h, w, cip = xq.shape
+    co, kh, kw, cip_w = wq.shape
+    if cip_w != cip or cip % 64:
+        raise ValueError(f"int8 conv needs matching channel padding % 64 (x {cip}, weight {cip_w})")
+    H, W = (2 * h, 2 * w) if upsample2x else (h, w)
+    ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = _empty((n, ho, wo, co), torch.float16, xq.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
+          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0)
+    M, Kd = n * ho * wo, kh * kw * cip
+
+    def launch(c, y, am, ep, scratch):
+        _force(c if _OVERRIDE is None else _OVERRIDE)
+        try:
+            ws, wsn = _i8_ws(M, co, Kd, ho * wo, ep, xq.device, scratch)
+            _lib.call("qd_conv2d_i8", _p(xq), _p(sa), n, h, w, ci, cip, _p(wq), _p(sw), co, kh, kw, stride, pad,
+                      1 if upsample2x else 0, _p(bias), _p(residual), _p(y), ep, _p(am), _p(ws), wsn, _stream())
+        finally:
+            _force(-1)
+
+    key = ("conv_i8", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        ta = torch.empty_like(amax) if amax is not None else None
+        c = _choose(key, list(I8_VARIANTS), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else -1, out, amax, epi, False)
+    return out
+
+
 def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
     """out = half(fq(y) + residual | + chan_add[n, c]); y NHWC [N, H, W, C] (or [N, HW, C]).
     chan_add may be a row-strided [N, C] view (e.g. a column slice of a stacked projection)."""

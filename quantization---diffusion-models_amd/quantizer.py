@@ -84,6 +84,9 @@ class AwqQuantizer:
         self.quantTransformer = quantTransformer
         self.codeBookQuantInd = codeBookQuantInd
         self.diffusion_model = diffusion_model
+        # this build's int8-MFMA W8A8 mode: per-output-channel int8 weights,
+        # per-token (linear) / per-sample (conv) int8 activations on v_mfma_i32_16x16x64_i8
+        self.int8_mfma = bool(kwargs.pop("int8_mfma", False))
         self.calib_kwargs = kwargs
         if not diffusion_model:
             raise NotImplementedError("the LLM/VLM AWQ path is out of scope (SURVEY.md §2); diffusion_model=True only")
@@ -128,17 +131,20 @@ class AwqQuantizer:
     def _apply_quant_fake_act(self, module, named_linears, bitWidth, debugStruct=None, debug=False):
         """Diffusion branch of quantizer.py:491-533."""
         for parent, name, layer in named_linears:
+            i8 = getattr(self, "int8_mfma", False) and bitWidth == 8
             if isinstance(layer, nn.Linear):
                 fake = WxAxLinear.from_float(layer, weight_quant=self.weight_quant_type, act_quant="per_token",
                                              quantize_output=_is_bmm_input(name), n_bits_W=bitWidth,
                                              n_bits_A=self.a_bit, group_size_W=self.group_size,
-                                             codeBookQuantInd=self.codeBookQuantInd)
+                                             codeBookQuantInd=self.codeBookQuantInd,
+                                             int8_mfma=i8 and layer.in_features % 64 == 0)
                 setattr(parent, name, fake)
             elif isinstance(layer, nn.Conv2d):
                 fake = WxAxConv2d.from_float(layer, weight_quant=self.weight_quant_conv_type,
                                              act_quant=self.act_quant_conv_type, quantize_output=self.quantise_act,
                                              act_group_size=self.act_quant_conv_group_size, n_bits_W=bitWidth,
-                                             n_bits_A=self.a_bit, codeBookQuantInd=self.codeBookQuantInd)
+                                             n_bits_A=self.a_bit, codeBookQuantInd=self.codeBookQuantInd,
+                                             int8_mfma=i8)
                 setattr(parent, name, fake)
 
     @torch.no_grad()

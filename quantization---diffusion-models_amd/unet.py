@@ -429,6 +429,11 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
     is None when y is already final."""
     if isinstance(layer, WxAxConv2d):
         layer._check_supported()
+        i8 = layer.i8_operand()
+        if isinstance(x, tuple):  # (int8 codes, per-sample scales) from a fused producer
+            return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer)
+        if i8 is not None and co_pad in (None, layer.out_channels) and x.shape[-1] == layer.ci_pad:
+            return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer)
     wk, bias = _conv_weight(layer, co_pad)
     stride, pad = layer.stride[0], layer.padding[0]
     ci = layer.weight.shape[1]
@@ -463,6 +468,31 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
     return K.fq_finalize(y, None, 0, residual=residual, chan_add=chan_add, out=y)
 
 
+def conv_i8(layer):
+    """True when `layer` runs in the int8-MFMA mode (its producer may then emit int8 codes)."""
+    return isinstance(layer, WxAxConv2d) and layer.i8_operand() is not None
+
+
+def lin_i8(layer):
+    return isinstance(layer, WxAxLinear) and layer.i8_operand() is not None and \
+        getattr(layer, "_qd_hook", None) is None
+
+
+def _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer):
+    """int8-MFMA mode conv: per-sample int8 codes of the fp16 NHWC input (or the producer's fused
+    (codes, scales)), int8 implicit GEMM with the output (+ bias, + residual) in fp16; the
+    time-embedding add is deferred to the consumer like the fake-quant path's (no output
+    fake-quant in this mode)."""
+    xq, sa = x if isinstance(x, tuple) else K.quant_samples_i8(x)
+    y = K.conv2d_i8(xq, sa, i8[0], i8[1], layer.in_channels, layer.stride[0], layer.padding[0], upsample,
+                    bias=layer.bias, residual=residual)
+    if chan_add is None:
+        return (y, None) if defer else y
+    if defer and residual is None:
+        return y, (None, 0, chan_add)
+    return K.fq_finalize(y, None, 0, chan_add=chan_add, out=y)
+
+
 def _conv_via_module(layer, x, residual, chan_add, upsample, co_pad):
     n, h, w, cp = x.shape
     if upsample:
@@ -475,13 +505,31 @@ def _conv_via_module(layer, x, residual, chan_add, upsample, co_pad):
     return yh
 
 
+# int8-MFMA mode: linears with fewer input rows (the time-embedding projections at the CFG batch)
+# keep the fp16 MFMA on their dequantized codes - a 16-row MFMA tile would idle there
+I8_MIN_ROWS = 64
+
+
 def run_linear(layer, x2d, residual=None, out=None):
     """x2d [M, K] -> [M, N] for an nn.Linear or WxAxLinear (fake_quant.py:214-225 semantics).
-    out: optional contiguous [M, N] destination."""
+    out: optional contiguous [M, N] destination.  x2d may be (int8 codes, per-row scales) from a
+    fused producer (int8-MFMA mode layers only)."""
+    if isinstance(x2d, tuple):
+        xq, sa = x2d
+        i8 = layer.i8_operand()
+        return K.linear_i8(xq, sa, i8[0], i8[1], bias=layer.bias, residual=residual, out=out)
     hook = getattr(layer, "_qd_hook", None)
     if hook is not None:  # SmoothQuant calibration (calib.py)
         hook(x2d)
     if isinstance(layer, WxAxLinear):
+        i8 = layer.i8_operand() if x2d.shape[0] >= I8_MIN_ROWS else None
+        if i8 is not None:
+            xq, sa = K.quant_rows_i8(x2d)
+            if layer.output_quant_name != "None":
+                y = K.linear_i8(xq, sa, i8[0], i8[1], bias=layer.bias, out=out)
+                y = K.act_fakequant(y, layer.output_quant_name, layer.n_bits_A, out=y)
+                return K.add(y, residual, out=y) if residual is not None else y
+            return K.linear_i8(xq, sa, i8[0], i8[1], bias=layer.bias, residual=residual, out=out)
         xin = layer.act_quant(x2d) if layer.quantize_act else x2d
         w, fmt, sc, g = layer.gemm_weight()
         wf = layer.weight if fmt != "f16" else None  # the same weight's fp16 dequantized buffer
@@ -515,15 +563,38 @@ def _geglu_operand(layer):
 
 
 def ff_geglu(layer, x2d):
-    """diffusers GEGLU(proj) = h * gelu(g) with (h, g) = proj(x).chunk(2): one GEMM, fused epilogue."""
+    """diffusers GEGLU(proj) = h * gelu(g) with (h, g) = proj(x).chunk(2): one GEMM, fused epilogue.
+    x2d may be (int8 codes, per-row scales) in the int8-MFMA mode."""
+    if isinstance(x2d, tuple):
+        wq, sw, b = _geglu_operand_i8(layer, layer.i8_operand())
+        return K.linear_i8(x2d[0], x2d[1], wq, sw, bias=b, geglu=True)
     if isinstance(layer, WxAxLinear) and layer.output_quant_name != "None":
         return K.geglu(run_linear(layer, x2d))  # output fake-quant sits between proj and GEGLU
     hook = getattr(layer, "_qd_hook", None)
     if hook is not None:  # SmoothQuant calibration observes the projection input
         hook(x2d)
+    i8 = layer.i8_operand() if isinstance(layer, WxAxLinear) and x2d.shape[0] >= I8_MIN_ROWS else None
+    if i8 is not None:
+        wq, sw, b = _geglu_operand_i8(layer, i8)
+        xq, sa = K.quant_rows_i8(x2d)
+        return K.linear_i8(xq, sa, wq, sw, bias=b, geglu=True)
     xin = layer.act_quant(x2d) if isinstance(layer, WxAxLinear) and layer.quantize_act else x2d
     w, fmt, sc, g, b, wf = _geglu_operand(layer)
     return K.linear(xin, w, fmt, sc, g, bias=b, geglu=True, weight_f16=wf)
+
+
+def _geglu_operand_i8(layer, i8):
+    """int8 codes / fp32 scales / bias of ff.net[0].proj with rows interleaved for the GEGLU epilogue."""
+    wq, sw = i8
+    b = layer.bias
+    ver = (wq.data_ptr(), wq._version, sw.data_ptr(), None if b is None else (b.data_ptr(), b._version))
+    cache = getattr(layer, "_qd_geglu_i8", None)
+    if cache is not None and cache[0] == ver:
+        return cache[1]
+    perm = K.geglu_interleave_rows(wq.shape[0], wq.device)
+    op = (wq[perm].contiguous(), sw[perm].contiguous(), None if b is None else b.detach()[perm].contiguous())
+    layer._qd_geglu_i8 = (ver, op)
+    return op
 
 
 def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
@@ -539,8 +610,12 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
         return _resnet_tail(res, h, temb_silu, tp, sc)
     xin = K.concat_c(x, skip) if skip is not None else x
     q1 = conv_qbits(res.conv1)
-    h = K.groupnorm_nhwc(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
-                         silu=True, q_bits=max(q1, 0))
+    if conv_i8(res.conv1):  # int8-MFMA mode: GroupNorm + SiLU emits conv1's int8 codes
+        h = K.groupnorm_nhwc_i8(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight),
+                                _f16(res.norm1.bias), silu=True)
+    else:
+        h = K.groupnorm_nhwc(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
+                             silu=True, q_bits=max(q1, 0))
     if tp is None:
         tp = run_linear(res.time_emb_proj, temb_silu)
     sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
@@ -555,8 +630,12 @@ def _resnet_tail(res, h, temb_silu, tp, sc):
     # conv1's output quant + temb add are applied inside norm2 (never materialised)
     h, spec = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp, defer=True)
     q2 = conv_qbits(res.conv2)
-    h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
-                         silu=True, q_bits=max(q2, 0), fq_in=spec)
+    if conv_i8(res.conv2):
+        h = K.groupnorm_nhwc_i8(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
+                                silu=True, fq_in=spec)
+    else:
+        h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
+                             silu=True, q_bits=max(q2, 0), fq_in=spec)
     return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc)
 
 
@@ -566,6 +645,9 @@ def transformer_fwd(tm, x, ctx_kv):
     if tm.linear_proj:
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
         t = run_linear(tm.proj_in, h.view(-1, c))
+    elif conv_i8(tm.proj_in):
+        h = K.groupnorm_nhwc_i8(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
+        t = run_conv(tm.proj_in, h).view(-1, c)
     else:
         q = conv_qbits(tm.proj_in)
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias),
@@ -604,10 +686,41 @@ def _qkv_operand(attn):
     return op
 
 
+def _qkv_operand_i8(attn):
+    """int8-MFMA mode: (codes [3C, C], fp32 scales [3C]) of to_q | to_k | to_v stacked, or None."""
+    layers = (attn.to_q, attn.to_k, attn.to_v)
+    ops = []
+    for l in layers:
+        if not isinstance(l, WxAxLinear) or getattr(l, "_qd_hook", None) is not None or l.bias is not None \
+                or l.output_quant_name != "None":
+            return None
+        op = l.i8_operand()
+        if op is None:
+            return None
+        ops.append(op)
+    ver = tuple((o[0].data_ptr(), o[0]._version, o[1].data_ptr()) for o in ops)
+    cache = getattr(attn, "_qd_qkv_i8", None)
+    if cache is not None and cache[0] == ver:
+        return cache[1]
+    op = (torch.cat([o[0] for o in ops]).contiguous(), torch.cat([o[1] for o in ops]).contiguous())
+    attn._qd_qkv_i8 = (ver, op)
+    return op
+
+
 def self_attn_qkv(attn, h, n, s):
     """q, k, v [n, s, C] views of ONE projection GEMM with the three weights stacked (same
-    input, same per-row math as three F.linear calls)."""
+    input, same per-row math as three F.linear calls).  h may be (int8 codes, row scales)."""
+    if isinstance(h, tuple):
+        op8 = _qkv_operand_i8(attn)
+        c = h[0].shape[1]
+        y = K.linear_i8(h[0], h[1], op8[0], op8[1]).view(n, s, 3 * c)
+        return y[:, :, :c], y[:, :, c:2 * c], y[:, :, 2 * c:]
     c = h.shape[1]
+    op8 = _qkv_operand_i8(attn) if h.shape[0] >= I8_MIN_ROWS else None
+    if op8 is not None:
+        xq, sa = K.quant_rows_i8(h)
+        y = K.linear_i8(xq, sa, op8[0], op8[1]).view(n, s, 3 * c)
+        return y[:, :, :c], y[:, :, c:2 * c], y[:, :, 2 * c:]
     op = _qkv_operand(attn)
     if op is None:
         return tuple(run_linear(l, h).view(n, s, c) for l in (attn.to_q, attn.to_k, attn.to_v))
@@ -620,16 +733,20 @@ def block_fwd(blk, t, n, s, ctx_kv):
     """BasicTransformerBlock: self-attn, cross-attn, GEGLU feed-forward, each + residual."""
     c = t.shape[1]
     a1 = blk.attn1
-    h = K.layernorm(t, blk.norm1.eps, _f16(blk.norm1.weight), _f16(blk.norm1.bias))
+    # int8-MFMA mode: each LayerNorm emits its consumer's per-token int8 codes directly
+    big = t.shape[0] >= I8_MIN_ROWS
+    ln = lambda norm, i8: (K.layernorm_i8 if i8 and big else K.layernorm)(t, norm.eps, _f16(norm.weight),
+                                                                           _f16(norm.bias))
+    h = ln(blk.norm1, _qkv_operand_i8(a1) is not None)
     q, k, v = self_attn_qkv(a1, h, n, s)
     o = K.attention(q, k, v, a1.heads)
     t = run_linear(a1.to_out[0], o.view(-1, c), residual=t)
     a2 = blk.attn2
-    h = K.layernorm(t, blk.norm2.eps, _f16(blk.norm2.weight), _f16(blk.norm2.bias))
+    h = ln(blk.norm2, lin_i8(a2.to_q) and a2.to_q.output_quant_name == "None")
     q = run_linear(a2.to_q, h).view(n, s, c)
     k, v = ctx_kv[id(a2)]
     o = K.attention(q, k, v, a2.heads)
     t = run_linear(a2.to_out[0], o.view(-1, c), residual=t)
-    h = K.layernorm(t, blk.norm3.eps, _f16(blk.norm3.weight), _f16(blk.norm3.bias))
+    h = ln(blk.norm3, lin_i8(blk.ff.net[0].proj) and blk.ff.net[0].proj.output_quant_name == "None")
     g = ff_geglu(blk.ff.net[0].proj, h)
     return run_linear(blk.ff.net[2], g, residual=t)

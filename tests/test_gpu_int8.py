@@ -1,0 +1,313 @@
+"""The int8-MFMA W8A8 mode against its CPU restatement (oracle/int8_ref.py): integer sums are
+exact, so every output must match BIT FOR BIT, for every tile variant and split-K plan.  The
+activation codes are additionally pinned to the reference's own per-token fake-quant golden
+(half(q * s) == quantize_activation_per_token_absmax output, fake_quant.py:108-118)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import int8_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def K():
+    from qdiff import kernels
+    return kernels
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint16)
+
+
+def test_row_codes_match_reference_fake_quant(golden, dev):
+    """The int8 codes of quant_rows_i8, dequantized, ARE the reference's per-token fake-quant."""
+    k = K()
+    g = golden["fake_quant_golden"]
+    x = g["atok_b8_in"].reshape(-1, 320)
+    q, s = k.quant_rows_i8(torch.from_numpy(x).to(dev))
+    q, s = q.cpu().numpy(), s.cpu().numpy()
+    qr, sr = R.quant_rows_i8(x)
+    assert np.array_equal(q, qr) and np.array_equal(s, sr)
+    deq = (q.astype(np.float32) * s[:, None]).astype(np.float16)
+    # value-equal (an integer code cannot carry the -0.0 that rint gives small negatives)
+    assert np.array_equal(deq.astype(np.float32), g["atok_b8_out"].reshape(-1, 320).astype(np.float32))
+
+
+def test_sample_codes(dev):
+    k = K()
+    rng = np.random.default_rng(1)
+    x = (rng.standard_normal((3, 16, 16, 64)) * 2).astype(np.float16)
+    x[1] *= 40
+    x[2, :, :, 5] = 0
+    q, s = k.quant_samples_i8(torch.from_numpy(x).to(dev))
+    qr, sr = R.quant_samples_i8(x)
+    assert np.array_equal(q.cpu().numpy(), qr) and np.array_equal(s.cpu().numpy(), sr)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(64, 64, 64), (200, 320, 320), (616, 640, 768), (4096, 2560, 320),
+                                    (8, 1280, 1280), (1000, 64, 128), (256, 1280, 5120), (77, 320, 2560)])
+@pytest.mark.parametrize("variant", [None, 110, 111, 112, 113])
+def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
+    k = K()
+    rng = np.random.default_rng(M + N + Kd)
+    x = rng.standard_normal((M, Kd)).astype(np.float16)
+    w = (rng.standard_normal((N, Kd)) / Kd ** 0.5).astype(np.float16)
+    b = rng.standard_normal(N).astype(np.float16)
+    res = rng.standard_normal((M, N)).astype(np.float16)
+    xq, sa = R.quant_rows_i8(x)
+    wq, sw = R.weight_rows_i8(w)
+    ref = R.linear_i8(xq, sa, wq, sw, b, res)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    k.force_gemm(variant)
+    try:
+        y = k.linear_i8(t(xq), t(sa), t(wq), t(sw), bias=t(b), residual=t(res)).cpu().numpy()
+    finally:
+        k.force_gemm(None)
+    assert np.array_equal(_bits(y), _bits(ref)), np.abs(y.astype(np.float32) - ref.astype(np.float32)).max()
+
+
+def test_linear_i8_geglu_and_amax(dev):
+    k = K()
+    rng = np.random.default_rng(9)
+    M, I, Kd = 512, 640, 320
+    x = rng.standard_normal((M, Kd)).astype(np.float16)
+    w = (rng.standard_normal((2 * I, Kd)) / Kd ** 0.5).astype(np.float16)
+    xq, sa = R.quant_rows_i8(x)
+    wq, sw = R.weight_rows_i8(w)
+    pre = R.linear_i8(xq, sa, wq, sw).astype(np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    perm = k.geglu_interleave_rows(2 * I, dev)
+    fused = k.linear_i8(t(xq), t(sa), t(wq)[perm].contiguous(), t(sw)[perm].contiguous(), geglu=True).cpu().float()
+    h, gt = torch.from_numpy(pre).chunk(2, -1)
+    ref = (h * torch.nn.functional.gelu(gt).half().float()).half().float()
+    u = torch.pow(2.0, torch.floor(torch.log2(ref.abs().clamp(min=6.1e-5))) - 10)
+    assert ((fused - ref).abs() <= 2 * u + 1e-3).all()   # the GELU fit vs torch's erf (common.h)
+    amax = torch.empty(2 * 2 * I, dtype=torch.float32, device=dev)
+    y = k.linear_i8(t(xq), t(sa), t(wq), t(sw), amax=amax, rows_per_sample=256)
+    assert torch.equal(amax.cpu(), y.float().abs().view(2, 256, -1).amax(1).reshape(-1).cpu())
+
+
+@pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups", [(64, 64, 3, 1, 16, False), (64, 128, 3, 2, 16, False),
+                                                        (128, 64, 1, 1, 8, False), (64, 64, 3, 1, 8, True),
+                                                        (320, 320, 3, 1, 32, False), (640, 640, 3, 1, 16, False),
+                                                        (1280, 1280, 3, 1, 8, False), (960, 320, 3, 1, 16, False)])
+@pytest.mark.parametrize("variant", [None, 110, 111, 112, 113])
+def test_conv2d_i8_bit_exact(cin, cout, ksz, stride, hw, ups, variant, dev):
+    k = K()
+    rng = np.random.default_rng(cin * 7 + cout + ksz)
+    n = 2
+    x = rng.standard_normal((n, cin, hw, hw)).astype(np.float16)
+    x[1] *= 3
+    w = (rng.standard_normal((cout, cin, ksz, ksz)) / (cin * ksz * ksz) ** 0.5).astype(np.float16)
+    b = rng.standard_normal(cout).astype(np.float16)
+    xq, sa = R.quant_samples_i8(x)
+    wk = w.transpose(0, 2, 3, 1).reshape(cout, -1)        # [Co][kh][kw][Ci]
+    wkq, sw = R.weight_rows_i8(wk)
+    wq = wkq.reshape(cout, ksz, ksz, cin).transpose(0, 3, 1, 2)
+    pad = ksz // 2
+    xin = xq.repeat(2, axis=2).repeat(2, axis=3) if ups else xq
+    ref = R.conv2d_i8(xin, sa, wq, sw, b, stride, pad)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    xh = t(xq.transpose(0, 2, 3, 1))
+    k.force_gemm(variant)
+    try:
+        y = k.conv2d_i8(xh, t(sa), t(wkq.reshape(cout, ksz, ksz, cin)), t(sw), cin, stride, pad, ups, bias=t(b))
+    finally:
+        k.force_gemm(None)
+    got = y.permute(0, 3, 1, 2).cpu().numpy()
+    assert np.array_equal(_bits(got), _bits(ref)), np.abs(got.astype(np.float32) - ref.astype(np.float32)).max()
+
+
+# ------------------------------------------------------------------ model level
+def _cfgdict(cfg):
+    import dataclasses
+    return {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(cfg).items()}
+
+
+def _one_eval(model, x, t, ctx):
+    from qdiff import kernels as k
+    unet = model.pipeline.unet
+    dev = torch.device("cuda:0")
+    kv = unet.prepare_context(ctx.to(dev))
+    temb = k.timestep_embedding(torch.tensor([float(t)], device=dev), None, x.shape[0], unet.config.block_out_channels[0])
+    return k.nhwc_to_nchw(unet.fwd(k.nchw_to_nhwc(x.to(dev), 8), temb, kv), 4).cpu()
+
+
+QC8 = dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True)
+
+
+def test_int8_mode_swap_and_buffers(dev):
+    """quantize(int8_mfma=True): every eligible layer gets per-output-channel int8 codes whose
+    dequantized values are the module's `weight` buffer and equal the oracle's."""
+    from oracle.unet_ref import RefUNet
+    from qdiff.fake_quant import WxAxConv2d, WxAxLinear
+    from qdiff.models import StableDiffusion1_x
+    model = StableDiffusion1_x.from_pretrained("synthetic:tiny", device="cuda:0", seed=21)
+    sd = {kk: v.detach().cpu() for kk, v in model.pipeline.unet.state_dict().items()}
+    model.quantize(quant_config=dict(QC8), quantUnet=True, int8_mfma=True)
+    ref = RefUNet(_cfgdict(model.pipeline.unet.config), sd, dict(QC8), int8=True)
+    n_i8 = 0
+    for name, m in model.pipeline.unet.named_modules():
+        if isinstance(m, (WxAxLinear, WxAxConv2d)):
+            assert torch.equal(m.weight.cpu().view(torch.int16), ref.sd[name + ".weight"].view(torch.int16)), name
+            if m.i8_operand() is not None:
+                n_i8 += 1
+                assert name in ref.i8
+    assert n_i8 == len(ref.i8) and n_i8 > 0
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_tiny_unet_int8_eval_vs_int8_oracle(dev, seed):
+    """One tiny UNet eval in the int8-MFMA mode vs the int8 oracle (torch-CPU Half for the
+    non-int8 ops).  The int8 layers are exact; the norms / attention / fp16 layers differ by ulps,
+    which per-token / per-sample re-quantization amplifies like the fake-quant W8A8 network, so the
+    bound is self-calibrated as tests/test_gpu_unet.py: <= 1.5 x the oracle's own Half-vs-fp32
+    spread + 2e-3 (max and mean, relative to max |ref|)."""
+    from oracle.unet_ref import RefUNet
+    from qdiff.models import StableDiffusion1_x
+    model = StableDiffusion1_x.from_pretrained("synthetic:tiny", device="cuda:0", seed=seed)
+    cfg = model.pipeline.unet.config
+    sd = {kk: v.detach().cpu() for kk, v in model.pipeline.unet.state_dict().items()}
+    model.quantize(quant_config=dict(QC8), quantUnet=True, int8_mfma=True)
+    g = torch.Generator().manual_seed(seed + 100)
+    x = torch.randn(2, 4, cfg.sample_size, cfg.sample_size, generator=g).half()
+    ctx = torch.randn(2, 77, cfg.cross_attention_dim, generator=g).half()
+    got = _one_eval(model, x, 701, ctx).float()
+    ref = RefUNet(_cfgdict(cfg), sd, dict(QC8), int8=True).forward(x, 701, ctx).float()
+    ref32 = RefUNet(_cfgdict(cfg), sd, dict(QC8), variant="fp32", int8=True).forward(x, 701, ctx).float()
+    sc = ref.abs().max().item()
+    rel = lambda a, b: ((a - b).abs().max().item() / sc, (a - b).abs().mean().item() / sc)
+    smx, smean = rel(ref32, ref)
+    mx, mean = rel(got, ref)
+    print(f"int8 tiny eval seed {seed}: gpu-vs-half max {mx:.4g} mean {mean:.4g} | spread max {smx:.4g} mean {smean:.4g}")
+    assert mx <= 1.5 * smx + 2e-3 and mean <= 1.5 * smean + 2e-3
+
+
+@pytest.fixture(scope="module")
+def sd15_int8():
+    """Full-size SD1.5 in the int8-MFMA mode: one GPU eval at 64x64 latents, batch 2, the fp32
+    int8 oracle with every layer recorded, and the fp32 oracles of the unquantized UNet and of the
+    reference's fake-quant W8A8."""
+    import time
+    from oracle.unet_ref import RefUNet
+    from qdiff.models import StableDiffusion1_x
+    t0 = time.time()
+    model = StableDiffusion1_x.from_pretrained("synthetic:sd15", device="cuda:0", seed=0)
+    cfg = model.pipeline.unet.config
+    sd = {kk: v.detach().cpu() for kk, v in model.pipeline.unet.state_dict().items()}
+    model.quantize(quant_config=dict(QC8), quantUnet=True, int8_mfma=True)
+    g = torch.Generator().manual_seed(42)
+    x = torch.randn(2, 4, 64, 64, generator=g).half()
+    ctx = torch.randn(2, 77, 768, generator=g).half()
+    got = _one_eval(model, x, 981, ctx)
+    print(f"[sd15 int8] gpu eval {time.time() - t0:.1f}s", flush=True)
+    ref = RefUNet(_cfgdict(cfg), sd, dict(QC8), variant="fp32", int8=True)
+    ref.record = rec = {}
+    ref_i8 = ref.forward(x, 981, ctx)
+    print(f"[sd15 int8] int8 oracle {time.time() - t0:.1f}s", flush=True)
+    ref.record = None
+    ref.ops = torch.nn.functional  # the "half" variant of the same oracle (torch-CPU Half non-int8 ops)
+    ref_i8h = ref.forward(x, 981, ctx)
+    print(f"[sd15 int8] int8 oracle (half) {time.time() - t0:.1f}s", flush=True)
+    r16 = RefUNet(_cfgdict(cfg), sd, None, variant="fp32").forward(x, 981, ctx)
+    rfq = RefUNet(_cfgdict(cfg), sd, dict(QC8), variant="fp32").forward(x, 981, ctx)
+    print(f"[sd15 int8] fp16 / fake-quant oracles {time.time() - t0:.1f}s", flush=True)
+    return dict(model=model, got=got, ref_i8=ref_i8, ref_i8h=ref_i8h, r16=r16, rfq=rfq, record=rec, i8=set(ref.i8))
+
+
+@pytest.mark.timeout(900)
+def test_sd15_int8_teacher_forced_bit_exact(sd15_int8):
+    """Every int8 layer of the full-size SD1.5 UNet, fed the int8 oracle's input of that layer,
+    reproduces the oracle's output BIT FOR BIT (codes, exact int32 sums, fp32 epilogue)."""
+    from qdiff import kernels as k
+    from qdiff.unet import run_conv, run_linear
+    f = sd15_int8
+    unet = f["model"].pipeline.unet
+    dev = torch.device("cuda:0")
+    n = {"conv": 0, "linear": 0}
+    bad = []
+    for name, tens in f["record"].items():
+        if name not in f["i8"]:
+            continue
+        mod = unet.get_submodule(name)
+        x, y = tens
+        if isinstance(mod, torch.nn.Module) and hasattr(mod, "kernel_size"):
+            n["conv"] += 1
+            up = name.endswith("upsamplers.0.conv")
+            xin = x[:, :, ::2, ::2].contiguous() if up else x
+            got = k.nhwc_to_nchw(run_conv(mod, k.nchw_to_nhwc(xin.contiguous().to(dev), mod.ci_pad),
+                                          upsample=up)).cpu()
+        else:
+            if x.numel() // x.shape[-1] < 64:  # I8_MIN_ROWS: the fp16 path (time embeddings)
+                continue
+            n["linear"] += 1
+            got = run_linear(mod, x.reshape(-1, x.shape[-1]).contiguous().to(dev)).view(*y.shape).cpu()
+        if not torch.equal(got.view(torch.int16), y.view(torch.int16)):
+            bad.append((name, (got.float() - y.float()).abs().max().item()))
+    print(f"int8 layers checked: {n}, mismatching: {len(bad)}")
+    assert n["conv"] > 90 and n["linear"] > 150, n
+    assert not bad, bad[:10]
+
+
+def test_sd15_int8_eval_accuracy(sd15_int8):
+    """Stated tolerance of the int8-MFMA mode (one full-size SD1.5 UNet eval, latent space,
+    relative to max |fp16 output|):
+      * vs its own oracle: the self-calibrated W8A8 bound of tests/test_gpu_unet.py - within 1.5 x
+        the oracle's own Half-vs-fp32 spread + 2e-3 of BOTH oracle variants (the int8 layers are
+        exact; per-token / per-sample re-quantization amplifies the norms' / attention's ulps);
+      * vs the unquantized fp16 UNet: at most 2x the error of the reference's own fake-quant W8A8
+        (measured in the build container: int8 6.8 % max / 1.27 % mean vs fake-quant 5.2 % / 0.93 %)."""
+    f = sd15_int8
+    got, ri8, ri8h, r16, rfq = (f[kk].float() for kk in ("got", "ref_i8", "ref_i8h", "r16", "rfq"))
+    sc = r16.abs().max().item()
+    rel = lambda a, b: ((a - b).abs().max().item() / sc, (a - b).abs().mean().item() / sc)
+    s_mx, s_mean = rel(ri8, ri8h)
+    o_mx, o_mean = rel(got, ri8)
+    h_mx, h_mean = rel(got, ri8h)
+    i_mx, i_mean = rel(got, r16)
+    q_mx, q_mean = rel(rfq, r16)
+    print(f"SD1.5 int8 eval: gpu vs int8 oracle fp32 max {o_mx:.4g} mean {o_mean:.4g}, half max {h_mx:.4g} "
+          f"mean {h_mean:.4g} (oracle spread max {s_mx:.4g} mean {s_mean:.4g}) | gpu vs fp16 max {i_mx:.4g} "
+          f"mean {i_mean:.4g} | fake-quant W8A8 vs fp16 max {q_mx:.4g} mean {q_mean:.4g}")
+    assert torch.isfinite(got).all()
+    tmx, tmean = 1.5 * s_mx + 2e-3, 1.5 * s_mean + 2e-3
+    assert o_mx <= tmx and o_mean <= tmean and h_mx <= tmx and h_mean <= tmean
+    assert i_mx <= 2 * q_mx and i_mean <= 2 * q_mean
+
+
+@pytest.mark.parametrize("silu,concat,fq", [(True, False, False), (False, False, False), (True, True, False),
+                                            (True, False, True)])
+def test_groupnorm_i8_equals_quantized_groupnorm(dev, silu, concat, fq):
+    """GroupNorm(+SiLU) with fused int8 output == per-sample codes of the fp16 GroupNorm output."""
+    k = K()
+    g = torch.Generator().manual_seed(5)
+    n, h, w, c1, c2 = 2, 16, 16, 320, 320 if concat else 0
+    x = (torch.randn(n, h, w, c1, generator=g) * 3).half().to(dev)
+    x2 = (torch.randn(n, h, w, c2, generator=g)).half().to(dev) if concat else None
+    c = c1 + c2
+    gamma = (1 + 0.1 * torch.randn(c, generator=g)).half().to(dev)
+    beta = (0.1 * torch.randn(c, generator=g)).half().to(dev)
+    fq_in = None
+    if fq:
+        cadd = torch.randn(n, c, generator=g).half().to(dev)
+        fq_in = (None, 0, cadd)
+    ref16 = k.groupnorm_nhwc(x, 32, 1e-5, gamma, beta, silu=silu, x2=x2, fq_in=fq_in)
+    q_ref, s_ref = k.quant_samples_i8(ref16)
+    q, s = k.groupnorm_nhwc_i8(x, 32, 1e-5, gamma, beta, silu=silu, x2=x2, fq_in=fq_in)
+    assert torch.equal(s, s_ref) and torch.equal(q, q_ref)
+
+
+@pytest.mark.parametrize("rows,c", [(4096, 320), (1000, 640), (256, 1280), (77, 768)])
+def test_layernorm_i8_and_rows_equal_oracle(dev, rows, c):
+    k = K()
+    g = torch.Generator().manual_seed(rows + c)
+    x = (torch.randn(rows, c, generator=g) * 2).half().to(dev)
+    gamma = (1 + 0.1 * torch.randn(c, generator=g)).half().to(dev)
+    beta = (0.1 * torch.randn(c, generator=g)).half().to(dev)
+    ref16 = k.layernorm(x, 1e-5, gamma, beta)
+    q_ref, s_ref = R.quant_rows_i8(ref16.cpu().numpy())
+    q, s = k.layernorm_i8(x, 1e-5, gamma, beta)
+    assert np.array_equal(q.cpu().numpy(), q_ref) and np.array_equal(s.cpu().numpy(), s_ref)
+    q2, s2 = k.quant_rows_i8(ref16)
+    assert np.array_equal(q2.cpu().numpy(), q_ref) and np.array_equal(s2.cpu().numpy(), s_ref)
