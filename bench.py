@@ -10,9 +10,10 @@ Also reported (rank 0):
                 with HIP events on the stream it runs on; ALGORITHMIC flops / duration vs the
                 fp16 dense MFMA peak (the path computes fake-quant operands in fp16)
   path_roofline whole-loop FLOP rate (803.3 GFLOP per UNet eval per sample)
-  cpu_baseline  the reference's CPU path restated by the oracle (torch-CPU fp16 ops, W8A8
-                fake-quant) timed on this box's host cores on a bounded sample (one op of each
-                FLOP class; see cpu_baseline())
+  cpu_baseline  BASELINE.md §2: the reference's CPU path (config C1) restated by the oracle
+                (torch-CPU fp16 ops) timed on this box's host cores: every distinct op shape of a
+                UNet evaluation on a bounded slice, warm-up + median of 3 (see cpu_baseline())
+  int8_blended_roofline  images/s against the int8-MFMA-blended bound of north_star's target
 Secondary lines (same JSON contract): --model sdxl (SURVEY config C4: SDXL W8A8 1024^2, 2
 prompts per GPU, 50 EulerDiscrete steps) and --model sd35 (config C5: SD3.5-Large W4A16 g128
 1024^2, 1 prompt per GPU, flow-match Euler).
@@ -203,42 +204,31 @@ def pmc_traffic(variant=None):
 
 
 def cpu_baseline(threads):
-    """The reference's CPU fake-quant path (oracle restatement: torch-CPU fp16 ops, W8A8
-    per-channel act quant) on a BOUNDED sample: one op of each FLOP class of the SD1.5 UNet at
-    CFG batch 2 (1 image), timed on this host; the per-image time is the class FLOPs of
-    SURVEY App. B divided by the measured class rates (conv 443.9, linear 233.3, attention
-    126.1 GFLOP per sample per UNet eval; x2 CFG; x50 steps)."""
+    """the reference's CPU fake-quant path on config C1 (SD1.5 W8 RTN, 1 prompt,
+    512x512, 10 DDIM steps with CFG = 10 UNet evaluations at batch 2) restated by the oracle
+    (torch-CPU fp16 ops, bit-exact per op to the reference's goldens), timed on this host's cores:
+    every distinct op shape of one UNet evaluation (census of the oracle's own forward) on a
+    bounded slice, 1 warm-up + median of 3, scaled by FLOPs and summed with multiplicities
+    (oracle/cpu_baseline.py; a whole C1 run takes hours where torch's Half conv is scalar)."""
+    import dataclasses
     import torch
-    import torch.nn.functional as F
-    from oracle import fake_quant_torch as FT
-    torch.set_num_threads(threads)
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(2, 320, 64, 64, generator=g).half()
-    w = FT.weight_per_channel((torch.randn(320, 320, 3, 3, generator=g) * 0.02).half(), 8)
-    b = torch.zeros(320).half()
-    t0 = time.time()
-    FT.per_channel(F.conv2d(FT.per_channel(x, 8), w, b, 1, 1), 8)
-    t_conv = time.time() - t0
-    conv_rate = 2 * 2 * 4096 * 320 * 2880 / t_conv
-    xt = torch.randn(2, 4096, 320, generator=g).half()
-    wl = FT.weight_group((torch.randn(2560, 320, generator=g) * 0.05).half(), 8, 128)
-    t0 = time.time()
-    F.linear(xt, wl, torch.zeros(2560).half())
-    t_lin = time.time() - t0
-    lin_rate = 2 * 8192 * 2560 * 320 / t_lin
-    q = torch.randn(2, 8, 4096, 40, generator=g).half()
-    t0 = time.time()
-    F.scaled_dot_product_attention(q, q, q)
-    t_att = time.time() - t0
-    att_rate = 4 * 2 * 8 * 4096 * 4096 * 40 / t_att
-    per_eval = 2 * (443.9e9 / conv_rate + 233.3e9 / lin_rate + 126.1e9 / att_rate)
-    per_image = 50 * per_eval
-    return {"value": round(1.0 / per_image, 8), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": (f"one fp16 op per FLOP class at SD1.5 CFG batch 2: W8A8 conv3x3 320@64x64 {t_conv:.2f}s "
-                       f"({conv_rate / 1e9:.2f} GFLOP/s), linear 320->2560 x8192 {t_lin:.3f}s "
-                       f"({lin_rate / 1e9:.1f} GFLOP/s), SDPA 4096^2 d40 x16 heads {t_att:.3f}s "
-                       f"({att_rate / 1e9:.1f} GFLOP/s); image = 50 steps x class FLOPs / class rates"),
-            "seconds_per_image": round(per_image, 1)}
+    from oracle import cpu_baseline as CB
+    from qdiff.unet import SD15, UNet2DConditionModel
+    with torch.device("meta"):
+        net = UNet2DConditionModel(SD15)
+    shapes = {k: torch.empty(v.shape, dtype=torch.float16) for k, v in net.state_dict().items()}
+    cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(SD15).items()}
+    r = CB.c1_baseline(cd, shapes, threads=threads)
+    pc = r["per_class"]
+    return {"value": round(1.0 / r["seconds_per_image"], 8), "unit": "images/s", "cores": r["threads"],
+            "kind": "port", "cpu": r["cpu"], "config": "C1: SD1.5 W8 RTN fake-quant (A16), 1 prompt 512x512, "
+                                                       "10 DDIM steps + CFG (10 UNet evals at batch 2)",
+            "sample": (f"{r['distinct_shapes']} distinct op shapes / {r['ops_per_eval']} ops per UNet eval, each on a "
+                       f"bounded slice (1 warm-up + median of 3, scaled by FLOPs): conv2d "
+                       f"{pc['conv2d']['gflops']} GFLOP/s, linear {pc['linear']['gflops']} GFLOP/s, SDPA "
+                       f"{pc['sdpa']['gflops']} GFLOP/s; {r['seconds_per_unet_eval']:.1f} s per eval; sampling wall "
+                       f"{r['wall_s']:.1f} s; elementwise ops untimed (upper bound on CPU speed)"),
+            "per_class": pc, "seconds_per_image": round(r["seconds_per_image"], 1)}
 
 
 def launch_ranks(args):
@@ -598,12 +588,12 @@ def main_sdxl(args, model, rank, world, dev, log):
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
             base = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))
-            # the SD1.5 sample's per-image seconds scaled by the FLOP ratio of one SDXL image
+            # the SD1.5 C1 image's seconds scaled by the FLOP ratio of one SDXL image
             per_image = base["seconds_per_image"] * (2 * args.denoise_steps * SDXL_TFLOP_PER_SAMPLE * 1e12) / \
-                (2 * 50 * UNET_GFLOP_PER_SAMPLE * 1e9)
+                (2 * 10 * UNET_GFLOP_PER_SAMPLE * 1e9)
             line["cpu_baseline"] = {"value": round(1.0 / per_image, 10), "unit": "images/s", "cores": base["cores"],
                                     "kind": "port", "sample": base["sample"] + "; scaled to one SDXL 1024^2 image by "
-                                    "the FLOP ratio (6.76 TFLOP per SDXL eval vs 0.803 for SD1.5)",
+                                    "the FLOP ratio (6.76 TFLOP per SDXL eval vs 0.803 for SD1.5; 50 vs 10 steps)",
                                     "seconds_per_image": round(per_image, 1)}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -246,6 +246,15 @@ int qd_timestep_embedding(const float* timesteps, const int* step_idx, int b, in
 int qd_cfg_ddim_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
                      const float* alpha_t, const float* alpha_prev, int* step_idx,
                      void* next_in, int c, int c_pad, void* stream);
+/* CFG + PNDMScheduler.step with skip_prk_steps (PLMS; SD1.5's own scheduler_config) on fp16
+ * latents [B, L]: the linear multistep of the last <= 4 noise predictions (device ring `ets`,
+ * 4 * B * L fp16) and the step-1 re-evaluation (`cur`, B * L fp16), then
+ * prev = sqrt(a_prev / a_t) x - (a_prev - a_t) eps' / (a_t sqrt(1 - a_prev) + sqrt(a_t (1 - a_t) a_prev)).
+ * alpha_t / alpha_prev: fp32 [steps + 1] host tables (scheduler.pndm_tables); step index read
+ * from and incremented in `step_idx`; next_in as qd_cfg_ddim_step. */
+int qd_cfg_pndm_step(void* latents, const void* unet_out, int b, int64_t l, float guidance, const float* alpha_t,
+                     const float* alpha_prev, int* step_idx, void* ets, void* cur, void* next_in, int c, int c_pad,
+                     void* stream);
 /* CFG + EulerDiscreteScheduler.step (epsilon, s_churn 0; the SDXL pipeline's scheduler) on fp16
  * latents [B, L]: sample in fp32, x0 = x - sigma*eps, x += (x - x0)/sigma * (sigma_next - sigma);
  * writes the next UNet input [2B, L] = latents / dscale[i + 1] (scale_model_input).  sigmas,

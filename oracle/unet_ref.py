@@ -413,3 +413,69 @@ def denoise_euler(unet, latents, ctx, add_emb, timesteps, sigmas, init_sigma, gu
         eps = unet.forward(x, float(timesteps[i]), ctx, add_emb)
         lat = euler_step(eps, i, lat, sigmas, guidance)
     return lat
+
+
+# ------------------------------------------------------------------ PNDM (SD1.5's scheduler_config)
+def pndm_tables(num_inference_steps, num_train=1000, beta_start=0.00085, beta_end=0.012, steps_offset=1):
+    """PNDMScheduler.set_timesteps with skip_prk_steps: the PLMS timesteps (second one repeated)."""
+    ratio = num_train // num_inference_steps
+    t = (np.arange(0, num_inference_steps) * ratio).round().astype(np.int64) + steps_offset
+    return np.concatenate([t[:-1], t[-2:-1], t[-1:]])[::-1].copy(), ratio
+
+
+class PNDMRef:
+    """PNDMScheduler.step_plms restated with torch-CPU ops in diffusers' order (fp16 sample /
+    model_output tensors, fp32 0-d alphas): the multistep history ets, the counter-1 restart."""
+
+    def __init__(self, num_train=1000, beta_start=0.00085, beta_end=0.012, num_inference_steps=50):
+        betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train, dtype=torch.float32) ** 2
+        self.ac = torch.cumprod(1.0 - betas, dim=0)
+        self.final = self.ac[0]
+        self.ratio = num_train // num_inference_steps
+        self.ets, self.counter, self.cur = [], 0, None
+
+    def _prev_sample(self, sample, t, prev_t, mo):
+        a_t = self.ac[t]
+        a_p = self.ac[prev_t] if prev_t >= 0 else self.final
+        b_t, b_p = 1 - a_t, 1 - a_p
+        sample_coeff = (a_p / a_t) ** 0.5
+        denom = a_t * b_p ** 0.5 + (a_t * b_t * a_p) ** 0.5
+        return sample_coeff * sample - (a_p - a_t) * mo / denom
+
+    def step(self, mo, t, sample):
+        prev_t = t - self.ratio
+        if self.counter != 1:
+            self.ets = self.ets[-3:]
+            self.ets.append(mo)
+        else:
+            prev_t = t
+            t = t + self.ratio
+        if len(self.ets) == 1 and self.counter == 0:
+            self.cur = sample
+        elif len(self.ets) == 1 and self.counter == 1:
+            mo = (mo + self.ets[-1]) / 2
+            sample = self.cur
+            self.cur = None
+        elif len(self.ets) == 2:
+            mo = (3 * self.ets[-1] - self.ets[-2]) / 2
+        elif len(self.ets) == 3:
+            mo = (23 * self.ets[-1] - 16 * self.ets[-2] + 5 * self.ets[-3]) / 12
+        else:
+            mo = (1 / 24) * (55 * self.ets[-1] - 59 * self.ets[-2] + 37 * self.ets[-3] - 9 * self.ets[-4])
+        prev = self._prev_sample(sample, t, prev_t, mo)
+        self.counter += 1
+        return prev
+
+
+@torch.no_grad()
+def denoise_pndm(unet, latents, ctx, num_inference_steps, guidance=7.5, steps=None):
+    """The SD pipeline loop with PNDMScheduler (skip_prk_steps) on CPU."""
+    ts, _ = pndm_tables(num_inference_steps)
+    sch = PNDMRef(num_inference_steps=num_inference_steps)
+    lat = latents.to(F16)
+    n = len(ts) if steps is None else steps
+    for i in range(n):
+        eps = unet.forward(torch.cat([lat] * 2), int(ts[i]), ctx)
+        u, c = eps.chunk(2)
+        lat = sch.step(u + guidance * (c - u), int(ts[i]), lat)
+    return lat

@@ -46,6 +46,7 @@ SIGNATURES = {
     "qd_attention": [P, I, P, I, P, I, P, I, I, I, I, I, I, F, P],
     "qd_timestep_embedding": [P, P, I, I, I, F, P, P],
     "qd_cfg_ddim_step": [P, P, I, I64, F, P, P, P, P, I, I, P],
+    "qd_cfg_pndm_step": [P, P, I, I64, F, P, P, P, P, P, P, I, I, P],
     "qd_cfg_euler_discrete_step": [P, P, I, I64, F, P, P, P, P, I, I, P],
     "qd_scale_latents": [P, I64, F, F, P, I, I, P],
     "qd_channel_absmax_accum": [P, I64, I, P, P, P, P],

@@ -21,7 +21,7 @@ from torch import nn
 
 from .config import AwqConfig
 from .fake_quant import WxAxConv2d, WxAxLinear
-from .pipeline import DenoiseLoop, synthetic_text_embeddings
+from .pipeline import make_loop, synthetic_text_embeddings
 from .pipeline_io import QDiffPipeline, load_config, load_pipeline
 from .quantizer import AwqQuantizer, MyTraversal, SqQuantizer
 
@@ -63,10 +63,12 @@ class BaseAWQForDiffusion(nn.Module):
     @classmethod
     def from_pretrained(cls, model_path, model_type=None, torch_dtype=torch.float16, trust_remote_code=True,
                         safetensors=True, device_map="auto", download_kwargs=None, low_cpu_mem_usage=True,
-                        use_cache=False, refiner_path=None, token=None, device="cuda", seed=0,
+                        use_cache=False, refiner_path=None, token=None, device="cuda", seed=0, scheduler=None,
                         **model_init_kwargs):
-        """base.py:143-212 (local directories / synthetic names only; fp16 always, as base.py:199)."""
-        pipe = load_pipeline(model_path, device=device, seed=seed)
+        """base.py:143-212 (local directories / synthetic names only; fp16 always, as base.py:199).
+        The scheduler is the checkpoint's own (scheduler/scheduler_config.json: PNDM for SD1.5, as
+        DiffusionPipeline.from_pretrained builds it); scheduler="ddim" / "pndm" overrides it."""
+        pipe = load_pipeline(model_path, device=device, seed=seed, scheduler=scheduler)
         quant_config = AwqConfig.from_pretrained(model_path, is_diffusion_model=True)
         config = load_config(model_path)
         model_type = config["_class_name"]
@@ -132,9 +134,8 @@ class BaseAWQForDiffusion(nn.Module):
     def get_loop(self, batch, height, width, steps, guidance, use_graph=True):
         key = (batch, height, width, steps, float(guidance), use_graph)
         if key not in self._loops:
-            self._loops[key] = DenoiseLoop(self.pipeline.unet, batch, height, width, steps, guidance,
-                                           device=self.pipeline.device, use_graph=use_graph,
-                                           sched_cfg=self.pipeline.scheduler_config)
+            self._loops[key] = make_loop(self.pipeline.unet, batch, height, width, steps, guidance,
+                                         self.pipeline.device, use_graph, self.pipeline.scheduler_config)
         return self._loops[key]
 
     @torch.no_grad()

@@ -864,6 +864,94 @@ __global__ void k_cfg_ddim(f16* __restrict__ lat, const f16* __restrict__ uo, in
 __global__ void k_step_inc(int* step_idx) { step_idx[0] += 1; }
 
 // ---------------------------------------------------------------------------------------
+// CFG combine + PNDMScheduler.step with skip_prk_steps (the PLMS branch, step_plms) - the SD1.5
+// checkpoint's own scheduler (scheduler_config.json), which the reference's generate() runs
+// (models/base.py:848).  The multistep history ets (<= 4 past noise predictions) lives in a
+// device ring of 4 [B, L] slots, cur_sample in one more; the branch is taken from the device step
+// counter, so one graph replays every step.  Host tables give per step the (possibly shifted)
+// timestep's alpha_t and the previous one's alpha_prev (counter 1 re-evaluates the first step:
+// timestep + ratio -> timestep).  Op order / torch-CPU Half scalar semantics as k_cfg_ddim:
+//   i == 0 : ets = [e]; mo = e; cur = x
+//   i == 1 : mo = (e + ets[-1]) / 2; x = cur                      (ets unchanged)
+//   i >= 2 : ets.append(e) (last 4 kept); len 2: (3 e1 - e0) / 2; len 3: (23 e2 - 16 e1 + 5 e0) / 12;
+//            len 4: (1 / 24) * (55 e3 - 59 e2 + 37 e1 - 9 e0)
+//   prev = sc * x - (a_prev - a_t) * mo / denom,  sc = (a_prev / a_t) ** 0.5,
+//   denom = a_t * (1 - a_prev) ** 0.5 + (a_t * (1 - a_t) * a_prev) ** 0.5      (0-d fp32 scalars)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ f16 h_mul(float s, f16 x) { return (f16)(s * (float)x); }
+__device__ __forceinline__ f16 h_sub(f16 a, f16 b) { return (f16)((float)a - (float)b); }
+__device__ __forceinline__ f16 h_add(f16 a, f16 b) { return (f16)((float)a + (float)b); }
+
+__global__ void k_cfg_pndm(f16* __restrict__ lat, const f16* __restrict__ uo, int b, long l, float g,
+                           const float* __restrict__ at, const float* __restrict__ ap,
+                           const int* __restrict__ step_idx, f16* __restrict__ ets, f16* __restrict__ cur,
+                           f16* __restrict__ next_in, int c, int cp) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // over b * l
+  const long bl = (long)b * l;
+  if (e >= bl) return;
+  const int ch = e % cp;
+  const int si = step_idx[0];
+  f16 out = (f16)0.f;
+  if (ch < c) {
+    const long bi = e / l, off = e % l;
+    const float u = (float)uo[bi * l + off];
+    const float cc = (float)uo[((long)b + bi) * l + off];
+    const f16 gd = (f16)(g * (float)(f16)(cc - u));
+    const f16 eps = (f16)(u + (float)gd);
+    f16 x = lat[e], mo;
+    if (si == 0) {
+      ets[e] = eps;
+      cur[e] = x;
+      mo = eps;
+    } else if (si == 1) {
+      mo = (f16)((float)h_add(eps, ets[e]) / 2.0f);
+      x = cur[e];
+    } else {
+      const int k = si - 1;  // append index of this step's eps (step 0 was append 0)
+      ets[(long)(k & 3) * bl + e] = eps;
+      const f16 e1 = eps;
+      const f16 e0 = ets[(long)((k - 1) & 3) * bl + e];
+      if (si == 2) {
+        mo = (f16)((float)h_sub(h_mul(3.f, e1), e0) / 2.0f);
+      } else if (si == 3) {
+        const f16 em = ets[(long)((k - 2) & 3) * bl + e];  // ets[-3]
+        // (23 * e[-1] - 16 * e[-2] + 5 * e[-3]) / 12
+        mo = (f16)((float)h_add(h_sub(h_mul(23.f, e1), h_mul(16.f, e0)), h_mul(5.f, em)) / 12.0f);
+      } else {
+        const f16 em = ets[(long)((k - 2) & 3) * bl + e], en = ets[(long)((k - 3) & 3) * bl + e];
+        const f16 sum = h_sub(h_add(h_sub(h_mul(55.f, e1), h_mul(59.f, e0)), h_mul(37.f, em)), h_mul(9.f, en));
+        mo = h_mul((float)(1.0 / 24.0), sum);
+      }
+    }
+    const float a_t = at[si], a_p = ap[si];
+    const float sc = (float)(f16)sqrtf(a_p / a_t);                        // 0-d * half: scalar -> fp16
+    const float denom = a_t * sqrtf(1.0f - a_p) + sqrtf(a_t * (1.0f - a_t) * a_p);
+    const f16 t1 = (f16)(sc * (float)x);
+    const f16 t2 = (f16)((float)(f16)(a_p - a_t) * (float)mo);
+    const f16 t3 = (f16)((float)t2 / denom);                               // half / 0-d: scalar fp32
+    out = (f16)((float)t1 - (float)t3);
+  }
+  lat[e] = out;
+  if (next_in) {
+    next_in[e] = out;
+    next_in[bl + e] = out;
+  }
+}
+
+extern "C" int qd_cfg_pndm_step(void* latents, const void* unet_out, int b, int64_t l, float guidance,
+                                const float* alpha_t, const float* alpha_prev, int* step_idx, void* ets, void* cur,
+                                void* next_in, int c, int c_pad, void* stream) {
+  QD_REQUIRE(latents && unet_out && alpha_t && alpha_prev && step_idx && ets && cur, "null pointer");
+  QD_REQUIRE(c_pad >= c && l % c_pad == 0, "bad channel padding");
+  hipStream_t st = S(stream);
+  k_cfg_pndm<<<grid1((long)b * l), 256, 0, st>>>((f16*)latents, (const f16*)unet_out, b, l, guidance, alpha_t,
+                                                 alpha_prev, step_idx, (f16*)ets, (f16*)cur, (f16*)next_in, c, c_pad);
+  k_step_inc<<<1, 1, 0, st>>>(step_idx);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
 // CFG + EulerDiscreteScheduler.step (epsilon prediction, s_churn = 0) and the next step's
 // scale_model_input, in diffusers' op order with the torch-CPU scalar semantics above:
 //   eps   = u + g * (c - u)                                (fp16 ops)

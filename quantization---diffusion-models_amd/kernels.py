@@ -784,6 +784,23 @@ def unpatchify(tokens, b, h, w, p, c, out=None):
     return o
 
 
+def cfg_pndm_step(latents, unet_out, guidance, alpha_t, alpha_prev, step_idx, ets, cur, next_in=None, c=None):
+    """CFG + PNDMScheduler.step (PLMS, skip_prk_steps); latents NHWC [B, H, W, Cp] updated in
+    place; ets [4, B, H, W, Cp] / cur [B, H, W, Cp] fp16 device state of the multistep."""
+    _chk(latents, "latents")
+    _chk(unet_out, "unet_out")
+    _chk(ets, "ets")
+    _chk(cur, "cur")
+    b = latents.shape[0]
+    cp = latents.shape[-1]
+    l = latents.numel() // b
+    if ets.numel() != 4 * latents.numel() or cur.numel() != latents.numel():
+        raise ValueError("ets must hold 4 latent tensors and cur one")
+    _lib.call("qd_cfg_pndm_step", _p(latents), _p(unet_out), b, l, float(guidance), _p(alpha_t), _p(alpha_prev),
+              _p(step_idx), _p(ets), _p(cur), _p(next_in), c or cp, cp, _stream())
+    return latents
+
+
 def cfg_euler_step(latents, model_out, guidance, sigmas, step_idx, next_in=None):
     """CFG + FlowMatchEulerDiscreteScheduler.step; latents [B, ...] updated in place."""
     _chk(latents, "latents")

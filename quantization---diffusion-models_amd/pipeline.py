@@ -15,8 +15,8 @@ import torch
 
 from . import arena as A
 from . import kernels as K
-from .scheduler import (DDIMConfig, EulerDiscreteConfig, FlowMatchConfig, ddim_tables, euler_discrete_tables,
-                        flowmatch_tables)
+from .scheduler import (DDIMConfig, EulerDiscreteConfig, FlowMatchConfig, PNDMConfig, ddim_tables,
+                        euler_discrete_tables, flowmatch_tables, pndm_tables)
 
 C_PAD = 8
 
@@ -133,6 +133,44 @@ class DenoiseLoop:
 
     def latents_nchw(self):
         return K.nhwc_to_nchw(self.lat, self.cin)
+
+
+class PNDMDenoiseLoop(DenoiseLoop):
+    """SD1.5 with its checkpoint's own PNDMScheduler (skip_prk_steps PLMS): S + 1 UNet
+    evaluations, CFG + the linear-multistep step fused in one kernel whose noise-prediction history
+    (4 slots) and step-1 restart sample stay on device; same one-graph-per-step replay."""
+
+    def __init__(self, unet, batch, height=512, width=512, num_inference_steps=50, guidance_scale=7.5,
+                 device="cuda", use_graph=True, sched_cfg=PNDMConfig(), ctx_len=77):
+        super().__init__(unet, batch, height, width, num_inference_steps, guidance_scale, device, use_graph,
+                         sched_cfg, ctx_len)
+        ts, a_t, a_p = pndm_tables(num_inference_steps, sched_cfg)
+        self.timesteps = ts
+        self.ts_f32 = ts.to(torch.float32).to(self.device)
+        self.a_t = a_t.to(self.device)
+        self.a_p = a_p.to(self.device)
+        self.steps = len(ts)
+        self.ets = torch.zeros(4, *self.lat.shape, dtype=torch.float16, device=self.device)
+        self.cur = torch.zeros_like(self.lat)
+
+    @torch.no_grad()
+    def step(self, frozen=False):
+        with A.using(self.arena, frozen=frozen):
+            K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
+                                 shift=float(self.unet.config.freq_shift), out=self.temb_in)
+            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
+            K.cfg_pndm_step(self.lat, out, self.guidance, self.a_t, self.a_p, self.step_idx, self.ets, self.cur,
+                            self.next_in, c=self.cin)
+        self.last_out = out
+        return out
+
+
+def make_loop(unet, batch, height, width, steps, guidance, device, use_graph, sched_cfg, ctx_len=77):
+    """The UNet denoising loop of the pipeline's scheduler (DDIM or PNDM; SDXL's Euler loop is built
+    by its adapter)."""
+    cls = PNDMDenoiseLoop if isinstance(sched_cfg, PNDMConfig) else DenoiseLoop
+    return cls(unet, batch, height, width, steps, guidance, device=device, use_graph=use_graph, sched_cfg=sched_cfg,
+               ctx_len=ctx_len)
 
 
 class FlowMatchDenoiseLoop(DenoiseLoop):

@@ -15,7 +15,8 @@ import os
 import torch
 
 from .mmdit import SD35_LARGE, SD35_MEDIUM, MMDiTConfig, SD3Transformer2DModel, tiny_mmdit_config
-from .scheduler import DDIMConfig, EulerDiscreteConfig, FlowMatchConfig
+from .scheduler import (DDIMConfig, EulerDiscreteConfig, FlowMatchConfig, PNDMConfig, config_from_diffusers,
+                        config_to_diffusers)
 from .unet import SD15, SDXL, UNet2DConditionModel, UNetConfig, tiny_config, tiny_sdxl_config
 
 SYNTHETIC = {
@@ -72,16 +73,19 @@ class QDiffPipeline:
         from safetensors.torch import save_file
         name = self.denoiser_name
         os.makedirs(os.path.join(save_dir, name), exist_ok=True)
+        sched = config_to_diffusers(self.scheduler_config)
         if name == "unet":
-            sched = "EulerDiscreteScheduler" if self.class_name == "StableDiffusionXLPipeline" else "DDIMScheduler"
-            index = {"unet": ["diffusers", "UNet2DConditionModel"], "scheduler": ["diffusers", sched]}
+            index = {"unet": ["diffusers", "UNet2DConditionModel"], "scheduler": ["diffusers", sched["_class_name"]]}
             cls = "UNet2DConditionModel"
         else:
             index = {"transformer": ["diffusers", "SD3Transformer2DModel"],
-                     "scheduler": ["diffusers", "FlowMatchEulerDiscreteScheduler"]}
+                     "scheduler": ["diffusers", sched["_class_name"]]}
             cls = "SD3Transformer2DModel"
         with open(os.path.join(save_dir, "model_index.json"), "w") as f:
             json.dump({"_class_name": self.class_name, **index}, f, indent=2)
+        os.makedirs(os.path.join(save_dir, "scheduler"), exist_ok=True)
+        with open(os.path.join(save_dir, "scheduler", "scheduler_config.json"), "w") as f:
+            json.dump(sched, f, indent=2)
         cfg = dict(vars(self.denoiser.config))
         cfg = {k: (list(v) if isinstance(v, tuple) else v) for k, v in cfg.items()}
         cfg["_class_name"] = cls
@@ -111,10 +115,29 @@ def _load_weights(module, path, dtype):
         raise KeyError(f"weights missing keys (first 5): {missing[:5]}")
 
 
-def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16):
+def load_scheduler_config(model_path, override=None):
+    """The checkpoint's scheduler (scheduler/scheduler_config.json), as diffusers'
+    DiffusionPipeline.from_pretrained instantiates it (the reference's generate() runs that
+    scheduler, models/base.py:848); override: "ddim" / "pndm" / "euler" or a config object."""
+    if override is not None and not isinstance(override, str):
+        return override
+    if isinstance(override, str):
+        return {"ddim": DDIMConfig, "pndm": PNDMConfig, "euler": EulerDiscreteConfig,
+                "flowmatch": FlowMatchConfig}[override.lower()]()
+    if model_path in SYNTHETIC:
+        return None  # synthetic checkpoints: the measurement protocol's DDIM (SURVEY §8d) / model defaults
+    p = os.path.join(model_path, "scheduler", "scheduler_config.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return config_from_diffusers(json.load(f))
+
+
+def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16, scheduler=None):
     cfg = load_config(model_path)
     cls = cfg["_class_name"]
     mmdit = cls in MMDIT_PIPELINES
+    sched_cfg = load_scheduler_config(model_path, scheduler)
     if model_path in SYNTHETIC:
         mcfg = SYNTHETIC[model_path][1] or (tiny_mmdit_config() if mmdit else
                                             tiny_sdxl_config() if cls == "StableDiffusionXLPipeline" else tiny_config())
@@ -139,5 +162,5 @@ def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16):
     net.to(device)
     net.eval()
     if mmdit:
-        return QDiffPipeline(transformer=net, class_name=cls, config=cfg)
-    return QDiffPipeline(net, cls, config=cfg)
+        return QDiffPipeline(transformer=net, class_name=cls, config=cfg, scheduler_config=sched_cfg)
+    return QDiffPipeline(net, cls, config=cfg, scheduler_config=sched_cfg)

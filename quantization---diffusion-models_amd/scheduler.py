@@ -67,6 +67,71 @@ def ddim_tables(num_inference_steps, cfg: DDIMConfig = DDIMConfig()):
 
 
 @dataclass
+class PNDMConfig(DDIMConfig):
+    """PNDMScheduler of the SD1.5 checkpoints (scheduler/scheduler_config.json: skip_prk_steps
+    true, steps_offset 1, set_alpha_to_one false, the SD1.5 betas): the scheduler the reference's
+    generate() runs through the pipeline (models/base.py:848)."""
+    skip_prk_steps: bool = True
+
+
+def pndm_tables(num_inference_steps, cfg: PNDMConfig = PNDMConfig()):
+    """(timesteps int64 [S + 1], alpha_t f32 [S + 1], alpha_prev f32 [S + 1]) of
+    PNDMScheduler.set_timesteps + step_plms (skip_prk_steps): the PLMS timesteps repeat the
+    second one ([981, 961, 961, 941, ..., 1] for 50 steps, S + 1 UNet evaluations); step 1
+    re-evaluates step 0's interval (alphas of t + ratio -> t); prev_t < 0 -> final_alpha_cumprod."""
+    if not cfg.skip_prk_steps:
+        raise NotImplementedError("PNDM Runge-Kutta (prk) warm-up steps: the SD pipelines set skip_prk_steps")
+    ac = alphas_cumprod(cfg)
+    final = torch.tensor(1.0) if cfg.set_alpha_to_one else ac[0]
+    ratio = cfg.num_train_timesteps // num_inference_steps
+    t = (np.arange(0, num_inference_steps) * ratio).round().astype(np.int64) + cfg.steps_offset
+    ts = np.concatenate([t[:-1], t[-2:-1], t[-1:]])[::-1].copy()
+    a_t, a_p = [], []
+    for i, ti in enumerate(ts):
+        cur, prev = (int(ti) + ratio, int(ti)) if i == 1 else (int(ti), int(ti) - ratio)
+        a_t.append(ac[cur])
+        a_p.append(ac[prev] if prev >= 0 else final)
+    return torch.from_numpy(ts), torch.stack(a_t).float(), torch.stack(a_p).float()
+
+
+def config_from_diffusers(d):
+    """A scheduler config object from a diffusers scheduler_config.json dict (the local
+    checkpoint's own scheduler, as DiffusionPipeline.from_pretrained would build it)."""
+    name = d.get("_class_name", "DDIMScheduler")
+    if name == "FlowMatchEulerDiscreteScheduler":
+        return FlowMatchConfig(num_train_timesteps=d.get("num_train_timesteps", 1000), shift=d.get("shift", 3.0))
+    cls = {"DDIMScheduler": DDIMConfig, "PNDMScheduler": PNDMConfig,
+           "EulerDiscreteScheduler": EulerDiscreteConfig}.get(name)
+    if cls is None:
+        raise NotImplementedError(f"scheduler {name} has no device step kernel in this build")
+    kw = {k: d[k] for k in ("num_train_timesteps", "beta_start", "beta_end", "beta_schedule", "steps_offset",
+                            "set_alpha_to_one") if k in d}
+    if cls is PNDMConfig and "skip_prk_steps" in d:
+        kw["skip_prk_steps"] = d["skip_prk_steps"]
+    if d.get("prediction_type", "epsilon") != "epsilon":
+        raise NotImplementedError(f"prediction_type {d['prediction_type']}: the SD pipelines use epsilon")
+    if name == "EulerDiscreteScheduler" and d.get("timestep_spacing", "leading") != "leading":
+        raise NotImplementedError("EulerDiscreteScheduler timestep_spacing other than 'leading'")
+    return cls(**kw)
+
+
+def config_to_diffusers(cfg):
+    """scheduler_config.json dict of a scheduler config object (save_pretrained)."""
+    if isinstance(cfg, FlowMatchConfig):
+        return {"_class_name": "FlowMatchEulerDiscreteScheduler", "num_train_timesteps": cfg.num_train_timesteps,
+                "shift": cfg.shift}
+    name = {PNDMConfig: "PNDMScheduler", EulerDiscreteConfig: "EulerDiscreteScheduler"}.get(type(cfg), "DDIMScheduler")
+    d = {"_class_name": name, "num_train_timesteps": cfg.num_train_timesteps, "beta_start": cfg.beta_start,
+         "beta_end": cfg.beta_end, "beta_schedule": cfg.beta_schedule, "steps_offset": cfg.steps_offset,
+         "set_alpha_to_one": cfg.set_alpha_to_one, "prediction_type": "epsilon"}
+    if isinstance(cfg, PNDMConfig):
+        d["skip_prk_steps"] = cfg.skip_prk_steps
+    if isinstance(cfg, EulerDiscreteConfig):
+        d["timestep_spacing"] = "leading"
+    return d
+
+
+@dataclass
 class EulerDiscreteConfig(DDIMConfig):
     """EulerDiscreteScheduler of the SDXL base pipeline: the SD1.5 beta schedule, "leading"
     timestep spacing with steps_offset 1, epsilon prediction, linear sigma interpolation."""

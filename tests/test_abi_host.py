@@ -196,3 +196,51 @@ def test_sdxl_tiny_tree_and_oracle_euler_runs():
     out = denoise_euler(r, torch.randn(1, 4, 16, 16, generator=g).half(), torch.randn(2, 77, 64, generator=g).half(),
                         add, ts, sig, init)
     assert out.shape == (1, 4, 16, 16) and torch.isfinite(out.float()).all()
+
+
+def test_scheduler_config_roundtrip_and_pndm_tables(tmp_path):
+    """A checkpoint's scheduler/scheduler_config.json selects the device loop's scheduler (the
+    reference's generate() runs the pipeline's own scheduler, models/base.py:848): PNDM for SD1.5."""
+    import json
+    from oracle.unet_ref import PNDMRef, pndm_tables as oracle_tables
+    from qdiff import pipeline_io as PIO
+    from qdiff.scheduler import (DDIMConfig, EulerDiscreteConfig, PNDMConfig, config_from_diffusers,
+                                 config_to_diffusers, pndm_tables)
+    sd15 = {"_class_name": "PNDMScheduler", "beta_end": 0.012, "beta_schedule": "scaled_linear",
+            "beta_start": 0.00085, "num_train_timesteps": 1000, "set_alpha_to_one": False, "skip_prk_steps": True,
+            "steps_offset": 1, "trained_betas": None, "clip_sample": False}
+    cfg = config_from_diffusers(sd15)
+    assert isinstance(cfg, PNDMConfig) and cfg.skip_prk_steps
+    for c in (cfg, DDIMConfig(), EulerDiscreteConfig()):
+        assert config_from_diffusers(config_to_diffusers(c)) == c
+    os_ = tmp_path / "scheduler"
+    os_.mkdir()
+    (os_ / "scheduler_config.json").write_text(json.dumps(sd15))
+    assert isinstance(PIO.load_scheduler_config(str(tmp_path)), PNDMConfig)
+    assert isinstance(PIO.load_scheduler_config(str(tmp_path), "ddim"), DDIMConfig)
+    ts, a_t, a_p = pndm_tables(50)
+    assert ts.tolist() == oracle_tables(50)[0].tolist() and len(ts) == 51
+    r = PNDMRef()
+    assert a_t[1].item() == r.ac[981].item() and a_p[1].item() == r.ac[961].item()   # counter-1 restart
+    assert a_p[-1].item() == r.final.item()
+
+
+def test_cpu_baseline_census_covers_the_unet():
+    """The C1 CPU baseline times every op of a UNet evaluation: the census of the oracle's own
+    forward finds SD1.5's 98 convs, 184 linears, 32 SDPA, 61 GroupNorms and 48 LayerNorms with the
+    analytic FLOPs of SURVEY App. B (x CFG batch 2)."""
+    import dataclasses
+    from oracle import cpu_baseline as CB
+    from qdiff.unet import SD15, UNet2DConditionModel
+    with torch.device("meta"):
+        net = UNet2DConditionModel(SD15)
+    sd = {k: torch.empty(v.shape, dtype=torch.float16) for k, v in net.state_dict().items()}
+    cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(SD15).items()}
+    cen = CB.census(cd, sd)
+    count, flop = {}, {}
+    for (op, s), n in cen.items():
+        count[op] = count.get(op, 0) + n
+        flop[op] = flop.get(op, 0.0) + n * CB._flops(op, s)
+    assert count == {"conv2d": 98, "linear": 184, "sdpa": 32, "group_norm": 61, "layer_norm": 48}
+    assert abs(flop["conv2d"] / 2e9 - 443.9) < 1 and abs(flop["linear"] / 2e9 - 233.3) < 1
+    assert abs(flop["sdpa"] / 2e9 - 126.1) < 1

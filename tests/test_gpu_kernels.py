@@ -554,3 +554,31 @@ def test_linear_gelu_tanh_epilogue(variant, forced_gemm, dev):
         # a 1-ulp move of the pre-activation propagates through gelu' <= 1.13
         tol = 1.13 * ulp16(pre.float()) + ulp16(ref) + 1e-3
         assert ((y - ref).abs() <= tol).all(), (variant, M, N, Kd, (y - ref).abs().max())
+
+
+def test_cfg_pndm_step_bit_exact_vs_torch_pndm(dev):
+    """CFG + PNDMScheduler.step_plms (skip_prk_steps) on device == the torch-CPU restatement in
+    diffusers' op order (oracle/unet_ref.py PNDMRef), bit for bit, over every branch: the first
+    step, the counter-1 restart, the 2-, 3- and 4-term multisteps and the final alpha."""
+    from oracle.unet_ref import PNDMRef
+    from qdiff.scheduler import pndm_tables
+    k = K()
+    steps = 8
+    ts, a_t, a_p = pndm_tables(steps)
+    g = torch.Generator().manual_seed(4)
+    b, h, w, c, cp = 2, 8, 8, 4, 8
+    lat0 = torch.randn(b, c, h, w, generator=g).half()
+    lat = k.nchw_to_nhwc(lat0.to(dev), cp)
+    ets = torch.zeros(4, *lat.shape, dtype=torch.float16, device=dev)
+    cur = torch.zeros_like(lat)
+    idx = torch.zeros(1, dtype=torch.int32, device=dev)
+    at_d, ap_d = a_t.to(dev), a_p.to(dev)
+    ref = PNDMRef(num_inference_steps=steps)
+    rl = lat0
+    for i in range(len(ts)):
+        uo = (torch.randn(2 * b, c, h, w, generator=g) * 0.5).half()
+        k.cfg_pndm_step(lat, k.nchw_to_nhwc(uo.to(dev), cp), 7.5, at_d, ap_d, idx, ets, cur, c=c)
+        u, cc = uo.chunk(2)
+        rl = ref.step(u + 7.5 * (cc - u), int(ts[i]), rl)
+        got = k.nhwc_to_nchw(lat, c).cpu()
+        assert same_bits(got.numpy(), rl.numpy()), (i, (got.float() - rl.float()).abs().max().item())

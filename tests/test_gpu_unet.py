@@ -423,3 +423,40 @@ def _half_conv_usable():
     t0 = time.time()
     F.conv2d(x, w, padding=1)
     return 2 * 1024 * 64 * 576 / max(time.time() - t0, 1e-9) >= 20e9
+
+
+def test_pndm_denoise_matches_oracle():
+    """SD1.5 with its checkpoint scheduler (PNDM): a local checkpoint whose
+    scheduler/scheduler_config.json names PNDMScheduler runs the PLMS loop (S + 1 evals), graph ==
+    eager, and matches the oracle loop within the tight (no activation quant) bound."""
+    import os
+    import tempfile
+    from oracle.unet_ref import denoise_pndm
+    from qdiff.models import AWQ, StableDiffusion1_x
+    from qdiff.scheduler import PNDMConfig
+    base = _model(seed=6)
+    with tempfile.TemporaryDirectory() as d:
+        base.pipeline.scheduler_config = PNDMConfig()
+        base.pipeline.save_pretrained(d)
+        assert os.path.exists(os.path.join(d, "scheduler", "scheduler_config.json"))
+        model = AWQ.from_pretrained(d)
+    assert isinstance(model.pipeline.scheduler_config, PNDMConfig)
+    cfg = model.pipeline.unet.config
+    sd = {k: v.detach().cpu() for k, v in model.pipeline.unet.state_dict().items()}
+    g = torch.Generator().manual_seed(8)
+    lat = torch.randn(1, 4, cfg.sample_size, cfg.sample_size, generator=g).half()
+    pe = torch.randn(1, 77, cfg.cross_attention_dim, generator=g).half()
+    ne = torch.randn(1, 77, cfg.cross_attention_dim, generator=g).half()
+    hw = cfg.sample_size * 8
+    kw = dict(prompt_embeds=pe, negative_prompt_embeds=ne, lat=lat, height=hw, width=hw, num_inference_steps=4,
+              output_type="latent")
+    eager = model.generate(use_graph=False, **kw).cpu()
+    graph = model.generate(use_graph=True, **kw).cpu()
+    assert torch.equal(eager, graph)
+    assert model.get_loop(1, hw, hw, 4, 7.5).steps == 5
+    ref = denoise_pndm(RefUNet(_cfgdict(cfg), sd, None), lat, torch.cat([ne, pe]), 4)
+    mx, mean = _rel_errs(graph, ref)
+    print(f"PNDM 4-step (5 evals) tiny W16: gpu-vs-oracle max {mx:.4g} mean {mean:.4g}")
+    # the per-eval bound of the tight single-eval test (4e-3 / 6e-4), compounded over 5 evals
+    # through the 4-term multistep (weights up to 55/24): max 1e-2 / mean 2e-3 (measured 4.8e-3 / 9.6e-4)
+    assert mx <= 1e-2 and mean <= 2e-3
