@@ -161,11 +161,16 @@ class BaseAWQForDiffusion(nn.Module):
         return loop.run(lat.to(self.pipeline.device), ctx)
 
     # ---------------------------------------------------------------- save / load
-    def save_quantized(self, save_dir, safetensors=True, shard_size="5GB", export_compatible=False, quant_act=False):
+    def save_quantized(self, save_dir, safetensors=True, shard_size="5GB", export_compatible=False, quant_act=False,
+                       awq_export=True):
         """base.py:530-582: pipeline files + quantization_config in each quantized component's
         config.json + quant_components.json (reference-compatible fp16 dequantized buffers), plus
-        our extension: the integer codes / scales (unet/qdiff_codes.safetensors) and the full
-        quant config (qdiff_quant.json)."""
+        this build's integer formats (export.py): every linear's codes / scales and every conv's
+        codes (the reference's per-(Co, Ci, kh) granularity, and the int8-MFMA mode's
+        per-output-channel codes) in <denoiser>/qdiff_codes.safetensors, the 4-bit linears also in
+        the AWQ GEMM layout (<denoiser>/awq_gemm.safetensors: qweight / qzeros / scales, the
+        reference's utils/quant_utils.py / packing_utils.py order), and the full quant config
+        (qdiff_quant.json)."""
         from safetensors.torch import save_file
         save_dir = save_dir[:-1] if save_dir.endswith("/") else save_dir
         os.makedirs(save_dir, exist_ok=True)
@@ -182,15 +187,33 @@ class BaseAWQForDiffusion(nn.Module):
         with open(os.path.join(save_dir, "quant_components.json"), "w") as f:
             json.dump(self.quantized_components, f, indent=2)
         with open(os.path.join(save_dir, "qdiff_quant.json"), "w") as f:
-            json.dump(self.quant_config.full_dict(), f, indent=2)
-        codes = {}
+            json.dump(dict(self.quant_config.full_dict(), int8_mfma=bool(getattr(self, "int8_mfma", False))), f,
+                      indent=2)
+        from .export import awq_pack_linear, conv_codes, packed_nibbles_to_codes
+        codes, awq = {}, {}
         for name, m in self.pipeline.denoiser.named_modules():
-            if isinstance(m, WxAxLinear) and m.qcodes is not None:
+            if isinstance(m, WxAxLinear) and m.gemm_weight()[1] != "f16":
                 codes[f"{name}.qcodes"] = m.qcodes.detach().cpu().contiguous()
                 codes[f"{name}.qscales"] = m.qscales.detach().cpu().contiguous()
-                codes[f"{name}.qmeta"] = torch.tensor([m.qgroup, m.n_bits_W], dtype=torch.int32)
+                codes[f"{name}.qmeta"] = torch.tensor([m.qgroup, m.n_bits_W, int(m.int8_mfma)], dtype=torch.int32)
+                if awq_export and m.qfmt == "i4":
+                    c = packed_nibbles_to_codes(m.qcodes, m.in_features)
+                    for k, v in awq_pack_linear(c, m.qscales, m.qgroup).items():
+                        awq[f"{name}.{k}"] = v.detach().cpu().contiguous()
+            elif isinstance(m, WxAxConv2d):
+                i8 = m.i8_operand()
+                if i8 is not None:
+                    codes[f"{name}.i8_w"] = i8[0].detach().cpu().contiguous()
+                    codes[f"{name}.i8_sw"] = i8[1].detach().cpu().contiguous()
+                elif m.weight_quant_name == "per_channel" and getattr(m, "n_bits_W", 16) <= 8:
+                    cc, cs = conv_codes(m.weight.detach(), m.n_bits_W)
+                    codes[f"{name}.conv_qcodes"] = cc.cpu().contiguous()
+                    codes[f"{name}.conv_qscales"] = cs.cpu().contiguous()
+        sub = os.path.join(save_dir, self.pipeline.denoiser_name)
         if codes:
-            save_file(codes, os.path.join(save_dir, self.pipeline.denoiser_name, "qdiff_codes.safetensors"))
+            save_file(codes, os.path.join(sub, "qdiff_codes.safetensors"))
+        if awq:
+            save_file(awq, os.path.join(sub, "awq_gemm.safetensors"))
 
     def _load_quantized_modules(self, module, bitWidth=4, group_size=128, act_bits=16, full_config=None):
         return load_quantized_modules(module, bitWidth, group_size, act_bits, full_config)
@@ -221,27 +244,48 @@ class BaseAWQForDiffusion(nn.Module):
         if os.path.exists(fpath):
             with open(fpath) as f:
                 full = json.load(f)
-        qcfg = AwqConfig(**full) if full else AwqConfig(**AwqConfig.from_transformers_dict(AwqConfig, qc))
+        if full:
+            from dataclasses import fields as _fields
+            qcfg = AwqConfig(**{f.name: full[f.name] for f in _fields(AwqConfig) if f.name in full})
+        else:
+            qcfg = AwqConfig(**AwqConfig.from_transformers_dict(AwqConfig, qc))
         load_quantized_modules(net, bitWidth=qc["bits"], group_size=qc["group_size"], act_bits=qc["act_bits"],
                                full_config=full)
         sd = load_file(os.path.join(model_path, sub, "diffusion_pytorch_model.safetensors"))
         net.load_state_dict({k: v.to(device) for k, v in sd.items()}, strict=True)
         cpath = os.path.join(model_path, sub, "qdiff_codes.safetensors")
         codes = load_file(cpath) if os.path.exists(cpath) else {}
+        apath = os.path.join(model_path, sub, "awq_gemm.safetensors")
+        awq = load_file(apath) if os.path.exists(apath) and not codes else {}
+        int8 = bool((full or {}).get("int8_mfma", False))
         for name, m in net.named_modules():
+            if isinstance(m, WxAxConv2d):
+                if f"{name}.i8_w" in codes:
+                    _attach_conv_i8(m, codes[f"{name}.i8_w"].to(device), codes[f"{name}.i8_sw"].to(device))
+                continue
             if not isinstance(m, WxAxLinear):
                 continue
             if f"{name}.qcodes" in codes:
-                g, nb = codes[f"{name}.qmeta"].tolist()
+                meta = codes[f"{name}.qmeta"].tolist()
+                g, nb = meta[0], meta[1]
                 m.qcodes = codes[f"{name}.qcodes"].to(device)
                 m.qscales = codes[f"{name}.qscales"].to(device)
                 m.qgroup, m.n_bits_W = g, nb
                 m.qfmt = "i4" if nb <= 4 else "i8"
                 m._codes_ver = (m.weight.data_ptr(), m.weight._version)
+                m.int8_mfma = bool(meta[2]) if len(meta) > 2 else False
+            elif f"{name}.qweight" in awq:
+                from .export import awq_unpack_linear
+                from .kernels import pack_int4
+                c, sc = awq_unpack_linear(awq[f"{name}.qweight"], awq[f"{name}.qzeros"], awq[f"{name}.scales"],
+                                          qc["group_size"] if m.in_features % qc["group_size"] == 0 else
+                                          m.in_features // awq[f"{name}.scales"].shape[0])
+                m.set_codes(c.to(device), sc.to(device), m.in_features // sc.shape[1], 4)
             else:
                 # a reference-written checkpoint holds only the dequantized fp16 buffers: re-derive
                 # the integer codes and keep them only if they reproduce the buffer bit for bit
                 rederive_codes(m, qc["bits"], qc["group_size"])
+                m.int8_mfma = int8 and m.qfmt == "i8" and m.qgroup == m.in_features
         if sub == "transformer":
             pipe = QDiffPipeline(transformer=net, class_name=cls_name, config={"_class_name": cls_name})
         else:
@@ -255,7 +299,23 @@ class BaseAWQForDiffusion(nn.Module):
             obj.quant_config = qcfg
             obj._loops = {}
         obj.quantized_components = comps
+        obj.int8_mfma = bool((full or {}).get("int8_mfma", False))
         return obj
+
+
+@torch.no_grad()
+def _attach_conv_i8(m, codes, sw):
+    """int8-MFMA conv codes from a checkpoint; kept only if they dequantize to the stored buffer."""
+    co, ci, kh, kw = m.weight.shape
+    deq = (codes.float() * sw[:, None, None, None]).to(torch.float16)[..., :ci].permute(0, 3, 1, 2)
+    if not torch.equal(deq.float(), m.weight.float()):  # value-equal (-0.0 of the fp16 buffer)
+        return False
+    m.i8_w, m.i8_sw = codes.contiguous(), sw.contiguous()
+    m._i8_ver = (m.weight.data_ptr(), m.weight._version)
+    m.quantise_act = False
+    m.output_quant_name = "None"
+    m.output_quant = lambda x: x
+    return True
 
 
 @torch.no_grad()

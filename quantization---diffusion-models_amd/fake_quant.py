@@ -448,6 +448,7 @@ class WxAxConv2d(nn.Module):
             raise ValueError(f"Invalid weight_quant: {weight_quant}")
         new.weight.copy_(wdq)
         new.weight_quant_name = weight_quant
+        new.n_bits_W = n_bits_W
         if module.bias is not None:
             new.bias.copy_(module.bias.to(torch.float16))
         if int8_mfma and n_bits_W == 8 and new.set_int8(w):

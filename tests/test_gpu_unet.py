@@ -460,3 +460,54 @@ def test_pndm_denoise_matches_oracle():
     # the per-eval bound of the tight single-eval test (4e-3 / 6e-4), compounded over 5 evals
     # through the 4-term multistep (weights up to 55/24): max 1e-2 / mean 2e-3 (measured 4.8e-3 / 9.6e-4)
     assert mx <= 1e-2 and mean <= 2e-3
+
+
+@pytest.mark.parametrize("qc,i8", [(dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False), False),
+                                   (dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True), True)])
+def test_save_load_integer_formats(tmp_path, qc, i8):
+    """On-disk integer formats: int4 linears in the AWQ GEMM layout decode (through
+    the oracle's restatement of the reference's unpack_awq / reverse_awq_order / dequantize_gemm)
+    to the module buffers bit for bit; conv codes (per (Co, Ci, kh)) dequantize to the conv
+    buffers; int8-MFMA checkpoints reload into the int8 path; every reload evaluates identically."""
+    import numpy as np
+    from safetensors.torch import load_file
+    from oracle import awq_pack as AP
+    from qdiff.export import dequant_conv_codes
+    from qdiff.fake_quant import WxAxConv2d, WxAxLinear
+    from qdiff.models import StableDiffusion1_x
+    model = _model(seed=9)
+    model.quantize(quant_config=dict(qc), quantUnet=True, int8_mfma=i8)
+    model.save_quantized(str(tmp_path))
+    codes = load_file(str(tmp_path / "unet" / "qdiff_codes.safetensors"))
+    mods = dict(model.pipeline.unet.named_modules())
+    n_awq = n_conv = n_i8 = 0
+    if not i8:
+        awq = load_file(str(tmp_path / "unet" / "awq_gemm.safetensors"))
+        for key in [k for k in awq if k.endswith(".qweight")]:
+            name = key[: -len(".qweight")]
+            m = mods[name]
+            deq = AP.dequantize_gemm(awq[key].numpy(), awq[name + ".qzeros"].numpy(), awq[name + ".scales"].numpy(),
+                                     m.qgroup)
+            assert np.array_equal(deq.T.astype(np.float32), m.weight.float().cpu().numpy()), name
+            n_awq += 1
+        assert n_awq == sum(isinstance(m, WxAxLinear) and m.qfmt == "i4" for m in mods.values()) > 0
+    for name, m in mods.items():
+        if isinstance(m, WxAxConv2d) and name + ".conv_qcodes" in codes:
+            deq = dequant_conv_codes(codes[name + ".conv_qcodes"], codes[name + ".conv_qscales"])
+            assert torch.equal(deq.float(), m.weight.float().cpu()), name
+            n_conv += 1
+        if isinstance(m, WxAxConv2d) and name + ".i8_w" in codes:
+            n_i8 += 1
+    assert (n_i8 > 0) if i8 else (n_conv == sum(isinstance(m, WxAxConv2d) for m in mods.values()))
+    re = StableDiffusion1_x.from_quantized(str(tmp_path), "StableDiffusionPipeline")
+    rmods = dict(re.pipeline.unet.named_modules())
+    for name, m in mods.items():
+        if isinstance(m, WxAxLinear):
+            assert rmods[name].gemm_weight()[1] == m.gemm_weight()[1] and rmods[name].int8_mfma == m.int8_mfma, name
+        if isinstance(m, WxAxConv2d):
+            assert (rmods[name].i8_operand() is None) == (m.i8_operand() is None), name
+    cfg = model.pipeline.unet.config
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 4, cfg.sample_size, cfg.sample_size, generator=g).half()
+    ctx = torch.randn(2, 77, cfg.cross_attention_dim, generator=g).half()
+    assert torch.equal(_one_eval(model, x, 501, ctx), _one_eval(re, x, 501, ctx))

@@ -174,3 +174,30 @@ def test_install_decisions(golden):
             if k.startswith(tag + "_quant|"):
                 key = k.split("|", 1)[1]
                 assert same_bits(qsd[key].numpy(), g[k]), key
+
+
+def test_awq_pack_oracle_and_export_vs_reference_golden():
+    """The reference's own AWQ int4 packing (tests/golden/awq_pack_golden.npz): the oracle's
+    unpack / dequantize restatement reproduces it, and this build's exporter writes the same words
+    the reference's pack (AWQ_PACK_ORDER, column direction) writes; round trip through the AWQ order."""
+    import os
+    from oracle import awq_pack as AP
+    from qdiff import export as E
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "awq_pack_golden.npz"))
+    iw = AP.reverse_awq_order(AP.unpack_awq(g["qweight"]))
+    assert np.array_equal(iw, g["iweight"]) and np.array_equal(iw, g["unpacked_iweight"])
+    deq = AP.dequantize_gemm(g["qweight"], g["qzeros"], g["scales"], 128)
+    assert np.array_equal(deq.view(np.uint16), g["dequantize_gemm"].view(np.uint16))
+    assert np.array_equal(E._pack_cols(torch.from_numpy(g["iweight"])).numpy(), g["qweight"])
+    assert np.array_equal(E._pack_cols(torch.from_numpy(g["izeros"])).numpy(), g["qzeros"])
+    assert np.array_equal(E._unpack_cols(torch.from_numpy(g["qweight"])).numpy(), g["iweight"])
+    # symmetric codes -> AWQ (zero 8) -> reference dequantize == half(q * s)
+    rng = np.random.default_rng(3)
+    codes = torch.from_numpy(rng.integers(-8, 8, (64, 256)).astype(np.int8))
+    sc = torch.from_numpy((rng.random((64, 2)) * 0.05 + 1e-3).astype(np.float16))
+    d = E.awq_pack_linear(codes, sc, 128)
+    deq = AP.dequantize_gemm(d["qweight"].numpy(), d["qzeros"].numpy(), d["scales"].numpy(), 128)
+    ref = (codes.float() * sc.float().repeat_interleave(128, 1)).half().numpy()
+    assert np.array_equal(deq.T.view(np.uint16), ref.view(np.uint16))
+    c2, s2 = E.awq_unpack_linear(d["qweight"], d["qzeros"], d["scales"], 128)
+    assert torch.equal(c2, codes) and torch.equal(s2, sc)
