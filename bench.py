@@ -180,6 +180,27 @@ def _conv_choice(shape=(8, 64, 64, 320), kind="conv"):
     return None
 
 
+def linear_families():
+    """GEMM family the tuner chose for each linear shape of the loop, counted per operand:
+    packed int4 / int8 codes dequantized in the register-tile staging (k_gemm) or the fp16
+    dequantized copy through the LDS-DMA / ping-pong families; int8-MFMA linears separately."""
+    from qdiff import kernels as K
+    fam = {}
+    for key, ch in K.gemm_choices().items():
+        if ch is None:
+            continue
+        if key[0] == "linear_i8":
+            name = "int8 codes -> k_gemm_dma<I8>"
+        elif key[0] == "linear":
+            fmt, v = key[-1][ch[0]], ch[1]
+            kind = "k_gemm_pp" if v >= 300 else "k_gemm_dma" if v >= 100 else "k_gemm register tile"
+            name = f"{key[-1][0]} weights: {fmt} operand -> {kind}"
+        else:
+            continue
+        fam[name] = fam.get(name, 0) + 1
+    return fam
+
+
 def pmc_traffic(variant=None):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 --pmc
     measurement (profiles/*pmc_dominant.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes over
@@ -330,8 +351,9 @@ def main():
         # north_star's target metric: images/s against the int8-blended bound of one GPU
         # (int8-eligible GEMM FLOP at the int8 peak + attention FLOP at the fp16 peak)
         t_min = SD15_I8_FLOP_PER_IMAGE / (PEAK_I8_TOPS * 1e12) + SD15_F16_FLOP_PER_IMAGE / (PEAK_F16_TFLOPS * 1e12)
+        wq = "W8A8" if args.mode.startswith("w8a8") else args.mode.upper()
         line = {
-            "metric": "images/sec SD1.5 W8A8 512x512 50-step",
+            "metric": f"images/sec SD1.5 {wq} {args.res}x{args.res} 50-step",
             "value": round(value, 4), "unit": "images/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "i8 (int32 accumulate) + f16" if int8 else "f16",
@@ -349,6 +371,7 @@ def main():
                                       "target_frac": 0.40,
                                       "basis": "67.72 TFLOP int8-eligible @ 5.0 POPS + 12.61 TFLOP attention @ 2.5 PF "
                                                "per 512^2 image (SURVEY 8d)"},
+            "linear_kernel_choice": linear_families(),
         }
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")

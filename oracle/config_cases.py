@@ -1,0 +1,84 @@
+"""BASELINE.json's configs as full-size oracle cases - TEST INFRASTRUCTURE ONLY (tests/ and
+tests/golden/make_config_golden.py; the product never imports oracle/).
+
+  c1  configs[0]: SD1.5 UNet W8 RTN fake-quant (A16), 1 prompt, 512x512, 10 DDIM steps + CFG
+  c3  configs[2]: SD1.5 W4A16 g128, 512x512, batch 8 (CFG batch 16), one UNet evaluation
+  c4  configs[3]: SDXL W8A8 g128, 1024x1024, the 2 prompts one of the 8 GPUs holds (CFG batch 4),
+      one UNet evaluation with the "text_time" conditioning
+
+The weights are the synthetic checkpoints' (N(0, 1/fan_in) drawn on the CPU
+generator, seed 0), so the build container and the GPU box hold the same bits; the inputs are
+drawn here from fixed seeds.  The half oracle (torch-CPU Half kernels, the reference's library
+calls) is only fast where torch has vectorised fp16 CPU kernels (this container's AVX512-FP16
+Xeon; the GPU box's host runs a scalar Half conv at ~0.7 GFLOP/s), so its outputs - and the fp32
+oracle's, for the same reason of box time - are computed once here and committed as
+tests/golden/config_golden.safetensors; `fingerprint` pins the weights they were computed from.
+"""
+import dataclasses
+
+import torch
+
+from .unet_ref import RefUNet, ddim_tables, denoise
+
+F16 = torch.float16
+
+CASES = {
+    "c1": dict(model="sd15", qc=dict(w_bit=8, a_bit=16, q_group_size=128, quantize_act=False),
+               prompts=1, res=512, steps=10, guidance=7.5, seed=1001),
+    "c3": dict(model="sd15", qc=dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
+               prompts=8, res=512, t=801, seed=1003),
+    "c4": dict(model="sdxl", qc=dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
+               prompts=2, res=1024, t=961.0, seed=1004),
+}
+
+
+def cfgdict(cfg):
+    return {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(cfg).items()}
+
+
+def fingerprint(sd):
+    """float64 sum over every tensor of (index-weighted) values: changes with any weight drift."""
+    tot = 0.0
+    for i, k in enumerate(sorted(sd)):
+        v = sd[k].detach().to("cpu", torch.float64).reshape(-1)
+        tot += (i + 1) * float(v.sum()) + float(v[: 4096].abs().sum())
+    return tot
+
+
+def inputs(name, cfg):
+    """Seeded fp16 CPU inputs of case `name` for the UNet config `cfg`."""
+    c = CASES[name]
+    g = torch.Generator().manual_seed(c["seed"])
+    b, hw = c["prompts"], c["res"] // 8
+    d = cfg.cross_attention_dim
+    if name == "c1":
+        lat = torch.randn(b, 4, hw, hw, generator=g).half()
+        pe = torch.randn(b, 77, d, generator=g).half()
+        ne = torch.randn(b, 77, d, generator=g).half()
+        return dict(lat=lat, pe=pe, ne=ne)
+    x = torch.randn(2 * b, 4, hw, hw, generator=g).half()
+    ctx = torch.randn(2 * b, 77, d, generator=g).half()
+    out = dict(x=x, ctx=ctx)
+    if name == "c4":
+        pooled = cfg.projection_class_embeddings_input_dim - 6 * cfg.addition_time_embed_dim
+        out["text"] = torch.randn(2 * b, pooled, generator=g).half()
+        res = c["res"]
+        out["time_ids"] = torch.tensor([[res, res, 0, 0, res, res]] * (2 * b), dtype=torch.float32)
+    return out
+
+
+@torch.no_grad()
+def oracle_output(name, cfg, sd, variant):
+    """The oracle's result of case `name` (variant "half" or "fp32"): final latents (c1) or the
+    UNet's noise prediction [2B, 4, H, W] (c3, c4)."""
+    c = CASES[name]
+    ref = RefUNet(cfgdict(cfg), sd, dict(c["qc"]), variant=variant)
+    inp = inputs(name, cfg)
+    if name == "c1":
+        ts, a_t, a_p = ddim_tables(c["steps"])
+        ctx = torch.cat([inp["ne"], inp["pe"]])
+        return denoise(ref, inp["lat"], ctx, ts, a_t, a_p, c["guidance"])
+    add = ref.add_embeds(inp["text"], inp["time_ids"]) if name == "c4" else None
+    if add is None:
+        return ref.forward(inp["x"], c["t"], inp["ctx"])
+    return ref.forward(inp["x"], c["t"], inp["ctx"], add)

@@ -363,6 +363,18 @@ def ddim_step(eps_cfg_in, t_idx, latents, a_t, a_p, guidance):
     return ap ** 0.5 * x0 + direction
 
 
+def ddim_tables(num_inference_steps, num_train=1000, beta_start=0.00085, beta_end=0.012, steps_offset=1):
+    """DDIMScheduler.set_timesteps ("leading", scaled_linear betas, set_alpha_to_one False):
+    (timesteps int64 [S], alpha_t f32 [S], alpha_prev f32 [S])."""
+    betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_train, dtype=torch.float32) ** 2
+    ac = torch.cumprod(1.0 - betas, dim=0)
+    ratio = num_train // num_inference_steps
+    ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.int64) + steps_offset
+    a_t = torch.stack([ac[int(t)] for t in ts])
+    a_p = torch.stack([ac[int(t) - ratio] if int(t) - ratio >= 0 else ac[0] for t in ts])
+    return torch.from_numpy(ts), a_t, a_p
+
+
 @torch.no_grad()
 def denoise(unet, latents, ctx, timesteps, a_t, a_p, guidance=7.5, steps=None):
     """The reference's pipeline loop on CPU: returns latents after `steps` steps."""
