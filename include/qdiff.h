@@ -231,6 +231,11 @@ int qd_nhwc_to_nchw(const void* x, int n, int c, int hw, int c_pad, void* y, voi
  * softmax/accumulation). */
 int qd_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                  int ldo, int b, int heads, int sq, int skv, int d, float scale, void* stream);
+/* head_dim d: a multiple of 8 up to 512 (d > 256: the VAE mid block's single 512-wide head).
+ * Causal self-attention (transformers CLIPAttention with the causal mask; sq == skv == s):
+ * query i attends keys 0..i. */
+int qd_attention_causal(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                        int ldo, int b, int heads, int s, int d, float scale, void* stream);
 
 /* ---------------- time embedding / scheduler ---------------------------------------- */
 /* diffusers Timesteps(dim, flip_sin_to_cos, downscale_freq_shift) on timesteps[step_idx[0]]
@@ -266,6 +271,31 @@ int qd_cfg_euler_discrete_step(void* latents, const void* unet_out, int b, int64
  * next_in != NULL (EulerDiscrete init_noise_sigma scaling + the first scale_model_input). */
 int qd_scale_latents(void* latents, int64_t n, float mul, float div, void* next_in, int c, int c_pad,
                      void* stream);
+
+/* ---------------- text encoder (CLIP) / VAE decoder ---------------------------------- */
+/* The models around the denoising loop: the reference's pipelines call them through diffusers
+ * (models/StableDiffusion1_x.py:19-33 component discovery; base.py:848 pipeline call, whose
+ * output_type decides whether the VAE decodes; quantTextEncoder / quantVAE (decoder only,
+ * StableDiffusion1_x.py:58-67) swap their layers like the UNet's).
+ * out[r, :] = half(tok[ids[r], :] + pos[r % seq, :]) - CLIPTextEmbeddings (ids int64 device,
+ * range-checked by the caller; c % 8 == 0). */
+int qd_embed_tokens(const int64_t* ids, int64_t rows, int seq, const void* tok, int64_t vocab, const void* pos,
+                    int c, void* out, void* stream);
+/* CLIP MLP activation, elementwise: kind 0 quick_gelu = x * sigmoid(1.702 x) (three fp16
+ * roundings, as the Half ops), kind 1 exact-erf gelu. */
+int qd_clip_act(const void* x, void* y, int64_t count, int kind, void* stream);
+/* y[i, :] = x[idx[i], :] (rows of c fp16, row stride ldx; idx int64 device) - pooled EOS rows. */
+int qd_gather_rows(const void* x, int64_t ldx, int64_t rows_x, const int64_t* idx, int n, int c, void* y,
+                   void* stream);
+/* VAE decode input: y = half(x / scale) [then half(y + shift) if has_shift], NHWC latents with c
+ * of cin_pad channels -> NHWC with cout_pad channels (the rest zero). */
+int qd_vae_prescale(const void* x, int64_t pix, int cin_pad, int c, float scale, float shift, int has_shift,
+                    int cout_pad, void* y, void* stream);
+/* VaeImageProcessor.postprocess of the decoder output y (NHWC, c of c_pad channels):
+ * v = clamp(half(half(y / 2) + 0.5), 0, 1) -> out_nchw fp16 [n, c, h, w] and/or
+ * out_u8 [n, h, w, c] = rint(v * 255) (either may be NULL, not both). */
+int qd_vae_postprocess(const void* y, int n, int64_t hw, int c_pad, int c, void* out_nchw, void* out_u8,
+                       void* stream);
 
 /* ---------------- calibration (SmoothQuant) ------------------------------------------ */
 /* Mean_Max_Activation_Hook (utils/calib_data.py:105-124): per-channel max |x| of x[rows, C]

@@ -44,6 +44,12 @@ SIGNATURES = {
     "qd_nchw_to_nhwc": [P, I, I, I, I, P, P],
     "qd_nhwc_to_nchw": [P, I, I, I, I, P, P],
     "qd_attention": [P, I, P, I, P, I, P, I, I, I, I, I, I, F, P],
+    "qd_attention_causal": [P, I, P, I, P, I, P, I, I, I, I, I, F, P],
+    "qd_embed_tokens": [P, I64, I, P, I64, P, I, P, P],
+    "qd_clip_act": [P, P, I64, I, P],
+    "qd_gather_rows": [P, I64, I64, P, I, I, P, P],
+    "qd_vae_prescale": [P, I64, I, I, F, F, I, I, P, P],
+    "qd_vae_postprocess": [P, I, I64, I, I, P, P, P],
     "qd_timestep_embedding": [P, P, I, I, I, F, P, P],
     "qd_cfg_ddim_step": [P, P, I, I64, F, P, P, P, P, I, I, P],
     "qd_cfg_pndm_step": [P, P, I, I64, F, P, P, P, P, P, P, I, I, P],

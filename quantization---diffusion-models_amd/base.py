@@ -7,8 +7,10 @@ Divergences from the reference, all deliberate and documented in DESIGN.md:
 * generate() honours height / width / num_inference_steps / guidance_scale (the reference
   passes only prompt, 50 steps, generator, latents, output_type: base.py:848).  The defaults
   equal the reference's effective values, so default calls match;
-* there is no CLIP text encoder or VAE (SURVEY.md §8f "next"): prompts map to deterministic
-  synthetic embeddings unless prompt_embeds are given, and generate() returns latents;
+* prompts are encoded by the pipeline's CLIP text encoder(s) and latents decoded by its VAE on
+  device (clip.py, vae.py); pipelines without them map prompts to synthetic embeddings and
+  return latents only; SD3 runs without T5 (zero T5 features, as diffusers does without
+  text_encoder_3);
 * from_pretrained() never contacts the hub; the hard-coded access token default of
   base.py:188 is not reproduced.
 """
@@ -117,19 +119,43 @@ class BaseAWQForDiffusion(nn.Module):
         self._loops = {}
 
     # ---------------------------------------------------------------- generate
+    def _has_text_encoder(self):
+        return "text_encoder" in self.pipeline.component_names()
+
     def _text_context(self, prompt, negative_prompt, prompt_embeds, negative_prompt_embeds):
+        """StableDiffusionPipeline.encode_prompt: [negative; positive] CLIP last hidden states
+        (the negative prompt defaults to ""); pipelines without a text encoder map prompt strings
+        to deterministic synthetic embeddings."""
         dim = self.pipeline.unet.config.cross_attention_dim
         dev = self.pipeline.device
+        pipe = self.pipeline
+        te = self._has_text_encoder()
         if prompt_embeds is None:
             prompts = [prompt] if isinstance(prompt, str) else list(prompt)
-            prompt_embeds = synthetic_text_embeddings(prompts, dim=dim, device=dev)
+            prompt_embeds = (pipe.text_encoder.encode(pipe.tokenizer(prompts))[0] if te else
+                             synthetic_text_embeddings(prompts, dim=dim, device=dev))
         if negative_prompt_embeds is None:
             b = prompt_embeds.shape[0]
             neg = negative_prompt if negative_prompt is not None else ""
             negs = [neg] * b if isinstance(neg, str) else list(neg)
-            negative_prompt_embeds = synthetic_text_embeddings(negs, seq_len=prompt_embeds.shape[1], dim=dim,
-                                                               device=dev)
+            negative_prompt_embeds = (pipe.text_encoder.encode(pipe.tokenizer(negs, max_length=prompt_embeds.shape[1]))[0]
+                                      if te else synthetic_text_embeddings(negs, seq_len=prompt_embeds.shape[1], dim=dim,
+                                                                           device=dev))
         return torch.cat([negative_prompt_embeds.to(dev), prompt_embeds.to(dev)]).to(torch.float16).contiguous()
+
+    def _decode(self, latents, output_type):
+        """output_type "latent": the latents; otherwise VAE decode + VaeImageProcessor.postprocess
+        (None -> "np", as diffusers treats it; "pt" / "pil" as diffusers)."""
+        if output_type == "latent":
+            return latents
+        if output_type not in (None, "np", "pt", "pil"):
+            raise ValueError(f"output_type {output_type!r}: one of 'latent', 'np', 'pt', 'pil' (None = 'np')")
+        if "vae" not in self.pipeline.component_names():
+            raise RuntimeError("this pipeline has no VAE (vae/ directory): use output_type='latent'")
+        from . import kernels as K
+        c = latents.shape[1]
+        return self.pipeline.vae.decode_images(K.nchw_to_nhwc(latents.contiguous(), (c + 7) // 8 * 8),
+                                               output_type or "np")
 
     def get_loop(self, batch, height, width, steps, guidance, use_graph=True):
         key = (batch, height, width, steps, float(guidance), use_graph)
@@ -142,11 +168,11 @@ class BaseAWQForDiffusion(nn.Module):
     def generate(self, prompt=None, height=512, width=512, num_inference_steps=50, guidance_scale=7.5,
                  negative_prompt=None, num_images_per_prompt=1, generator=None, device="cpu", lat=None,
                  output_type=None, prompt_embeds=None, negative_prompt_embeds=None, use_graph=True, **kwargs):
-        """base.py:828-850 -> the device denoising loop; returns latents [B, 4, h, w] fp16."""
+        """base.py:828-850 -> the device denoising loop, then the VAE decode (output_type None:
+        float32 numpy images [B, H, W, 3] as the reference's pipeline call returns; "latent":
+        the latents [B, 4, h, w] fp16)."""
         if self.pipeline is None:
             raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
-        if output_type not in (None, "latent"):
-            raise NotImplementedError("VAE decoding is not part of this build (SURVEY.md §8f); use output_type='latent'")
         ctx = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds)
         if num_images_per_prompt > 1:
             b0 = ctx.shape[0] // 2
@@ -158,7 +184,7 @@ class BaseAWQForDiffusion(nn.Module):
         if lat is None:
             lat = torch.randn(shape, generator=generator, dtype=torch.float32).to(torch.float16)
         loop = self.get_loop(b, height, width, num_inference_steps, guidance_scale, use_graph)
-        return loop.run(lat.to(self.pipeline.device), ctx)
+        return self._decode(loop.run(lat.to(self.pipeline.device), ctx), output_type)
 
     # ---------------------------------------------------------------- save / load
     def save_quantized(self, save_dir, safetensors=True, shard_size="5GB", export_compatible=False, quant_act=False,

@@ -54,7 +54,7 @@ template <int DP, int DV, int NB, int NW, int NQ>
 __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                               int ldk, const f16* __restrict__ v, int ldv,
                                               f16* __restrict__ o, int ldo, int heads, int sq, int skv,
-                                              int d, float scale_log2) {
+                                              int d, float scale_log2, int causal) {
   constexpr int KCH = DP / 8;                  // 16-B chunks per K row (QK^T depth DP)
   constexpr int KCHP = (KCH + 7) / 8 * 8;      // padded so the XOR swizzle stays in the row
   constexpr int VST = v_stride(DV);
@@ -195,6 +195,19 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
           for (int r = 0; r < 4; ++r)
             if (kv0 + j * 16 + fq * 4 + r >= skv) sacc[g][j][r] = -INFINITY;
     }
+    // causal (CLIP text encoder): key kv is visible to query q iff kv <= q; key 0 is in the
+    // first tile, so every query's running max is finite after it
+    if (causal && kv0 + KV_T - 1 > q0) {
+#pragma unroll
+      for (int g = 0; g < NQ; ++g) {
+        const int qrow = q0 + (wid * NQ + g) * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kv0 + j * 16 + fq * 4 + r > qrow) sacc[g][j][r] = -INFINITY;
+      }
+    }
     // ---- online softmax per query group (log2 domain) ----
     f16x8 pf[NQ][2];
 #pragma unroll
@@ -299,9 +312,16 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
 
 template <int DP, int DV>
 static void launch(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
-                   int ldo, int b, int heads, int sq, int skv, int d, float scale, hipStream_t st) {
+                   int ldo, int b, int heads, int sq, int skv, int d, float scale, int causal, hipStream_t st) {
   constexpr int NB = DP <= 96 ? 2 : 1;
   const float sl2 = scale * 1.4426950408889634f;
+  if constexpr (DP > 256) {
+    // wide heads (the VAE mid-block's single 512-channel head): 4 waves x 16 queries, one
+    // 64-key K tile (64 KB) + V tile (66 KB) in LDS, O^T accumulators mostly in AGPRs
+    k_attn<DP, DV, 1, 4, 1><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+    return;
+  } else {
   // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2); unset: heuristic
   static const int forced = [] {
     const char* e = getenv("QD_ATTN_CFG");
@@ -309,22 +329,22 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
   }();
   if (forced == 1) {
     k_attn<DP, DV, NB, 8, 2><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
     return;
   }
   if (forced == 2) {
     k_attn<DP, DV, NB, 8, 1><<<((sq + 127) / 128) * b * heads, 512, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
     return;
   }
   if (forced == 5) {
     k_attn<DP, DV, NB, 4, 2><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
     return;
   }
   if (forced == 3) {
     k_attn<DP, DV, NB, 4, 1><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
     return;
   }
   // long sequences: 8 waves x 2 query groups (256 queries) share each staged K/V tile while the
@@ -335,46 +355,60 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
   if (sq >= 512 && DV > 48 && DV <= 80) {
     const int grid = ((sq + 127) / 128) * b * heads;
     k_attn<DP, DV, NB, 4, 2><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
   } else if (sq >= 512 && DP <= 96 && (long)((sq + 255) / 256) * b * heads >= 512) {
     const int grid = ((sq + 255) / 256) * b * heads;
     k_attn<DP, DV, NB, 8, 2><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
   } else if (sq >= 512) {
     const int grid = ((sq + 127) / 128) * b * heads;
     k_attn<DP, DV, NB, 8, 1><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
   } else {
     const int grid = ((sq + 63) / 64) * b * heads;
     k_attn<DP, DV, NB, 4, 1><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
   }
+  }
+}
+
+static int attention_impl(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                          int ldo, int b, int heads, int sq, int skv, int d, float scale, int causal, void* stream) {
+  QD_REQUIRE(q && k && v && o, "null pointer");
+  QD_REQUIRE(d % 8 == 0 && d > 0 && d <= 512, "head_dim must be a multiple of 8 in (0, 512]");
+  QD_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
+             "leading dims must be multiples of 8 (q, k, v) and 4 (o)");
+  QD_REQUIRE(skv > 0, "empty key sequence");
+  QD_REQUIRE(!causal || skv == sq, "causal attention needs sq == skv");
+  if ((long)b * heads * sq == 0) return 0;
+  hipStream_t st = S(stream);
+  const int c = causal;
+  // DP: QK^T depth (multiple of 32 >= d); DV: PV rows, a multiple of 16 > d (row d = denominator)
+  if (d <= 32) launch<32, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 40) launch<64, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 56) launch<64, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 64) launch<64, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 72) launch<96, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 88) launch<96, 96>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 96) launch<96, 112>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 120) launch<128, 128>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 128) launch<128, 144>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 152) launch<160, 160>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 160) launch<160, 176>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 248) launch<256, 256>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else if (d <= 256) launch<256, 272>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  else launch<512, 528>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
+  QD_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int qd_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
                             void* o, int ldo, int b, int heads, int sq, int skv, int d, float scale,
                             void* stream) {
-  QD_REQUIRE(q && k && v && o, "null pointer");
-  QD_REQUIRE(d % 8 == 0 && d > 0 && d <= 256, "head_dim must be a multiple of 8 in (0, 256]");
-  QD_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
-             "leading dims must be multiples of 8 (q, k, v) and 4 (o)");
-  QD_REQUIRE(skv > 0, "empty key sequence");
-  if ((long)b * heads * sq == 0) return 0;
-  hipStream_t st = S(stream);
-  // DP: QK^T depth (multiple of 32 >= d); DV: PV rows, a multiple of 16 > d (row d = denominator)
-  if (d <= 32) launch<32, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 40) launch<64, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 56) launch<64, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 64) launch<64, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 72) launch<96, 80>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 88) launch<96, 96>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 96) launch<96, 112>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 120) launch<128, 128>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 128) launch<128, 144>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 152) launch<160, 160>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 160) launch<160, 176>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else if (d <= 248) launch<256, 256>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  else launch<256, 272>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, st);
-  QD_CHECK_LAUNCH();
-  return 0;
+  return attention_impl(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, 0, stream);
+}
+
+extern "C" int qd_attention_causal(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                                   void* o, int ldo, int b, int heads, int s, int d, float scale, void* stream) {
+  return attention_impl(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, s, s, d, scale, 1, stream);
 }

@@ -675,6 +675,79 @@ def attention(q, k, v, heads, out=None, b=None):
     return out
 
 
+def attention_causal(q, k, v, heads, out=None):
+    """Causal self-attention (CLIP): q/k/v [B, S, C] (row strides may exceed C) -> o [B, S, C]."""
+    B, s, c = q.shape
+    d = c // heads
+    if out is None:
+        out = _empty((B, s, c), torch.float16, q.device)
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        if t.dtype != torch.float16 or not t.is_cuda or t.stride(2) != 1 or t.shape[1] != s:
+            raise ValueError(f"{nm} must be fp16 HIP [B, S, C] with unit last stride")
+    _lib.call("qd_attention_causal", _p(q), q.stride(1), _p(k), k.stride(1), _p(v), v.stride(1), _p(out),
+              out.stride(1), B, heads, s, d, float(d ** -0.5), _stream())
+    return out
+
+
+def embed_tokens(ids, tok, pos, out=None):
+    """ids int64 [B, S] (device) -> half(tok[ids] + pos[:S]) as [B * S, C]."""
+    if ids.dtype != torch.int64 or not ids.is_cuda or not ids.is_contiguous():
+        raise ValueError("ids must be a contiguous int64 HIP tensor")
+    _chk(tok, "token table")
+    _chk(pos, "position table")
+    b, s = ids.shape
+    if s > pos.shape[0]:
+        raise ValueError(f"sequence length {s} exceeds the {pos.shape[0]} position embeddings")
+    c = tok.shape[1]
+    o = out if out is not None else _empty((b * s, c), torch.float16, ids.device)
+    _lib.call("qd_embed_tokens", _p(ids), b * s, s, _p(tok), tok.shape[0], _p(pos), c, _p(o), _stream())
+    return o
+
+
+CLIP_ACT = {"quick_gelu": 0, "gelu": 1}
+
+
+def clip_act(x, kind, out=None):
+    _chk(x, "x")
+    if kind not in CLIP_ACT:
+        raise ValueError(f"unsupported CLIP activation {kind!r} (quick_gelu, gelu)")
+    o = out if out is not None else _empty(x.shape, x.dtype, x.device)
+    _lib.call("qd_clip_act", _p(x), _p(o), x.numel(), CLIP_ACT[kind], _stream())
+    return o
+
+
+def gather_rows(x2d, idx, out=None):
+    """x2d [R, C] (row stride may exceed C), idx int64 [n] device -> [n, C]."""
+    if x2d.dtype != torch.float16 or not x2d.is_cuda or x2d.stride(1) != 1:
+        raise ValueError("x must be 2-D fp16 HIP with unit column stride")
+    if idx.dtype != torch.int64 or not idx.is_cuda:
+        raise ValueError("idx must be an int64 HIP tensor")
+    n, c = idx.numel(), x2d.shape[1]
+    o = out if out is not None else _empty((n, c), torch.float16, x2d.device)
+    _lib.call("qd_gather_rows", _p(x2d), x2d.stride(0), x2d.shape[0], _p(idx.contiguous()), n, c, _p(o), _stream())
+    return o
+
+
+def vae_prescale(lat, c, scale, shift=None, cout_pad=8, out=None):
+    """NHWC latents [N, H, W, Cp] (c valid) -> NHWC [N, H, W, cout_pad] = half(x / scale) (+ shift)."""
+    _chk(lat, "latents")
+    n, h, w, cp = lat.shape
+    o = out if out is not None else _empty((n, h, w, cout_pad), torch.float16, lat.device)
+    _lib.call("qd_vae_prescale", _p(lat), n * h * w, cp, c, float(scale), float(shift or 0.0),
+              1 if shift is not None else 0, cout_pad, _p(o), _stream())
+    return o
+
+
+def vae_postprocess(y, c=3, want_nchw=True, want_u8=False):
+    """decoder output NHWC [N, H, W, Cp] -> (fp16 NCHW image in [0, 1] or None, uint8 NHWC or None)."""
+    _chk(y, "y")
+    n, h, w, cp = y.shape
+    a = _empty((n, c, h, w), torch.float16, y.device) if want_nchw else None
+    u = torch.empty((n, h, w, c), dtype=torch.uint8, device=y.device) if want_u8 else None
+    _lib.call("qd_vae_postprocess", _p(y), n, h * w, cp, c, _p(a), _p(u), _stream())
+    return a, u
+
+
 def timestep_embedding(timesteps_f32, step_idx, b, dim, flip_sin_to_cos=True, shift=0.0, out=None, per_row=False):
     """per_row: row r embeds timesteps_f32[r] (b values) instead of timesteps_f32[step_idx]."""
     o = out if out is not None else _empty((b, dim), torch.float16, timesteps_f32.device)

@@ -15,6 +15,7 @@ import torch
 
 from .base import QUANTISABLE_COMPONENTS, BaseAWQForDiffusion
 from .calib import synthetic_calibration_set
+from .clip import encode_sd3, encode_sdxl
 from .pipeline import EulerDiscreteDenoiseLoop, FlowMatchDenoiseLoop, synthetic_text_embeddings
 from .pipeline_io import load_config
 from .unet import BasicTransformerBlock
@@ -33,9 +34,7 @@ class _DiffusionAdapter(BaseAWQForDiffusion):
         self.set_quantizable_components()
 
     def set_quantizable_components(self):
-        for component, obj in self.pipeline.components.items():
-            if obj is None or not isinstance(obj, torch.nn.Module):
-                continue
+        for component in self.pipeline.component_names():   # aux components stay unbuilt until used
             for key in QUANTISABLE_COMPONENTS:
                 if key in component:
                     self.quantizable_components[key].append(component)
@@ -151,18 +150,28 @@ class StableDiffusionXL(_DiffusionAdapter):
         cfg = self.pipeline.unet.config
         dev = self.pipeline.device
         pooled_dim = cfg.projection_class_embeddings_input_dim - 6 * cfg.addition_time_embed_dim
-        ctx = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds)
-        b = ctx.shape[0] // 2
-        if pooled_prompt_embeds is None:
-            prompts = [prompt] * b if isinstance(prompt, str) else list(prompt or [f"prompt{i}" for i in range(b)])
-            pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in prompts], seq_len=1,
-                                                             dim=pooled_dim, device=dev)[:, 0]
-        if negative_pooled_prompt_embeds is None:
-            neg = negative_prompt if negative_prompt is not None else ""
-            negs = [neg] * b if isinstance(neg, str) else list(neg)
-            negative_pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in negs], seq_len=1,
-                                                                      dim=pooled_dim, device=dev)[:, 0]
-        text = torch.cat([negative_pooled_prompt_embeds.to(dev), pooled_prompt_embeds.to(dev)]).to(torch.float16)
+        if prompt_embeds is None and self._has_text_encoder():
+            ctx, text = encode_sdxl(self.pipeline, prompt, negative_prompt)
+            b = ctx.shape[0] // 2
+        else:
+            if prompt_embeds is not None and negative_prompt_embeds is None and negative_prompt is None:
+                # force_zeros_for_empty_prompt (the SDXL base config): zero negative conditioning
+                negative_prompt_embeds = torch.zeros_like(prompt_embeds)
+                if negative_pooled_prompt_embeds is None and pooled_prompt_embeds is not None:
+                    negative_pooled_prompt_embeds = torch.zeros_like(pooled_prompt_embeds)
+            ctx = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds)
+            b = ctx.shape[0] // 2
+            if pooled_prompt_embeds is None:
+                prompts = [prompt] * b if isinstance(prompt, str) else list(prompt or [f"prompt{i}" for i in range(b)])
+                pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in prompts], seq_len=1,
+                                                                 dim=pooled_dim, device=dev)[:, 0]
+            if negative_pooled_prompt_embeds is None:
+                neg = negative_prompt if negative_prompt is not None else ""
+                negs = [neg] * b if isinstance(neg, str) else list(neg)
+                negative_pooled_prompt_embeds = synthetic_text_embeddings([f"{p}\x00pooled" for p in negs], seq_len=1,
+                                                                          dim=pooled_dim, device=dev)[:, 0]
+            text = torch.cat([negative_pooled_prompt_embeds.to(dev), pooled_prompt_embeds.to(dev)])
+        text = text.to(torch.float16)
         # StableDiffusionXLPipeline._get_add_time_ids: original_size + crops_coords_top_left + target_size
         ids = list(original_size or (height, width)) + list(crops_coords_top_left) + list(target_size or (height, width))
         time_ids = torch.tensor([ids] * (2 * b), dtype=torch.float32)
@@ -183,11 +192,9 @@ class StableDiffusionXL(_DiffusionAdapter):
                  negative_pooled_prompt_embeds=None, original_size=None, crops_coords_top_left=(0, 0),
                  target_size=None, use_graph=True, **kwargs):
         """base.py:828-850 for StableDiffusionXLPipeline (its default guidance 5.0; the reference
-        passes 50 steps) -> the device Euler-discrete loop; returns latents [B, 4, h, w] fp16."""
+        passes 50 steps) -> the device Euler-discrete loop and the VAE decode (see base generate)."""
         if self.pipeline is None:
             raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
-        if output_type not in (None, "latent"):
-            raise NotImplementedError("VAE decoding is not part of this build (SURVEY.md §8f); use output_type='latent'")
         ctx, text, time_ids = self._xl_conditioning(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
                                                     pooled_prompt_embeds, negative_pooled_prompt_embeds, height, width,
                                                     original_size, crops_coords_top_left, target_size)
@@ -200,7 +207,7 @@ class StableDiffusionXL(_DiffusionAdapter):
         if lat is None:
             lat = torch.randn((b, cin, height // 8, width // 8), generator=generator, dtype=torch.float32).to(torch.float16)
         loop = self.get_loop(b, height, width, num_inference_steps, guidance_scale, use_graph)
-        return loop.run(lat.to(self.pipeline.device), ctx, text, time_ids)
+        return self._decode(loop.run(lat.to(self.pipeline.device), ctx, text, time_ids), output_type)
 
 
 class StableDiffusion3_5(_DiffusionAdapter):
@@ -232,10 +239,13 @@ class StableDiffusion3_5(_DiffusionAdapter):
 
     def _text_context(self, prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
                       pooled_prompt_embeds=None, negative_pooled_prompt_embeds=None, seq_len=333):
-        """[neg; pos] T5+CLIP sequence embeddings [2B, Sc, joint_attention_dim] and pooled CLIP
-        embeddings [2B, pooled_projection_dim] (synthetic stand-ins for the three text encoders)."""
+        """[neg; pos] sequence embeddings [2B, Sc, joint_attention_dim] and pooled CLIP embeddings
+        [2B, pooled_projection_dim]: the two CLIP encoders (zero T5 features) when the pipeline has
+        them (clip.encode_sd3), else deterministic synthetic stand-ins."""
         cfg = self.pipeline.transformer.config
         dev = self.pipeline.device
+        if prompt_embeds is None and self._has_text_encoder():
+            return encode_sd3(self.pipeline, prompt, negative_prompt, joint_dim=cfg.joint_attention_dim)
         if prompt_embeds is None:
             prompts = [prompt] if isinstance(prompt, str) else list(prompt)
             prompt_embeds = synthetic_text_embeddings(prompts, seq_len=seq_len, dim=cfg.joint_attention_dim,
@@ -273,11 +283,9 @@ class StableDiffusion3_5(_DiffusionAdapter):
                  output_type=None, prompt_embeds=None, negative_prompt_embeds=None, pooled_prompt_embeds=None,
                  negative_pooled_prompt_embeds=None, use_graph=True, **kwargs):
         """base.py:828-850 for StableDiffusion3Pipeline (its default guidance 7.0; the reference
-        passes 50 steps) -> the device flow-match loop; returns latents [B, 16, h, w] fp16."""
+        passes 50 steps) -> the device flow-match loop and the VAE decode (see base generate)."""
         if self.pipeline is None:
             raise RuntimeError("The diffusion pipeline is not loaded. Please use `from_pretrained` or `from_quantized` first.")
-        if output_type not in (None, "latent"):
-            raise NotImplementedError("VAE decoding is not part of this build (SURVEY.md §8f); use output_type='latent'")
         ctx, pooled = self._text_context(prompt, negative_prompt, prompt_embeds, negative_prompt_embeds,
                                          pooled_prompt_embeds, negative_pooled_prompt_embeds)
         if num_images_per_prompt > 1:
@@ -291,7 +299,7 @@ class StableDiffusion3_5(_DiffusionAdapter):
         if lat is None:
             lat = torch.randn(shape, generator=generator, dtype=torch.float32).to(torch.float16)
         loop = self.get_loop(b, height, width, num_inference_steps, guidance_scale, use_graph, ctx.shape[1])
-        return loop.run(lat.to(self.pipeline.device), ctx, pooled)
+        return self._decode(loop.run(lat.to(self.pipeline.device), ctx, pooled), output_type)
 
     @torch.no_grad()
     def run_sq_calibration(self, *a, **k):

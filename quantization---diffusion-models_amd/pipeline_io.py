@@ -33,15 +33,29 @@ SYNTHETIC = {
 MMDIT_PIPELINES = ("StableDiffusion3Pipeline",)
 
 
+AUX_COMPONENTS = ("text_encoder", "text_encoder_2", "tokenizer", "tokenizer_2", "vae")
+
+
 class QDiffPipeline:
+    """Denoiser + scheduler config + the aux components (text encoder(s), tokenizers, VAE).
+    `lazy` maps aux component names to zero-argument factories: synthetic checkpoints and local
+    directories build their text encoders / VAE only when a prompt string must be encoded or
+    latents decoded (the denoising loop never needs them)."""
+
     def __init__(self, unet=None, class_name="StableDiffusionPipeline", scheduler_config=None, text_encoder=None,
-                 vae=None, config=None, transformer=None):
+                 vae=None, config=None, transformer=None, text_encoder_2=None, tokenizer=None, tokenizer_2=None,
+                 lazy=None):
         if (unet is None) == (transformer is None):
             raise ValueError("a pipeline holds exactly one denoiser: a unet or a transformer")
         self.unet = unet
         self.transformer = transformer
-        self.text_encoder = text_encoder
-        self.vae = vae
+        self._lazy = dict(lazy or {})
+        given = dict(text_encoder=text_encoder, text_encoder_2=text_encoder_2, tokenizer=tokenizer,
+                     tokenizer_2=tokenizer_2, vae=vae)
+        for name, obj in given.items():
+            if obj is not None or name not in self._lazy:
+                self._lazy.pop(name, None)
+                setattr(self, name, obj)
         if scheduler_config is None:
             scheduler_config = (FlowMatchConfig() if transformer is not None else
                                 EulerDiscreteConfig() if class_name == "StableDiffusionXLPipeline" else DDIMConfig())
@@ -49,6 +63,14 @@ class QDiffPipeline:
         self.class_name = class_name
         self.config = config or {"_class_name": class_name}
         self.device = next(self.denoiser.parameters()).device
+
+    def __getattr__(self, name):
+        lazy = self.__dict__.get("_lazy")
+        if lazy is not None and name in lazy:
+            obj = lazy.pop(name)(self)
+            setattr(self, name, obj)
+            return obj
+        raise AttributeError(name)
 
     @property
     def denoiser(self):
@@ -58,14 +80,32 @@ class QDiffPipeline:
     def denoiser_name(self):
         return "unet" if self.unet is not None else "transformer"
 
+    def component_names(self):
+        """Names of the model components present (built or buildable), denoiser first."""
+        names = [self.denoiser_name]
+        for n in ("text_encoder", "text_encoder_2", "vae"):
+            if n in self._lazy or self.__dict__.get(n) is not None:
+                names.append(n)
+        return names
+
     @property
     def components(self):
-        comps = {"text_encoder": self.text_encoder, "vae": self.vae, "scheduler": self.scheduler_config}
-        comps[self.denoiser_name] = self.denoiser
+        """diffusers' DiffusionPipeline.components: every model slot (None when absent; lazy ones
+        are built by this access) and the scheduler."""
+        comps = {self.denoiser_name: self.denoiser, "text_encoder": None, "vae": None}
+        for n in self.component_names()[1:]:
+            comps[n] = getattr(self, n)
+        comps["scheduler"] = self.scheduler_config
         return comps
+
+    def built_aux(self):
+        return {n: self.__dict__[n] for n in ("text_encoder", "text_encoder_2", "vae")
+                if self.__dict__.get(n) is not None}
 
     def to(self, device):
         self.denoiser.to(device)
+        for m in self.built_aux().values():
+            m.to(device)
         self.device = torch.device(device)
         return self
 
@@ -81,6 +121,20 @@ class QDiffPipeline:
             index = {"transformer": ["diffusers", "SD3Transformer2DModel"],
                      "scheduler": ["diffusers", sched["_class_name"]]}
             cls = "SD3Transformer2DModel"
+        for aux, m in self.built_aux().items():   # text encoders / VAE that were built (or loaded)
+            d = os.path.join(save_dir, aux)
+            os.makedirs(d, exist_ok=True)
+            if aux.startswith("text_encoder"):
+                arch = "CLIPTextModelWithProjection" if m.config.projection_dim else "CLIPTextModel"
+                c, fname, index[aux] = dict(m.config.to_transformers(), architectures=[arch]), "model.safetensors", \
+                    ["transformers", arch]
+            else:
+                c, fname, index[aux] = m.config.to_diffusers(), "diffusion_pytorch_model.safetensors", \
+                    ["diffusers", "AutoencoderKL"]
+            with open(os.path.join(d, "config.json"), "w") as f:
+                json.dump(c, f, indent=2)
+            save_file({k: v.detach().to("cpu").contiguous() for k, v in m.state_dict().items()},
+                      os.path.join(d, fname))
         with open(os.path.join(save_dir, "model_index.json"), "w") as f:
             json.dump({"_class_name": self.class_name, **index}, f, indent=2)
         os.makedirs(os.path.join(save_dir, "scheduler"), exist_ok=True)
@@ -107,9 +161,11 @@ def load_config(model_path):
         return json.load(f)
 
 
-def _load_weights(module, path, dtype):
+def _load_weights(module, path, dtype, rename=None):
     from safetensors.torch import load_file
     sd = load_file(path)
+    if rename is not None:
+        sd = {rename(k): v for k, v in sd.items()}
     missing, unexpected = module.load_state_dict({k: v.to(dtype) for k, v in sd.items()}, strict=False)
     if missing:
         raise KeyError(f"weights missing keys (first 5): {missing[:5]}")
@@ -133,6 +189,116 @@ def load_scheduler_config(model_path, override=None):
         return config_from_diffusers(json.load(f))
 
 
+# ------------------------------------------------------------------ text encoders / VAE
+def _te_factory(cfg, seed=None, path=None):
+    def build(pipe):
+        from .clip import CLIPTextModel
+        m = CLIPTextModel(cfg).half()
+        if path is None:
+            m.init_synthetic(seed)
+        else:
+            _load_weights(m, _first(path, ("model.safetensors", "model.fp16.safetensors")), torch.float16,
+                          rename=_clip_keys)
+        return m.to(pipe.device).eval()
+    return build
+
+
+def _vae_factory(cfg, seed=None, path=None):
+    def build(pipe):
+        from .vae import AutoencoderKL
+        m = AutoencoderKL(cfg).half()
+        if path is None:
+            m.init_synthetic(seed)
+        else:
+            _load_weights(m, _first(path, ("diffusion_pytorch_model.safetensors",
+                                           "diffusion_pytorch_model.fp16.safetensors")), torch.float16,
+                          rename=_vae_keys)
+        return m.to(pipe.device).eval()
+    return build
+
+
+def _first(d, names):
+    for n in names:
+        if os.path.exists(os.path.join(d, n)):
+            return os.path.join(d, n)
+    raise FileNotFoundError(f"no weights file ({', '.join(names)}) in {d}")
+
+
+def _clip_keys(k):
+    """transformers >= 5 may save CLIPTextModel without the text_model. prefix."""
+    if k.startswith(("embeddings.", "encoder.", "final_layer_norm.")):
+        return "text_model." + k
+    return k
+
+
+_VAE_LEGACY = {".query.": ".to_q.", ".key.": ".to_k.", ".value.": ".to_v.", ".proj_attn.": ".to_out.0."}
+
+
+def _vae_keys(k):
+    """diffusers' legacy VAE attention names (query / key / value / proj_attn)."""
+    for a, b in _VAE_LEGACY.items():
+        k = k.replace(a, b)
+    return k
+
+
+def _synthetic_aux(cls, mcfg, tiny, seed):
+    """{component: factory(pipeline)} of a synthetic checkpoint's text encoder(s), tokenizers and
+    VAE: the real architectures (CLIP ViT-L/14, OpenCLIP bigG, AutoencoderKL) for full-size
+    models, small ones sized to the denoiser's conditioning widths for the tiny test models."""
+    from .clip import CLIP_G, CLIP_L, CLIP_L_PROJ, EOS, HashTokenizer, tiny_clip_config
+    from .vae import SD3_VAE, SD_VAE, SDXL_VAE, tiny_vae_config
+    tok1, tok2 = (lambda p: HashTokenizer(pad_id=EOS)), (lambda p: HashTokenizer(pad_id=0))
+    if cls == "StableDiffusionPipeline":
+        te = tiny_clip_config(hidden=mcfg.cross_attention_dim) if tiny else CLIP_L
+        return {"text_encoder": _te_factory(te, seed + 1), "tokenizer": tok1,
+                "vae": _vae_factory(tiny_vae_config() if tiny else SD_VAE, seed + 3)}
+    if cls == "StableDiffusionXLPipeline":
+        if tiny:
+            cross = mcfg.cross_attention_dim
+            pooled = mcfg.projection_class_embeddings_input_dim - 6 * mcfg.addition_time_embed_dim
+            te1 = tiny_clip_config(hidden=cross // 2)
+            te2 = tiny_clip_config(hidden=cross - cross // 2, projection_dim=pooled, act="gelu")
+        else:
+            te1, te2 = CLIP_L, CLIP_G
+        return {"text_encoder": _te_factory(te1, seed + 1), "text_encoder_2": _te_factory(te2, seed + 2),
+                "tokenizer": tok1, "tokenizer_2": tok2,
+                "vae": _vae_factory(tiny_vae_config() if tiny else SDXL_VAE, seed + 3)}
+    if tiny:
+        pd = mcfg.pooled_projection_dim
+        te1 = tiny_clip_config(hidden=pd // 2, projection_dim=pd // 2)
+        te2 = tiny_clip_config(hidden=pd - pd // 2, projection_dim=pd - pd // 2, act="gelu")
+    else:
+        te1, te2 = CLIP_L_PROJ, CLIP_G
+    return {"text_encoder": _te_factory(te1, seed + 1), "text_encoder_2": _te_factory(te2, seed + 2),
+            "tokenizer": tok1, "tokenizer_2": tok2,
+            "vae": _vae_factory(tiny_vae_config(16) if tiny else SD3_VAE, seed + 3)}
+
+
+def _local_aux(model_path):
+    """{component: factory(pipeline)} for the text encoder / tokenizer / VAE sub-directories a
+    local diffusers checkpoint holds (text_encoder_3 / T5 is not supported: SD3 prompts encode
+    with the two CLIP encoders and zero T5 features, as diffusers does without it)."""
+    from .clip import EOS, CLIPTextConfig, load_tokenizer
+    from .vae import VAEConfig
+    out = {}
+    for name in ("text_encoder", "text_encoder_2"):
+        d = os.path.join(model_path, name)
+        if os.path.exists(os.path.join(d, "config.json")):
+            with open(os.path.join(d, "config.json")) as f:
+                c = json.load(f)
+            proj = any("WithProjection" in a for a in c.get("architectures", []))
+            out[name] = _te_factory(CLIPTextConfig.from_transformers(c, with_projection=proj), path=d)
+    for name, pad in (("tokenizer", EOS), ("tokenizer_2", 0)):
+        d = os.path.join(model_path, name)
+        if os.path.isdir(d):
+            out[name] = (lambda p, d=d, pad=pad: load_tokenizer(d, pad_id=pad))
+    d = os.path.join(model_path, "vae")
+    if os.path.exists(os.path.join(d, "config.json")):
+        with open(os.path.join(d, "config.json")) as f:
+            out["vae"] = _vae_factory(VAEConfig.from_diffusers(json.load(f)), path=d)
+    return out
+
+
 def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16, scheduler=None):
     cfg = load_config(model_path)
     cls = cfg["_class_name"]
@@ -150,6 +316,7 @@ def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16, schedu
         else:
             net = UNet2DConditionModel(mcfg).to(dtype)
             net.init_synthetic(seed)
+        lazy = _synthetic_aux(cls, mcfg, SYNTHETIC[model_path][1] is None or model_path.endswith("-tiny"), seed)
     else:
         sub = "transformer" if mmdit else "unet"
         with open(os.path.join(model_path, sub, "config.json")) as f:
@@ -159,8 +326,9 @@ def load_pipeline(model_path, device="cuda", seed=0, dtype=torch.float16, schedu
         else:
             net = UNet2DConditionModel(UNetConfig.from_diffusers(c)).to(dtype)
         _load_weights(net, os.path.join(model_path, sub, "diffusion_pytorch_model.safetensors"), dtype)
+        lazy = _local_aux(model_path)
     net.to(device)
     net.eval()
     if mmdit:
-        return QDiffPipeline(transformer=net, class_name=cls, config=cfg, scheduler_config=sched_cfg)
-    return QDiffPipeline(net, cls, config=cfg, scheduler_config=sched_cfg)
+        return QDiffPipeline(transformer=net, class_name=cls, config=cfg, scheduler_config=sched_cfg, lazy=lazy)
+    return QDiffPipeline(net, cls, config=cfg, scheduler_config=sched_cfg, lazy=lazy)

@@ -338,5 +338,5 @@ def test_awq_facade_save_load_roundtrip(tmp_path):
     x, enc, pooled = _inputs(cfg, 4)
     assert torch.equal(_one_eval(model, x, 501.0, enc, pooled), _one_eval(re, x, 501.0, enc, pooled))
     out = model.generate(prompt=["a red cube"], height=cfg.sample_size * 8, width=cfg.sample_size * 8,
-                         num_inference_steps=2)
+                         num_inference_steps=2, output_type="latent")
     assert out.shape == (1, 16, cfg.sample_size, cfg.sample_size) and torch.isfinite(out.float()).all()

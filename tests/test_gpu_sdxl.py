@@ -149,5 +149,5 @@ def test_sdxl_adapter_surface_and_prompt_generate():
     model.quantize(quant_config=dict(w_bit=4, a_bit=8, q_group_size=128, quantize_act=True), quantUnet=True)
     cfg = model.pipeline.unet.config
     out = model.generate(prompt=["a red cube", "a blue ball"], height=cfg.sample_size * 8, width=cfg.sample_size * 8,
-                         num_inference_steps=3)
+                         num_inference_steps=3, output_type="latent")
     assert out.shape == (2, 4, cfg.sample_size, cfg.sample_size) and torch.isfinite(out.float()).all()
