@@ -51,6 +51,7 @@ def parse():
                          "sd35 = SD3.5-Large W4A16 1024^2, 1 prompt per GPU (config C5)")
     ap.add_argument("--calib-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the text encoder + VAE end-to-end timing")
     ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
     if a.mode is None:
@@ -180,6 +181,44 @@ def _conv_choice(shape=(8, 64, 64, 320), kind="conv"):
     return None
 
 
+def end_to_end(model, lat_nchw, prompts, step_s, reps=3):
+    """Prompt -> image around the timed denoising loop (rank 0, same per-GPU batch): the CLIP
+    text encoder on the prompts + "" negatives (the pipeline's encode_prompt) and the VAE decode
+    of the loop's latents to uint8 images (output_type "pil" minus the PIL wrapping), each warmed
+    up, then the median of `reps` timed runs; images/s = B / (loop step + encode + decode)."""
+    import statistics
+    import torch
+    from qdiff import kernels as K
+    vae = model.pipeline.vae
+    lat = K.nchw_to_nhwc(lat_nchw.contiguous(), 8)
+
+    def enc():
+        return model._text_context(prompts, None, None, None)
+
+    def dec():
+        n, h, w, _ = lat.shape
+        for i in range(0, n, vae.samples_per_chunk(h, w)):
+            K.vae_postprocess(vae.decode_nhwc(lat[i:i + vae.samples_per_chunk(h, w)].contiguous()), 3,
+                              want_nchw=False, want_u8=True)
+
+    out = {}
+    for name, fn in (("text_encode", enc), ("vae_decode", dec)):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        out[name + "_ms"] = round(statistics.median(ts) * 1e3, 2)
+    tot = step_s + (out["text_encode_ms"] + out["vae_decode_ms"]) / 1e3
+    out["images_per_s"] = round(len(prompts) / tot, 4)
+    out["note"] = (f"{len(prompts)} prompts: CLIP ViT-L/14 (12 layers, 77 tokens, + negatives) and the SD VAE decoder "
+                   f"({lat.shape[1] * 8}^2 uint8 images), HIP path, synthetic weights; loop step {step_s * 1e3:.1f} ms")
+    return out
+
+
 def linear_families():
     """GEMM family the tuner chose for each linear shape of the loop, counted per operand:
     packed int4 / int8 codes dequantized in the register-tile staging (k_gemm) or the fp16
@@ -303,8 +342,8 @@ def main():
     loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.5, use_graph=True)
     # full CFG context for all ranks' prompts, created on rank 0 and broadcast each step
     full_ctx = torch.empty(2 * B * world, 77, 768, dtype=torch.float16, device=dev)
+    prompts = [f"a photograph of synthetic scene {i}" for i in range(B * world)]
     if rank == 0:
-        prompts = [f"a photograph of synthetic scene {i}" for i in range(B * world)]
         full_ctx.copy_(torch.cat([synthetic_text_embeddings([""] * (B * world), device=dev),
                                   synthetic_text_embeddings(prompts, device=dev)]))
     g = torch.Generator().manual_seed(42 + rank)
@@ -373,6 +412,9 @@ def main():
                                                "per 512^2 image (SURVEY 8d)"},
             "linear_kernel_choice": linear_families(),
         }
+        if not args.no_e2e:
+            log("end to end (text encoder + VAE decode) ...")
+            line["end_to_end"] = end_to_end(model, out[:B], prompts[:B], dt / args.steps)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
             line["cpu_baseline"] = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))

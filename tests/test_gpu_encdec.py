@@ -74,8 +74,13 @@ def test_embed_act_gather_postprocess_bit_exact():
     for kind, ref in (("quick_gelu", x * torch.sigmoid(1.702 * x)), ("gelu", F.gelu(x.float()).half())):
         got = K.clip_act(x.to(DEV), kind).cpu()
         ulp = torch.clamp(ref.float().abs(), min=2.0 ** -14) * 2.0 ** -10
+        # quick_gelu: a 1-ulp step of the fp16 sigmoid (subnormal where x << 0) moves x * s by |x| ulp(s)
+        sig = torch.sigmoid(1.702 * x).float()
+        ulp_s = torch.clamp(sig.abs(), min=2.0 ** -14) * 2.0 ** -10 if kind == "quick_gelu" else 0 * sig
         d = (got.float() - ref.float()).abs()
-        assert (d <= ulp + 1e-7).all() and (d == 0).float().mean() > 0.99, (kind, int((d > 0).sum()))
+        bad = d > ulp + x.float().abs() * ulp_s + 1e-7
+        assert not bad.any() and (d == 0).float().mean() > 0.99, \
+            (kind, int((d > 0).sum()), x[bad][:8].tolist(), got[bad][:8].tolist(), ref[bad][:8].tolist())
     rows = torch.randn(3 * 77, 64, generator=g).half()
     idx = torch.tensor([5, 77 + 76, 154], dtype=torch.int64)
     assert torch.equal(K.gather_rows(rows.to(DEV), idx.to(DEV)).cpu(), rows[idx])
