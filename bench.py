@@ -49,7 +49,11 @@ def parse():
     ap.add_argument("--model", default="sd15", choices=["sd15", "sdxl", "sd35"],
                     help="secondary lines: sdxl = SDXL W8A8 1024^2, 2 prompts per GPU (config C4); "
                          "sd35 = SD3.5-Large W4A16 1024^2, 1 prompt per GPU (config C5)")
-    ap.add_argument("--calib-steps", type=int, default=2)
+    # SmoothQuant calibration: the reference's defaults (quantizer_SQ.py:331-339: 96 samples in
+    # batches of 8, 50 denoising steps each = 600 UNet evaluations at CFG batch 16, eager, hooked)
+    ap.add_argument("--calib-steps", type=int, default=50)
+    ap.add_argument("--calib-samples", type=int, default=96)
+    ap.add_argument("--calib-batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the text encoder + VAE end-to-end timing")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -97,7 +101,7 @@ def build_model(args, dev):
         model = StableDiffusionXL.from_pretrained("synthetic:sdxl", device=dev, seed=0)
         if args.mode == "w8a8-sq":
             model.quantize(quant_config=dict(QCFG[args.mode]), quantType="sq", quantUnet=True,
-                           calibration=dict(n_samples=args.batch, batch_size=args.batch,
+                           calibration=dict(n_samples=args.calib_samples, batch_size=args.calib_batch,
                                             num_inference_steps=args.calib_steps, height=args.res, width=args.res))
         elif args.mode != "fp16":
             model.quantize(quant_config=dict(QCFG[args.mode]), quantUnet=True)
@@ -115,7 +119,7 @@ def build_model(args, dev):
         i8 = args.mode.endswith("-int8")
         if args.mode.startswith("w8a8-sq"):
             model.quantize(quant_config=qc, quantType="sq", quantUnet=True, int8_mfma=i8,
-                           calibration=dict(n_samples=args.batch, batch_size=args.batch,
+                           calibration=dict(n_samples=args.calib_samples, batch_size=args.calib_batch,
                                             num_inference_steps=args.calib_steps))
         else:
             model.quantize(quant_config=qc, quantUnet=True, int8_mfma=i8)

@@ -51,7 +51,12 @@ __global__ void k_clip_act(const f16* __restrict__ x, f16* __restrict__ y, long 
   if (e >= count) return;
   const float v = (float)x[e];
   if (kind == 0) {
-    const float t = (float)(f16)(1.702f * v);
+    // the f32 product must round to f32 before the f16 conversion (the CPU's two roundings):
+    // without the barrier the backend folds mul + cvt into one mixed-precision v_fma_mix with a
+    // single rounding, which differs on f32 ties (1 fp16 ulp of t, ~0.4 % of the sigmoid)
+    float p = 1.702f * v;
+    asm volatile("" : "+v"(p));
+    const float t = (float)(f16)p;
     // sigmoid in f64, rounded to f32 then f16: the correctly rounded value the CPU's f32
     // 1 / (1 + exp(-t)) lands on except within an ulp of an fp16 rounding boundary
     const float s = (float)(f16)(float)(1.0 / (1.0 + exp(-(double)t)));
