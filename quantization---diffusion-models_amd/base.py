@@ -87,10 +87,13 @@ class BaseAWQForDiffusion(nn.Module):
                  quantText=True, quantVisionProjection=False, quantTextProjection=False, quantUnet=False,
                  quantTextEncoder=False, quantVAE=False, quantTransformer=False, diffusion_model=True,
                  codeBookQuantInd=False, debugPlot=False, debugAttentionMap=False, debugSavePath="",
-                 calibration=None, int8_mfma=False, **kwargs):
+                 calibration=None, int8_mfma=False, awq_search=False, **kwargs):
         """base.py:215-528.  quantType 'awq' = RTN swap; 'sq' = SmoothQuant fold + swap.
         int8_mfma=True (this build, w_bit 8): the int8-MFMA W8A8 mode instead of the reference's
-        fake-quant arithmetic (re-granularized, tolerance-based parity)."""
+        fake-quant arithmetic (re-granularized, tolerance-based parity).
+        awq_search=True (quantType 'awq'): the AWQ activation-aware scale search and weight-clip
+        search on the UNet's transformer blocks before the RTN swap (awq_search.py; calibration=
+        as run_sq_calibration's keywords)."""
         if quant_act and quant_config.get("version", "fake_act").lower() != "fake_act":
             print("With activation quantization set to True, you can only use the fake quant kernel fake_act! "
                   "Changing to that....")
@@ -108,7 +111,7 @@ class BaseAWQForDiffusion(nn.Module):
                 qc.act_quant_conv_type, qc.act_quant_conv_group_size, qc.w_bit, qc.wv_bit, qc.a_bit,
                 qc.q_group_size, qc.zero_point, qc.version, calib_data, split, text_column, duo_scaling)
         if quantType.lower() == "awq":
-            self.quantizer = quantizer_cls(*args, **common, **kwargs)
+            self.quantizer = quantizer_cls(*args, **common, awq_search=awq_search, calibration=calibration, **kwargs)
         elif quantType.lower() == "sq":
             self.quantizer = SqQuantizer(*args, **common, calibration=calibration)
         else:

@@ -87,6 +87,12 @@ class AwqQuantizer:
         # this build's int8-MFMA W8A8 mode: per-output-channel int8 weights,
         # per-token (linear) / per-sample (conv) int8 activations on v_mfma_i32_16x16x64_i8
         self.int8_mfma = bool(kwargs.pop("int8_mfma", False))
+        # this build's AWQ scale + clip search for the UNet (awq_search.py; the reference keeps
+        # it off for diffusion, quantizer.py:1050); apply_clip / duo_scaling as the reference's
+        self.awq_search = bool(kwargs.pop("awq_search", False))
+        self.apply_clip = apply_clip
+        self.duo_scaling = duo_scaling
+        self.search_report = None
         self.calib_kwargs = kwargs
         if not diffusion_model:
             raise NotImplementedError("the LLM/VLM AWQ path is out of scope (SURVEY.md §2); diffusion_model=True only")
@@ -125,6 +131,13 @@ class AwqQuantizer:
                     self._apply_quant_fake_act(mod, trav.get_lin_conv(), self.w_bit)
 
     def quantize(self, debugSavePath="", debugPlot=False):
+        if self.awq_search:
+            if not self.quantUnet or not self.duo_scaling:
+                raise NotImplementedError("awq_search: UNet transformer blocks with duo_scaling only")
+            from .awq_search import run_awq_search
+            self.search_report = run_awq_search(self.awq_model, self.w_bit, self.group_size,
+                                                calibration=self.calib_kwargs.get("calibration"),
+                                                clip=self.apply_clip)
         self._swap_components()
 
     @torch.no_grad()

@@ -78,7 +78,10 @@ def test_embed_act_gather_postprocess_bit_exact():
         sig = torch.sigmoid(1.702 * x).float()
         ulp_s = torch.clamp(sig.abs(), min=2.0 ** -14) * 2.0 ** -10 if kind == "quick_gelu" else 0 * sig
         d = (got.float() - ref.float()).abs()
-        bad = d > ulp + x.float().abs() * ulp_s + 1e-7
+        # gelu: for x < -3 the CPU's and this kernel's f32 1 + erf(x / sqrt 2) both cancel (erfc ~ 1e-4
+        # from two ~1-ulp erf values), so the tiny results agree to ~1e-3 relative, not to the fp16 ulp
+        tail = 1e-6 if kind == "gelu" else 1e-7
+        bad = d > ulp + x.float().abs() * ulp_s + tail
         assert not bad.any() and (d == 0).float().mean() > 0.99, \
             (kind, int((d > 0).sum()), x[bad][:8].tolist(), got[bad][:8].tolist(), ref[bad][:8].tolist())
     rows = torch.randn(3 * 77, 64, generator=g).half()
