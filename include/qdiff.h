@@ -272,6 +272,21 @@ int qd_cfg_euler_discrete_step(void* latents, const void* unet_out, int b, int64
 int qd_scale_latents(void* latents, int64_t n, float mul, float div, void* next_in, int c, int c_pad,
                      void* stream);
 
+/* ---------------- fp8 (e4m3) activations: SD3.5's W4A8-fp8 mode ------------------------
+ * (quantize(..., fp8_act=True) with a 4-bit, group-128 config: BASELINE config C5's "fp8
+ * activations on CDNA4"; the reference has no fp8 path - stated-tolerance parity)
+ * Per-token activation codes: s[r] = max(amax_r, 1e-5) / 448 (f32), y = e4m3(x / s) (RNE). */
+int qd_quant_rows_fp8(const void* x, long rows, int c, int ldx, void* y, int ldy, float* scales, void* stream);
+/* W4 codes (int8 [N, K], -8..7) -> e4m3 bytes w8 [N, K] (exact), group scales fp16 [N, K/group] ->
+ * fp32 gs [K/group][N] (transposed for the GEMM's per-stage scale row). */
+int qd_fp8_weight(const int8_t* codes, const void* scales, int n, int k, int group, void* w8, float* gs,
+                  void* stream);
+/* y[M, N] = half(sa[m] * sum_g gs[g][n] * (x8[m, g] . w8[n, g]) + bias) [GELU-tanh] [+ residual]:
+ * x8 e4m3 [M, lda], w8 e4m3 [N, K], K % 128 == 0 (one 128-code group per
+ * v_mfma_scale_f32_16x16x128_f8f6f4), epi: QD_EPI_BIAS | QD_EPI_RESIDUAL | QD_EPI_GELU_TANH. */
+int qd_linear_fp8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* gs,
+                  const void* bias, const void* residual, void* y, int N, int ldy, int epi, void* stream);
+
 /* ---------------- text encoder (CLIP) / VAE decoder ---------------------------------- */
 /* The models around the denoising loop: the reference's pipelines call them through diffusers
  * (models/StableDiffusion1_x.py:19-33 component discovery; base.py:848 pipeline call, whose

@@ -91,10 +91,20 @@ class RefMMDiT:
     """variant "half": torch-CPU Half kernels (the reference's library calls); variant "fp32":
     GEMM / conv / norm / attention / GELU in fp32, rounded to fp16 once (see RefUNet)."""
 
-    def __init__(self, cfg, sd, qc=None, variant="half"):
+    def __init__(self, cfg, sd, qc=None, variant="half", fp8=False):
+        """fp8=True: the W4A8-fp8 mode (oracle/fp8_ref.py) on every linear the product runs it on
+        (4-bit group-128 codes, K % 128 == 0, N % 8 == 0) when the call has >= 64 rows."""
         self.cfg = cfg
         self.ops = _Fp32OpsMM if variant == "fp32" else _HalfOpsMM
         sd = {k: v.detach().to("cpu", F16).contiguous() for k, v in sd.items()}
+        self.f8 = {}
+        if fp8:
+            from . import fp8_ref as F8R
+            g = qc.get("q_group_size", 128)
+            for key, w in sd.items():
+                if key.endswith(".weight") and w.dim() == 2 and qc["w_bit"] <= 4 and g == 128 and \
+                        w.shape[1] % 128 == 0 and w.shape[0] % 8 == 0:
+                    self.f8[key[: -len(".weight")]] = F8R.weight_codes(w, qc["w_bit"], 128)
         if qc is not None:
             self.sd, self.flags = quantize_state_dict(sd, qc)
         else:
@@ -102,6 +112,16 @@ class RefMMDiT:
 
     # ---- layers
     def lin(self, name, x):
+        f8 = self.f8.get(name)
+        if f8 is not None and x.numel() // x.shape[-1] >= 64:
+            from . import fp8_ref as F8R
+            xq, sa = F8R.quant_rows_fp8(x.reshape(-1, x.shape[-1]))
+            _, y, _ = F8R.linear_fp8(xq, sa, f8[0], f8[1], 128, self.sd.get(name + ".bias"))
+            y = y.view(*x.shape[:-1], -1)
+            f = self.flags.get(name)
+            if f and f["out_quant"]:
+                y = FT.per_token(y, f["a_bit"])
+            return y
         y = self.ops.linear(x, self.sd[name + ".weight"], self.sd.get(name + ".bias"))
         f = self.flags.get(name)
         if f and f["out_quant"]:

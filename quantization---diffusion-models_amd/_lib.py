@@ -45,6 +45,9 @@ SIGNATURES = {
     "qd_nhwc_to_nchw": [P, I, I, I, I, P, P],
     "qd_attention": [P, I, P, I, P, I, P, I, I, I, I, I, I, F, P],
     "qd_attention_causal": [P, I, P, I, P, I, P, I, I, I, I, I, F, P],
+    "qd_quant_rows_fp8": [P, ctypes.c_long, I, I, P, I, P, P],
+    "qd_fp8_weight": [P, P, I, I, I, P, P, P],
+    "qd_linear_fp8": [P, P, I, I, I, P, P, P, P, P, I, I, I, P],
     "qd_embed_tokens": [P, I64, I, P, I64, P, I, P, P],
     "qd_clip_act": [P, P, I64, I, P],
     "qd_gather_rows": [P, I64, I64, P, I, I, P, P],

@@ -87,10 +87,12 @@ class BaseAWQForDiffusion(nn.Module):
                  quantText=True, quantVisionProjection=False, quantTextProjection=False, quantUnet=False,
                  quantTextEncoder=False, quantVAE=False, quantTransformer=False, diffusion_model=True,
                  codeBookQuantInd=False, debugPlot=False, debugAttentionMap=False, debugSavePath="",
-                 calibration=None, int8_mfma=False, awq_search=False, **kwargs):
+                 calibration=None, int8_mfma=False, awq_search=False, fp8_act=False, **kwargs):
         """base.py:215-528.  quantType 'awq' = RTN swap; 'sq' = SmoothQuant fold + swap.
         int8_mfma=True (this build, w_bit 8): the int8-MFMA W8A8 mode instead of the reference's
         fake-quant arithmetic (re-granularized, tolerance-based parity).
+        fp8_act=True (w_bit 4, group 128; the SD3.5 transformer): per-token e4m3 activations on
+        the fp8 MFMA, BASELINE config C5's "fp8 activations on CDNA4".
         awq_search=True (quantType 'awq'): the AWQ activation-aware scale search and weight-clip
         search on the UNet's transformer blocks before the RTN swap (awq_search.py; calibration=
         as run_sq_calibration's keywords)."""
@@ -106,7 +108,8 @@ class BaseAWQForDiffusion(nn.Module):
                       quant_act=quant_act, apply_clip=apply_clip, applyScale=applyScale, samples=samples,
                       calib_data_type=calib_data_type, blocksize=blocksize, quantUnet=quantUnet,
                       quantTextEncoder=quantTextEncoder, quantVAE=quantVAE, quantTransformer=quantTransformer,
-                      diffusion_model=True, codeBookQuantInd=codeBookQuantInd, int8_mfma=int8_mfma)
+                      diffusion_model=True, codeBookQuantInd=codeBookQuantInd, int8_mfma=int8_mfma,
+                      fp8_act=fp8_act)
         args = (self, None, None, qc.quantize_act, qc.weight_quant_conv_type, qc.weight_quant_type,
                 qc.act_quant_conv_type, qc.act_quant_conv_group_size, qc.w_bit, qc.wv_bit, qc.a_bit,
                 qc.q_group_size, qc.zero_point, qc.version, calib_data, split, text_column, duo_scaling)

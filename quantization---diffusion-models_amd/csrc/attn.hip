@@ -50,11 +50,11 @@ constexpr int v_stride(int dv) { return ((dv / 2 / 8) & 1) ? dv : dv + 16; }
 //   * NQ query groups of 16 per wave: every K / V^T fragment read from LDS feeds NQ MFMAs, and
 //     every staged K/V tile serves NW * 16 * NQ queries (LDS-read and L2->CU traffic per FLOP
 //     both / NQ; at head_dim 40 both bound the NQ = 1 loop).
-template <int DP, int DV, int NB, int NW, int NQ>
+template <int DP, int DV, int NB, int NW, int NQ, bool CAUSAL = false>
 __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                               int ldk, const f16* __restrict__ v, int ldv,
                                               f16* __restrict__ o, int ldo, int heads, int sq, int skv,
-                                              int d, float scale_log2, int causal) {
+                                              int d, float scale_log2) {
   constexpr int KCH = DP / 8;                  // 16-B chunks per K row (QK^T depth DP)
   constexpr int KCHP = (KCH + 7) / 8 * 8;      // padded so the XOR swizzle stays in the row
   constexpr int VST = v_stride(DV);
@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
     }
     // causal (CLIP text encoder): key kv is visible to query q iff kv <= q; key 0 is in the
     // first tile, so every query's running max is finite after it
-    if (causal && kv0 + KV_T - 1 > q0) {
+    if (CAUSAL && kv0 + KV_T - 1 > q0) {
 #pragma unroll
       for (int g = 0; g < NQ; ++g) {
         const int qrow = q0 + (wid * NQ + g) * 16 + fr;
@@ -315,11 +315,17 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, int causal, hipStream_t st) {
   constexpr int NB = DP <= 96 ? 2 : 1;
   const float sl2 = scale * 1.4426950408889634f;
+  if (causal) {
+    // CLIP text encoder (77 tokens): one compile-time-causal instantiation per head width
+    k_attn<DP, DV, NB, 4, 1, true><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
+    return;
+  }
   if constexpr (DP > 256) {
     // wide heads (the VAE mid-block's single 512-channel head): 4 waves x 16 queries, one
     // 64-key K tile (64 KB) + V tile (66 KB) in LDS, O^T accumulators mostly in AGPRs
     k_attn<DP, DV, 1, 4, 1><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   } else {
   // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2); unset: heuristic
@@ -329,22 +335,22 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
   }();
   if (forced == 1) {
     k_attn<DP, DV, NB, 8, 2><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   }
   if (forced == 2) {
     k_attn<DP, DV, NB, 8, 1><<<((sq + 127) / 128) * b * heads, 512, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   }
   if (forced == 5) {
     k_attn<DP, DV, NB, 4, 2><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   }
   if (forced == 3) {
     k_attn<DP, DV, NB, 4, 1><<<((sq + 63) / 64) * b * heads, 256, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   }
   // long sequences: 8 waves x 2 query groups (256 queries) share each staged K/V tile while the
@@ -355,19 +361,19 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
   if (sq >= 512 && DV > 48 && DV <= 80) {
     const int grid = ((sq + 127) / 128) * b * heads;
     k_attn<DP, DV, NB, 4, 2><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
   } else if (sq >= 512 && DP <= 96 && (long)((sq + 255) / 256) * b * heads >= 512) {
     const int grid = ((sq + 255) / 256) * b * heads;
     k_attn<DP, DV, NB, 8, 2><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
   } else if (sq >= 512) {
     const int grid = ((sq + 127) / 128) * b * heads;
     k_attn<DP, DV, NB, 8, 1><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
   } else {
     const int grid = ((sq + 63) / 64) * b * heads;
     k_attn<DP, DV, NB, 4, 1><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
-                                                  (f16*)o, ldo, heads, sq, skv, d, sl2, causal);
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
   }
   }
 }

@@ -108,7 +108,12 @@ __global__ void k_vae_prescale(const f16* __restrict__ x, long pix, int cin_pad,
   float v = 0.f;
   if (ch < c) {
     v = (float)(f16)((float)x[p * cin_pad + ch] / scale);
-    if (has_shift) v = (float)(f16)(v + shift);
+    if (has_shift) {
+      // keep the f32 rounding of the sum (shift is a full f32 constant): see k_clip_act
+      float t = v + shift;
+      asm volatile("" : "+v"(t));
+      v = (float)(f16)t;
+    }
   }
   y[e] = (f16)v;
 }

@@ -67,6 +67,13 @@ struct GemmArgs {
   int sa_rps;
   const float* sw;  // weight scale per output column (16-B aligned)
   int i8;
+  // fp8 path (qd_linear_fp8, SD3.5's W4A8-fp8 mode): A = per-token e4m3 activation codes, B = the
+  // W4 codes as e4m3 (integers -8..7, exact), both through the half view; one 128-code K group
+  // per LDS stage = one v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales); the group's fp32
+  // weight scales gs[k / 128][n] ride in the stage (LDS-DMA) and scale the MFMA result before it
+  // is added to the accumulator; the row's activation scale sa[m] multiplies the sum.
+  const float* gs;
+  int f8;
 };
 
 constexpr int BK = 64;
@@ -305,6 +312,12 @@ __device__ __forceinline__ float rowgroup_max(float v) {
 }
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ i32x8 f8_operand(f16x8 lo, f16x8 hi) {
+  const i32x4 a = __builtin_bit_cast(i32x4, lo), b = __builtin_bit_cast(i32x4, hi);
+  return (i32x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
 
 // int8 path: C^T fragments of int32 sums -> scaled fp32 (or the raw int32 bits for a split-K slab)
 template <int TM, int TN, bool SPLIT>
@@ -675,6 +688,11 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 constexpr int dma_lds_halves(int bm, int bn, int st, int bkt = 64) {
   return st * (bm + bn) * bkt > bm * (bn + 8) ? st * (bm + bn) * bkt : bm * (bn + 8);
 }
+// fp8 stages carry the group-scale row (BN fp32, one 1-KB DMA wave-instruction) after the B tile
+constexpr int F8_SCL = 512;  // halves
+constexpr int dma_lds_halves_f8(int bm, int bn, int st) {
+  return st * ((bm + bn) * 64 + F8_SCL) > bm * (bn + 8) ? st * ((bm + bn) * 64 + F8_SCL) : bm * (bn + 8);
+}
 // minimum waves per SIMD for __launch_bounds__: (blocks that fit the 160 KB LDS) x waves / 4
 constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt, int bkt = 64) {
   return (163840 / (2 * dma_lds_halves(bm, bn, st, bkt))) * nt / 256 > 0
@@ -682,17 +700,20 @@ constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt, int bkt = 64) {
              : 1;
 }
 
-template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false>
+template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false,
+          bool F8 = false>
 __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
     k_gemm_dma(GemmArgs p) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ASZ = BM * BKT, SSZ = (BM + BN) * BKT;
-  constexpr int LDSZ = dma_lds_halves(BM, BN, ST, BKT);
+  constexpr int ASZ = BM * BKT, SSZ = (BM + BN) * BKT + (F8 ? F8_SCL : 0);
+  constexpr int LDSZ = F8 ? dma_lds_halves_f8(BM, BN, ST) : dma_lds_halves(BM, BN, ST, BKT);
   constexpr int KSUB = BKT / 32;  // 32-deep MFMA slices per stage
   static_assert(PIPE == 0 || (ST >= 3 && BKT == 64), "split-phase pipeline needs >= 3 stages of 64");
   static_assert(!I8 || (BKT == 32 && PIPE == 0), "int8: one 64-code MFMA k-slice per 64-B LDS row");
+  static_assert(!F8 || (BKT == 64 && PIPE == 0 && !SPLIT && BN * 4 <= 1024),
+                "fp8: one 128-code group per 128-B LDS row, no split-K, the scale row in one DMA piece");
   using AL = ADma<BM, NT, AMODE, BKT>;
   using BL = BDma<BN, NT, BKT>;
   __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
@@ -713,12 +734,24 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
   const int fr = lane & 15, fq = lane >> 4;
-  const int per = AL::L + BL::count(wid);  // this wave's loads per K step
+  const int per = AL::L + BL::count(wid) + (F8 && wid == 0 ? 1 : 0);  // this wave's loads per K step
 
   AL al;
   BL bl;
   al.init(p, m0, kbeg, wid);
   bl.init(p, n0, wid);
+  // fp8: wave 0 DMAs the stage's group-scale row gs[k / 128][n0 .. n0 + BN) (4 floats per lane)
+  const __amdgpu_buffer_rsrc_t srs = rsrc(F8 ? (const void*)p.gs : p.b, F8 ? (unsigned)(((p.K + 63) / 64) * p.N * 4) : 0u);
+  unsigned soff = OOB;
+  if constexpr (F8) {
+    const int nn = n0 + lane * 4;
+    soff = (lane * 4 < BN && nn < p.N) ? (unsigned)nn * 4u : OOB;
+  }
+  auto issue_scale = [&](int k0, f16* stage) {
+    if constexpr (F8) {
+      if (wid == 0) glds16(srs, stage + ASZ + BN * BKT, soff == OOB ? OOB : soff + (unsigned)(k0 / 64) * (unsigned)p.N * 4u);
+    }
+  };
 
   f32x4 acc[TM][TN];
   i32x4 iacc[I8 ? TM : 1][I8 ? TN : 1];
@@ -736,6 +769,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
     if (s < nk) {
       al.issue(p, kbeg + s * BKT, smem + s * SSZ, wid);
       bl.issue(p, kbeg + s * BKT, smem + s * SSZ + ASZ, wid);
+      issue_scale(kbeg + s * BKT, smem + s * SSZ);
     }
   }
   auto read_frags = [&](const f16* As, int ks, f16x8 (&af)[TM], f16x8 (&bf)[TN]) {
@@ -780,12 +814,36 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
         if (nx >= ST) nx -= ST;
         al.issue(p, kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ, wid);
         bl.issue(p, kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ + ASZ, wid);
+        issue_scale(kbeg + (kt + ST - 1) * BKT, smem + nx * SSZ);
       }
+      if constexpr (F8) {
+        // the stage's two 16-B chunks per row (fq, fq + 4) form the 32-code operand; A and B take
+        // them in the same order, so the MFMA sums the stage's 128 codes exactly once each
+        f16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+        read_frags(smem + cur * SSZ, 0, a0, b0);
+        read_frags(smem + cur * SSZ, 1, a1, b1);
+        const float* sg = reinterpret_cast<const float*>(smem + cur * SSZ + ASZ + BN * BKT);
+        f32x4 sgv[TN];
 #pragma unroll
-      for (int ks = 0; ks < KSUB; ++ks) {
-        f16x8 af[TM], bf[TN];
-        read_frags(smem + cur * SSZ, ks, af, bf);
-        mfmas(af, bf);
+        for (int j = 0; j < TN; ++j) sgv[j] = *reinterpret_cast<const f32x4*>(sg + wn0 + j * 16 + fq * 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const i32x8 bop = f8_operand(a0[i], a1[i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const f32x4 t = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                f8_operand(b0[j], b1[j]), bop, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0, 127, 0, 127);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(t[r], sgv[j][r], acc[i][j][r]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KSUB; ++ks) {
+          f16x8 af[TM], bf[TN];
+          read_frags(smem + cur * SSZ, ks, af, bf);
+          mfmas(af, bf);
+        }
       }
       if (++cur == ST) cur = 0;
     }
@@ -819,6 +877,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if constexpr (I8) i8_scale<TM, TN, SPLIT>(p, iacc, acc, m0, n0, wm0, wn0);
+  if constexpr (F8) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float s = p.sa[min(m0 + wm0 + i * 16 + fr, p.M - 1)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] *= s;
+    }
+  }
   gemm_epilogue<BM, BN, NT, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
@@ -1310,8 +1376,9 @@ static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register
 extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
                  (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
-                 variant == 201 || (variant >= 300 && variant <= 304),
-             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113), 200/201 halo conv, 300-304 ping-pong");
+                 variant == 201 || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123),
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200/201 halo conv, "
+             "300-304 ping-pong");
   g_force = variant;
   return 0;
 }
@@ -1986,6 +2053,73 @@ extern "C" int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w,
     run_i8<AM_LINEAR>(p, ws, ws_elems, S(stream));
   } else {
     run_i8<AM_CONV>(p, ws, ws_elems, S(stream));
+  }
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- fp8 x fp8 GEMM (SD3.5's W4A8-fp8 mode, qd_linear_fp8) -------------------------------------
+// A: per-token e4m3 activation codes, B: W4 codes as e4m3 with per-(group of 128, column) fp32
+// scales gs[K / 128][N]; v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales: 2x the fp16 MFMA
+// rate) per 128-code group, the group scale applied to the MFMA result, the token scale in the
+// epilogue.  LDS-DMA variants with 128-B rows (BK 64 in the half view), no split-K.
+static constexpr int kF8Var[] = {0, 2, 4, 9};  // qd_gemm_force 120 + i (no 256x256: it spills with the group-scale FMAs)
+
+template <int V>
+static void launch_f8_v(const GemmArgs& p, hipStream_t st) {
+  constexpr DmaVar d = kDmaC[V];
+  static_assert(d.bkt == 64 && d.pipe == 0, "fp8 variants use the 128-B row layout");
+  const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn);
+  k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AM_LINEAR, false, false, true>
+      <<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+}
+
+static int plan_f8(int N) {
+  if (g_force >= 120 && g_force <= 123) return kF8Var[g_force - 120];
+  return N % 160 == 0 ? 0 : 4;
+}
+
+extern "C" int qd_linear_fp8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* gs,
+                             const void* bias, const void* residual, void* y, int N, int ldy, int epi, void* stream) {
+  QD_REQUIRE(x && sa && w && gs && y, "null pointer");
+  QD_REQUIRE(K % 128 == 0 && K > 0, "fp8 GEMM needs K % 128 == 0 (one 128-code weight group per step)");
+  QD_REQUIRE(lda >= K && lda % 16 == 0, "fp8 GEMM needs lda >= K, lda % 16 == 0");
+  QD_REQUIRE(M >= 0 && N > 0 && N % 8 == 0 && ldy % 8 == 0 && ldy >= N, "N / ldy must be multiples of 8, ldy >= N");
+  QD_REQUIRE(!(epi & (QD_EPI_AMAX | QD_EPI_GEGLU)), "fp8 GEMM: no amax / GEGLU epilogue");
+  QD_REQUIRE(!(epi & QD_EPI_GELU_TANH) || !(epi & QD_EPI_RESIDUAL), "GELU-tanh epilogue: no residual");
+  QD_REQUIRE(!(epi & QD_EPI_RESIDUAL) || residual, "residual epilogue without residual");
+  QD_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(gs) |
+               reinterpret_cast<uintptr_t>(y)) & 15) == 0, "x, w, gs, y must be 16-B aligned");
+  QD_REQUIRE(!bias || (reinterpret_cast<uintptr_t>(bias) & 7) == 0, "bias must be 8-B aligned");
+  QD_REQUIRE(!residual || (reinterpret_cast<uintptr_t>(residual) & 15) == 0, "residual must be 16-B aligned");
+  QD_REQUIRE((double)N * K < 2147483648.0 && (double)M * lda < 2147483648.0,
+             "operands exceed the 2 GiB buffer-addressing range");
+  if (M == 0) return 0;
+  GemmArgs p{};
+  p.a = (const f16*)x;
+  p.lda = lda / 2;
+  p.b = w;
+  p.bias = (const f16*)bias;
+  p.res = (const f16*)residual;
+  p.y = (f16*)y;
+  p.ldy = ldy;
+  p.M = M;
+  p.N = N;
+  p.K = K / 2;
+  p.epi = epi;
+  p.sa = sa;
+  p.gs = gs;
+  p.f8 = 1;
+  p.splits = 1;
+  p.kps = p.K;
+  p.a_bytes = (unsigned)((long)(M - 1) * lda + K);
+  p.b_bytes = (unsigned)((long)N * K);
+  hipStream_t st = S(stream);
+  switch (plan_f8(N)) {
+    case 0: launch_f8_v<0>(p, st); break;
+    case 2: launch_f8_v<2>(p, st); break;
+    case 9: launch_f8_v<9>(p, st); break;
+    default: launch_f8_v<4>(p, st); break;
   }
   QD_CHECK_LAUNCH();
   return 0;

@@ -858,3 +858,93 @@ extern "C" int qd_quant_samples_i8(const void* x, int n, long per_sample, int8_t
   QD_CHECK_LAUNCH();
   return 0;
 }
+
+// ---- fp8 (e4m3) activation codes per token (SD3.5's W4A8-fp8 mode) ---------------------------
+// s = max(amax, 1e-5) / 448 (f32), code = e4m3(x / s) with round-to-nearest-even (|x / s| <= 448:
+// no saturation case); scales fp32 [rows]
+template <int PER>
+__global__ void __launch_bounds__(256) k_quant_rows_f8(const f16* __restrict__ x, long rows, int c, int ldx,
+                                                       uint8_t* __restrict__ y, int ldy, float* __restrict__ sa) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int chunks = c >> 3;
+  if (row >= rows) return;
+  f16x8 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + i * 64;
+    v[i] = j < chunks ? *reinterpret_cast<const f16x8*>(x + row * ldx + j * 8) : (f16x8){};
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)v[i][e]));
+  const float s = fmaxf(wave_max(m), 1e-5f) / 448.0f;
+  if (lane == 0) sa[row] = s;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + i * 64;
+    if (j < chunks) {
+      unsigned w[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int pk = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[i][4 * h] / s, (float)v[i][4 * h + 1] / s, 0, false);
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[i][4 * h + 2] / s, (float)v[i][4 * h + 3] / s, pk, true);
+        w[h] = (unsigned)pk;
+      }
+      *reinterpret_cast<uint2*>(y + row * ldy + j * 8) = make_uint2(w[0], w[1]);
+    }
+  }
+}
+
+extern "C" int qd_quant_rows_fp8(const void* x, long rows, int c, int ldx, void* y, int ldy, float* scales,
+                                 void* stream) {
+  QD_REQUIRE(x && y && scales, "null pointer");
+  QD_REQUIRE(c % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && ldx >= c && ldy >= c, "c, ldx, ldy must be multiples of 8");
+  QD_REQUIRE(c <= 16384, "row quantization supports c <= 16384");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 7) == 0, "alignment");
+  if (rows <= 0) return 0;
+  const int per = (c / 8 + 63) / 64;
+  const f16* xp = (const f16*)x;
+  uint8_t* yp = (uint8_t*)y;
+  const int grid = (int)((rows + 3) / 4);
+  hipStream_t st = S(stream);
+  if (per <= 1) k_quant_rows_f8<1><<<grid, 256, 0, st>>>(xp, rows, c, ldx, yp, ldy, scales);
+  else if (per <= 2) k_quant_rows_f8<2><<<grid, 256, 0, st>>>(xp, rows, c, ldx, yp, ldy, scales);
+  else if (per <= 4) k_quant_rows_f8<4><<<grid, 256, 0, st>>>(xp, rows, c, ldx, yp, ldy, scales);
+  else if (per <= 8) k_quant_rows_f8<8><<<grid, 256, 0, st>>>(xp, rows, c, ldx, yp, ldy, scales);
+  else if (per <= 16) k_quant_rows_f8<16><<<grid, 256, 0, st>>>(xp, rows, c, ldx, yp, ldy, scales);
+  else k_quant_rows_f8<32><<<grid, 256, 0, st>>>(xp, rows, c, ldx, yp, ldy, scales);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
+// W4 codes (int8 [N, K], values -8..7) -> e4m3 bytes (exact: small integers), and the group scales
+// fp16 [N, K / g] -> fp32 transposed [K / g][N] (the fp8 GEMM's gs operand)
+__global__ void k_codes_to_fp8(const int8_t* __restrict__ q, long count, uint8_t* __restrict__ y) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= count) return;
+  y[e] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32((float)q[e], 0.f, 0, false) & 0xff);
+}
+
+__global__ void k_scales_t(const f16* __restrict__ s, int n, int ng, float* __restrict__ gs) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)n * ng) return;
+  const int g = (int)(e / n), col = (int)(e - (long)g * n);
+  gs[e] = (float)s[(long)col * ng + g];
+}
+
+extern "C" int qd_fp8_weight(const int8_t* codes, const void* scales, int n, int k, int group, void* w8, float* gs,
+                             void* stream) {
+  QD_REQUIRE(codes && scales && w8 && gs, "null pointer");
+  QD_REQUIRE(group > 0 && k % group == 0, "group must divide K");
+  const long cnt = (long)n * k;
+  if (cnt == 0) return 0;
+  hipStream_t st = S(stream);
+  k_codes_to_fp8<<<(int)((cnt + 255) / 256), 256, 0, st>>>(codes, cnt, (uint8_t*)w8);
+  const long sc = (long)n * (k / group);
+  k_scales_t<<<(int)((sc + 255) / 256), 256, 0, st>>>((const f16*)scales, n, k / group, gs);
+  QD_CHECK_LAUNCH();
+  return 0;
+}

@@ -168,6 +168,7 @@ class WxAxLinear(nn.Module):
         self.qgroup = 0
         self.n_bits_W = 16
         self.int8_mfma = False  # int8-MFMA W8A8 mode (per-row int8 codes x per-token int8 activations)
+        self.fp8_act = False    # W4A8-fp8 mode (W4 group-128 codes as e4m3 x per-token e4m3 activations)
         self.weight_quant_name = weight_quant
         if act_quant == "per_token":
             self.act_quant_name = "per_token"
@@ -215,6 +216,26 @@ class WxAxLinear(nn.Module):
             self._i8_sw = ((sc.data_ptr(), sc._version), sc.float().reshape(-1).contiguous())
         return w, self._i8_sw[1]
 
+    def f8_operand(self):
+        """(e4m3 weight bytes [N, K], fp32 group scales [K / 128, N]) of the W4A8-fp8 mode, or None
+        (layer not in that mode, or its codes went stale)."""
+        if not self.fp8_act:
+            return None
+        cache = getattr(self, "_f8", None)
+        if cache is None or cache[0] != (self.weight.data_ptr(), self.weight._version):
+            return None
+        return cache[1], cache[2]
+
+    def set_fp8(self, codes, scales, group, n_bits):
+        """Build the fp8 operand from the W4 codes (exact in e4m3) and their group-128 scales."""
+        if n_bits > 4 or group != 128 or self.in_features % 128 != 0 or self.out_features % 8 != 0:
+            return False
+        w8, gs = K.fp8_weight(codes.reshape(self.out_features, self.in_features).to(torch.int8),
+                              scales.reshape(self.out_features, -1).to(torch.float16), group)
+        self._f8 = ((self.weight.data_ptr(), self.weight._version), w8, gs)
+        self.fp8_act = True
+        return True
+
     def set_codes(self, codes, scales, group, n_bits):
         """Attach integer codes for the fused-dequant GEMM (int4 packed when n_bits <= 4)."""
         K_ = self.in_features
@@ -248,6 +269,12 @@ class WxAxLinear(nn.Module):
             y = K.linear_i8(xq, sa, i8[0], i8[1], bias=self.bias)
             y = y.reshape(*shape[:-1], self.out_features)
             return self.output_quant(y).to(x.dtype)
+        f8 = self.f8_operand()
+        if f8 is not None:
+            xq, sa = K.quant_rows_fp8(x2)
+            y = K.linear_fp8(xq, sa, f8[0], f8[1], bias=self.bias)
+            y = y.reshape(*shape[:-1], self.out_features)
+            return self.output_quant(y).to(x.dtype)
         w, fmt, sc, g = self.gemm_weight()
         y = K.linear(x2, w, fmt, sc, g, bias=self.bias)
         y = y.reshape(*shape[:-1], self.out_features)
@@ -264,9 +291,11 @@ class WxAxLinear(nn.Module):
     @torch.no_grad()
     def from_float(module, init_only=False, weight_quant="per_channel", act_quant="per_token",
                    quantize_output=False, n_bits_W=8, n_bits_A=16, group_size_W=0, codeBookQuantInd=False,
-                   debugPath=[], debug=False, int8_mfma=False):
+                   debugPath=[], debug=False, int8_mfma=False, fp8_act=False):
         """fake_quant.py:234-258.  int8_mfma=True (this build's int8-MFMA W8A8 mode): per-row
-        8-bit weight codes (weight_quant forced to per_channel) and per-token int8 activations."""
+        8-bit weight codes (weight_quant forced to per_channel) and per-token int8 activations.
+        fp8_act=True (this build's W4A8-fp8 mode): the 4-bit group-128 codes also as e4m3 for
+        the fp8 GEMM with per-token e4m3 activations (layers it does not fit keep A16)."""
         if int8_mfma:
             weight_quant, n_bits_W = "per_channel", 8
         assert isinstance(module, torch.nn.Linear)
@@ -291,6 +320,8 @@ class WxAxLinear(nn.Module):
         new.weight.copy_(wdq)
         if codes is not None and n_bits_W <= 8:
             new.set_codes(codes, scales, g, n_bits_W)
+            if fp8_act:
+                new.set_fp8(codes, scales, g, n_bits_W)
         new.weight_quant_name = weight_quant
         if module.bias is not None:
             new.bias.copy_(module.bias.to(torch.float16))

@@ -414,6 +414,62 @@ def quant_rows_i8(x2d, out=None, scales=None):
     return q, sa
 
 
+F8_VARIANTS = (120, 121, 122, 123)   # qd_gemm_force ids: fp8 LDS-DMA variants (128-B rows)
+
+
+def quant_rows_fp8(x2d, out=None, scales=None):
+    """Per-token e4m3 codes of x2d [M, K]: (codes uint8 [M, K], scales fp32 [M]),
+    s = max(amax, 1e-5) / 448, code = e4m3(x / s) round-to-nearest-even."""
+    if x2d.dtype != torch.float16 or not x2d.is_cuda or x2d.dim() != 2 or x2d.stride(1) != 1:
+        raise ValueError("x must be a 2-D fp16 HIP tensor with unit column stride")
+    M, Kd = x2d.shape
+    q = out if out is not None else _empty((M, Kd), torch.uint8, x2d.device)
+    sa = scales if scales is not None else _empty((M,), torch.float32, x2d.device)
+    _lib.call("qd_quant_rows_fp8", _p(x2d), M, Kd, x2d.stride(0), _p(q), q.stride(0), _p(sa), _stream())
+    return q, sa
+
+
+def fp8_weight(codes, scales, group):
+    """W4 codes int8 [N, K] + fp16 group scales [N, K / group] -> (e4m3 bytes [N, K], fp32 [K / group, N])."""
+    if codes.dtype != torch.int8 or scales.dtype != torch.float16:
+        raise ValueError("codes int8, scales fp16")
+    n, k = codes.shape
+    w8 = torch.empty((n, k), dtype=torch.uint8, device=codes.device)
+    gs = torch.empty((k // group, n), dtype=torch.float32, device=codes.device)
+    _lib.call("qd_fp8_weight", _p(codes.contiguous()), _p(scales.contiguous()), n, k, group, _p(w8), _p(gs), _stream())
+    return w8, gs
+
+
+def linear_fp8(xq, sa, w8, gs, bias=None, residual=None, out=None, gelu_tanh=False):
+    """y = half(sa[m] * sum_g gs[g][n] (x8 . w8)_g + bias) [GELU-tanh] [+ residual]: xq e4m3 codes
+    [M, K] (row stride may exceed K), w8 e4m3 [N, K], gs fp32 [K / 128, N]."""
+    if xq.dtype != torch.uint8 or w8.dtype != torch.uint8 or xq.dim() != 2 or xq.stride(1) != 1:
+        raise ValueError("xq / w8 must be uint8 e4m3 codes, xq 2-D with unit column stride")
+    M, Kd = xq.shape
+    N = w8.shape[0]
+    if out is None:
+        out = _empty((M, N), torch.float16, xq.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
+          (EPI_GELU_TANH if gelu_tanh else 0)
+
+    def launch(c, y):
+        _force(c if _OVERRIDE is None else _OVERRIDE)
+        try:
+            _lib.call("qd_linear_fp8", _p(xq), _p(sa), M, Kd, xq.stride(0), _p(w8), _p(gs), _p(bias), _p(residual),
+                      _p(y), N, y.stride(0), epi, _stream())
+        finally:
+            _force(-1)
+
+    key = ("linear_fp8", M, N, Kd, xq.stride(0), epi)
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        c = _choose(key, list(F8_VARIANTS), lambda c: launch(c, ty))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else -1, out)
+    return out
+
+
 def quant_samples_i8(x, out=None, scales=None):
     """int8 codes of x [N, ...] with one scale per sample (the conv-input granularity of the
     int8 mode): (codes int8 of x's shape, scales [N] fp32)."""

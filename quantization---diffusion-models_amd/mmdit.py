@@ -403,6 +403,34 @@ def _stacked_operand(owner, attr, layers, allow_out_quant=False):
     return op
 
 
+def _stacked_f8(owner, attr, layers, allow_out_quant=False):
+    """W4A8-fp8 form of _stacked_operand: (e4m3 weights [sum N, K], fp32 group scales
+    [K / 128, sum N], bias, slots) when every layer is in the fp8 mode, else None."""
+    oq = set()
+    for l in layers:
+        if not isinstance(l, WxAxLinear) or l.f8_operand() is None or getattr(l, "_qd_hook", None) is not None \
+                or l.bias is None or l.quantize_act:
+            return None
+        oq.add(_out_quant(l))
+    if len(oq) != 1 or (not allow_out_quant and oq != {None}):
+        return None
+    ops = [l.f8_operand() for l in layers]
+    ver = tuple((o[0].data_ptr(), l.weight._version, l.bias._version) for o, l in zip(ops, layers))
+    cache = owner.__dict__.get(attr)
+    if cache is not None and cache[0] == ver:
+        return cache[1]
+    w8 = torch.cat([o[0] for o in ops]).contiguous()
+    gs = torch.cat([o[1] for o in ops], dim=1).contiguous()
+    b = torch.cat([l.bias.detach() for l in layers]).contiguous()
+    slots, off = [], 0
+    for l in layers:
+        slots.append((off, l.out_features))
+        off += l.out_features
+    op = (w8, gs, b, slots)
+    owner.__dict__[attr] = (ver, op)
+    return op
+
+
 def joint_qkv(attn, nx, nc, n, s, sc):
     """The joint [x; context] q|k|v sequence [n, s + sc, 3C] of JointAttnProcessor2_0, qk-normed."""
     c = nx.shape[1]
@@ -412,7 +440,13 @@ def joint_qkv(attn, nx, nc, n, s, sc):
     J = A.empty((n, L, 3 * c), torch.float16, nx.device)
     # x stream: to_q | to_k | to_v, written per sample into its first s rows
     opx = _stacked_operand(attn, "_qd_qkv_x", [attn.to_q, attn.to_k, attn.to_v])
-    if opx is not None:
+    opx8 = _stacked_f8(attn, "_qd_qkv_x8", [attn.to_q, attn.to_k, attn.to_v]) if nx.shape[0] >= 64 else None
+    if opx8 is not None:   # W4A8-fp8 mode: one per-token e4m3 quantization, per-sample GEMMs
+        w8, gs, b, _ = opx8
+        xq, sa = K.quant_rows_fp8(nx)
+        for i in range(n):
+            K.linear_fp8(xq[i * s:(i + 1) * s], sa[i * s:(i + 1) * s], w8, gs, bias=b, out=J[i, :s])
+    elif opx is not None:
         w, fmt, scl, g, b, wf, _ = opx
         for i in range(n):
             K.linear(nx[i * s:(i + 1) * s], w, fmt, scl, g, bias=b, weight_f16=wf, out=J[i, :s])
@@ -422,7 +456,16 @@ def joint_qkv(attn, nx, nc, n, s, sc):
     # context stream: add_q | add_k | add_v (+ per-token output fake-quant of each projection)
     cl = (attn.add_q_proj, attn.add_k_proj, attn.add_v_proj)
     opc = _stacked_operand(attn, "_qd_qkv_c", list(cl), allow_out_quant=True)
-    if opc is not None:
+    opc8 = _stacked_f8(attn, "_qd_qkv_c8", list(cl), allow_out_quant=True) if nc.shape[0] >= 64 else None
+    if opc8 is not None:
+        w8, gs, b, _ = opc8
+        xq, sa = K.quant_rows_fp8(nc)
+        yc = K.linear_fp8(xq, sa, w8, gs, bias=b)
+        oq = _out_quant(cl[0])
+        if oq is not None:
+            y2 = yc.view(-1, c)
+            K.act_fakequant(y2, oq[0], oq[1], out=y2)
+    elif opc is not None:
         w, fmt, scl, g, b, wf, _ = opc
         yc = K.linear(nc, w, fmt, scl, g, bias=b, weight_f16=wf)
         oq = _out_quant(cl[0])
@@ -463,6 +506,10 @@ def _ff(ff, x):
     proj = ff.net[0].proj
     plain = getattr(proj, "_qd_hook", None) is None and not (
         isinstance(proj, WxAxLinear) and (proj.quantize_act or proj.output_quant_name != "None"))
+    f8 = proj.f8_operand() if plain and isinstance(proj, WxAxLinear) and x.shape[0] >= 64 else None
+    if f8 is not None:   # W4A8-fp8 mode: GELU-tanh in the fp8 GEMM's epilogue
+        xq, sa = K.quant_rows_fp8(x)
+        return run_linear(ff.net[2], K.linear_fp8(xq, sa, f8[0], f8[1], bias=proj.bias, gelu_tanh=True))
     if plain:
         w, fmt, sc, g = _linear_op(proj)
         wf = proj.weight if fmt != "f16" else None
@@ -482,7 +529,11 @@ def self_attn_fwd(attn, nx, n, s):
     heads = attn.heads
     d = c // heads
     op = _stacked_operand(attn, "_qd_qkv", [attn.to_q, attn.to_k, attn.to_v])
-    if op is not None:
+    op8 = _stacked_f8(attn, "_qd_qkv8", [attn.to_q, attn.to_k, attn.to_v]) if nx.shape[0] >= 64 else None
+    if op8 is not None:
+        xq, sa = K.quant_rows_fp8(nx)
+        J = K.linear_fp8(xq, sa, op8[0], op8[1], bias=op8[2])
+    elif op is not None:
         w, fmt, scl, g, b, wf, _ = op
         J = K.linear(nx, w, fmt, scl, g, bias=b, weight_f16=wf)
     else:

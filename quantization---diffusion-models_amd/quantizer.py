@@ -87,6 +87,8 @@ class AwqQuantizer:
         # this build's int8-MFMA W8A8 mode: per-output-channel int8 weights,
         # per-token (linear) / per-sample (conv) int8 activations on v_mfma_i32_16x16x64_i8
         self.int8_mfma = bool(kwargs.pop("int8_mfma", False))
+        # this build's W4A8-fp8 mode for the SD3.5 transformer (per-token e4m3 activations)
+        self.fp8_act = bool(kwargs.pop("fp8_act", False))
         # this build's AWQ scale + clip search for the UNet (awq_search.py; the reference keeps
         # it off for diffusion, quantizer.py:1050); apply_clip / duo_scaling as the reference's
         self.awq_search = bool(kwargs.pop("awq_search", False))
@@ -150,7 +152,8 @@ class AwqQuantizer:
                                              quantize_output=_is_bmm_input(name), n_bits_W=bitWidth,
                                              n_bits_A=self.a_bit, group_size_W=self.group_size,
                                              codeBookQuantInd=self.codeBookQuantInd,
-                                             int8_mfma=i8 and layer.in_features % 64 == 0)
+                                             int8_mfma=i8 and layer.in_features % 64 == 0,
+                                             fp8_act=self.fp8_act)
                 setattr(parent, name, fake)
             elif isinstance(layer, nn.Conv2d):
                 fake = WxAxConv2d.from_float(layer, weight_quant=self.weight_quant_conv_type,

@@ -522,6 +522,14 @@ def run_linear(layer, x2d, residual=None, out=None):
     if hook is not None:  # SmoothQuant calibration (calib.py)
         hook(x2d)
     if isinstance(layer, WxAxLinear):
+        f8 = layer.f8_operand() if x2d.shape[0] >= I8_MIN_ROWS else None
+        if f8 is not None:   # W4A8-fp8 mode (SD3.5): per-token e4m3 activations
+            xq, sa = K.quant_rows_fp8(x2d)
+            if layer.output_quant_name != "None":
+                y = K.linear_fp8(xq, sa, f8[0], f8[1], bias=layer.bias, out=out)
+                y = K.act_fakequant(y, layer.output_quant_name, layer.n_bits_A, out=y)
+                return K.add(y, residual, out=y) if residual is not None else y
+            return K.linear_fp8(xq, sa, f8[0], f8[1], bias=layer.bias, residual=residual, out=out)
         i8 = layer.i8_operand() if x2d.shape[0] >= I8_MIN_ROWS else None
         if i8 is not None:
             xq, sa = K.quant_rows_i8(x2d)
