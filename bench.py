@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4, help="prompts per GPU")
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--denoise-steps", type=int, default=50)
-    ap.add_argument("--mode", default=None, choices=["w8a8-sq", "w8a8", "w4a16", "fp16", "w8a8-sq-int8", "w8a8-int8"],
+    ap.add_argument("--mode", default=None, choices=["w8a8-sq", "w8a8", "w4a16", "fp16", "w8a8-sq-int8", "w8a8-int8",
+                                                     "w4a8-fp8"],
                     help="default: w8a8-sq (sd15), w4a16 (sd35, SURVEY config C5)")
     ap.add_argument("--model", default="sd15", choices=["sd15", "sdxl", "sd35"],
                     help="secondary lines: sdxl = SDXL W8A8 1024^2, 2 prompts per GPU (config C4); "
@@ -82,7 +83,11 @@ QCFG = {
     "w8a8-sq-int8": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
     "w8a8-int8": dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True),
     "w4a16": dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
+    # SD3.5 (config C5's "fp8 activations on CDNA4"): W4 g128 codes as e4m3,
+    # per-token e4m3 activations on v_mfma_scale_f32_16x16x128_f8f6f4
+    "w4a8-fp8": dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
 }
+PEAK_F8_TFLOPS = 5000.0         # MI355X_MICROARCH.md: block-scaled fp8 MFMA = 2x the BF16 rate (dense)
 
 
 def mmdit_gflop_per_sample(cfg, s, sc):
@@ -110,7 +115,7 @@ def build_model(args, dev):
         from qdiff.models import StableDiffusion3_5
         model = StableDiffusion3_5.from_pretrained("synthetic:sd35", device=dev, seed=0)
         if args.mode != "fp16":
-            model.quantize(quant_config=dict(QCFG[args.mode]), quantTransformer=True)
+            model.quantize(quant_config=dict(QCFG[args.mode]), quantTransformer=True, fp8_act=args.mode == "w4a8-fp8")
         return model
     from qdiff.models import StableDiffusion1_x
     model = StableDiffusion1_x.from_pretrained("synthetic:sd15", device=dev, seed=0)
@@ -449,9 +454,13 @@ def mmdit_dominant_roofline(model, dev, s, iters=10):
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
     tflops = 2.0 * m * n * k / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(tflops, 1), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
-            "kernel": f"ff.net.0.proj GEMM M={m} N={n} K={k} ({getattr(layer, 'qfmt', 'f16')} weights)",
+    f8 = getattr(layer, "fp8_act", False)
+    peak = PEAK_F8_TFLOPS if f8 else PEAK_F16_TFLOPS
+    return {"bound": "mfma", "achieved": round(tflops, 1), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(tflops / peak, 4), "traffic": None,
+            "kernel": f"ff.net.0.proj GEMM M={m} N={n} K={k} "
+                      + ("(e4m3 x e4m3, v_mfma_scale_f32_16x16x128_f8f6f4, per-token quant included)" if f8 else
+                         f"({getattr(layer, 'qfmt', 'f16')} weights)"),
             "avg_us": round(ms * 1e3, 2)}
 
 
@@ -553,7 +562,8 @@ def main_sd35(args, model, rank, world, dev, log):
             "metric": f"images/sec SD3.5-Large {args.mode.upper()} {args.res}x{args.res} {args.denoise_steps}-step",
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "e4m3 activations x e4m3-coded W4 (fp32 accumulate) + f16" if args.mode == "w4a8-fp8" else "f16",
             "data": "synthetic (random-init SD3.5-Large MMDiT weights N(0,1/fan_in), synthetic text embeddings)",
             "config": {"workload": f"SD3.5-Large MMDiT {args.mode} g128 fake-quant, {args.res}x{args.res}, {B} "
                                    f"prompt(s)/GPU (CFG batch {2 * B}), {args.denoise_steps} flow-match Euler "

@@ -122,6 +122,7 @@ class BaseAWQForDiffusion(nn.Module):
         self.quantizer.quantize(debugSavePath, debugPlot)
         self.is_quantized = True
         self.int8_mfma = bool(int8_mfma)
+        self.fp8_act = bool(fp8_act)
         self._loops = {}
 
     # ---------------------------------------------------------------- generate
@@ -219,8 +220,8 @@ class BaseAWQForDiffusion(nn.Module):
         with open(os.path.join(save_dir, "quant_components.json"), "w") as f:
             json.dump(self.quantized_components, f, indent=2)
         with open(os.path.join(save_dir, "qdiff_quant.json"), "w") as f:
-            json.dump(dict(self.quant_config.full_dict(), int8_mfma=bool(getattr(self, "int8_mfma", False))), f,
-                      indent=2)
+            json.dump(dict(self.quant_config.full_dict(), int8_mfma=bool(getattr(self, "int8_mfma", False)),
+                           fp8_act=bool(getattr(self, "fp8_act", False))), f, indent=2)
         from .export import awq_pack_linear, conv_codes, packed_nibbles_to_codes
         codes, awq = {}, {}
         for name, m in self.pipeline.denoiser.named_modules():
@@ -290,6 +291,7 @@ class BaseAWQForDiffusion(nn.Module):
         apath = os.path.join(model_path, sub, "awq_gemm.safetensors")
         awq = load_file(apath) if os.path.exists(apath) and not codes else {}
         int8 = bool((full or {}).get("int8_mfma", False))
+        fp8 = bool((full or {}).get("fp8_act", False))
         for name, m in net.named_modules():
             if isinstance(m, WxAxConv2d):
                 if f"{name}.i8_w" in codes:
@@ -318,10 +320,15 @@ class BaseAWQForDiffusion(nn.Module):
                 # the integer codes and keep them only if they reproduce the buffer bit for bit
                 rederive_codes(m, qc["bits"], qc["group_size"])
                 m.int8_mfma = int8 and m.qfmt == "i8" and m.qgroup == m.in_features
+            if fp8 and m.qfmt == "i4" and m.gemm_weight()[1] == "i4":
+                from .export import packed_nibbles_to_codes
+                m.set_fp8(packed_nibbles_to_codes(m.qcodes, m.in_features), m.qscales, m.qgroup, m.n_bits_W)
+        from .pipeline_io import _local_aux, load_scheduler_config
+        aux = dict(lazy=_local_aux(model_path), scheduler_config=load_scheduler_config(model_path))
         if sub == "transformer":
-            pipe = QDiffPipeline(transformer=net, class_name=cls_name, config={"_class_name": cls_name})
+            pipe = QDiffPipeline(transformer=net, class_name=cls_name, config={"_class_name": cls_name}, **aux)
         else:
-            pipe = QDiffPipeline(net, cls_name, config={"_class_name": cls_name})
+            pipe = QDiffPipeline(net, cls_name, config={"_class_name": cls_name}, **aux)
         if isinstance(self_or_cls, type):
             obj = self_or_cls(pipe, cls_name, is_quantized=True, config={"_class_name": cls_name}, quant_config=qcfg)
         else:
@@ -332,6 +339,7 @@ class BaseAWQForDiffusion(nn.Module):
             obj._loops = {}
         obj.quantized_components = comps
         obj.int8_mfma = bool((full or {}).get("int8_mfma", False))
+        obj.fp8_act = fp8
         return obj
 
 

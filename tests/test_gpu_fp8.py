@@ -181,3 +181,23 @@ def test_sd35_large_width_fp8_accuracy_vs_w4a16():
     print(f"SD3.5-L width, 2 blocks: W4A8-fp8 vs W4A16 max {mx:.4g} mean {mean:.4g}")
     assert torch.isfinite(outs[True].float()).all()
     assert mx <= 0.15 and mean <= 0.02, (mx, mean)
+
+
+def test_fp8_mode_save_load_roundtrip(tmp_path):
+    """save_quantized / from_quantized keep the fp8 mode (rebuilt from the stored W4 codes)."""
+    from qdiff.models import StableDiffusion3_5
+    model = StableDiffusion3_5.from_pretrained("synthetic:sd35-tiny", device=DEV, seed=5)
+    model.quantize(quant_config=dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False),
+                   quantTransformer=True, fp8_act=True)
+    cfg = model.pipeline.transformer.config
+    model.save_quantized(str(tmp_path))
+    re = StableDiffusion3_5.from_quantized(str(tmp_path), "StableDiffusion3Pipeline")
+    assert re.fp8_act
+    n1 = sum(1 for m in model.pipeline.transformer.modules() if getattr(m, "fp8_act", False))
+    n2 = sum(1 for m in re.pipeline.transformer.modules() if getattr(m, "fp8_act", False))
+    assert n1 == n2 > 0
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, cfg.in_channels, cfg.sample_size, cfg.sample_size, generator=g).half()
+    enc = torch.randn(2, 40, cfg.joint_attention_dim, generator=g).half()
+    pooled = torch.randn(2, cfg.pooled_projection_dim, generator=g).half()
+    assert torch.equal(_one_eval(model, x, 401.0, enc, pooled), _one_eval(re, x, 401.0, enc, pooled))
