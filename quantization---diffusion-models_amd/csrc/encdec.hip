@@ -109,8 +109,9 @@ __global__ void k_vae_prescale(const f16* __restrict__ x, long pix, int cin_pad,
   if (ch < c) {
     v = (float)(f16)((float)x[p * cin_pad + ch] / scale);
     if (has_shift) {
-      // keep the f32 rounding of the sum (shift is a full f32 constant): see k_clip_act
-      float t = v + shift;
+      // torch casts a Python-number addend to the tensor's dtype (div keeps the f32 scalar):
+      // half(shift), then the f32 sum rounded once (the barrier keeps it from folding, see k_clip_act)
+      float t = v + (float)(f16)shift;
       asm volatile("" : "+v"(t));
       v = (float)(f16)t;
     }
