@@ -909,7 +909,11 @@ constexpr int pp_lds_halves(int bn) {
   return 4 * (256 + bn) * 32 > 128 * (bn + 8) ? 4 * (256 + bn) * 32 : 128 * (bn + 8);
 }
 
-template <int BN, int WGM, int AMODE, bool SPLIT>
+// I8: the int8-MFMA mode's operands through the same half view (a 32-half K-tile = one 64-code
+// v_mfma_i32_16x16x64_i8 slice, the fragment reads unchanged); the int32 sums live in the fp32
+// accumulator registers (bit-cast) and are scaled by sa[m] * sw[n] before the epilogue, or go
+// to the split-K slab as int32 bits (k_splitk_reduce's i8 path) - the k_gemm_dma<I8> arithmetic.
+template <int BN, int WGM, int AMODE, bool SPLIT, bool I8 = false>
 __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   constexpr int BM = 256, BK = 32, NT = 512;
   constexpr int WGN = 8 / WGM;                      // wave grid WGM x WGN (2x4 or 4x2)
@@ -977,8 +981,14 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < TH; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[ih * TH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[ih * TH + i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (I8)
+          acc[ih * TH + i][j] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, bf[j]), __builtin_bit_cast(i32x4, af[i]),
+                                                          __builtin_bit_cast(i32x4, acc[ih * TH + i][j]), 0, 0, 0));
+        else
+          acc[ih * TH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[ih * TH + i][j], 0, 0, 0);
+      }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1053,15 +1063,23 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
         const bool col_ok = n < p.N;
         f16x4 bq = {};
         if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+        f32x4 sw = {};
+        if (I8 && col_ok) sw = *reinterpret_cast<const f32x4*>(p.sw + n);
         float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int ml = wm0 - pass * 128 + i * 16 + fr;  // row within this pass's 128
           const bool ok = m0 + pass * 128 + ml < p.M && col_ok;
+          float sa = 0.f;
+          if constexpr (I8) {  // int32 sum -> (q * sa[m]) * sw[n], as i8_scale
+            const int m = min(m0 + pass * 128 + ml, p.M - 1);
+            sa = p.sa[p.sa_rps ? m / p.sa_rps : m];
+          }
           f16x4 h;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
+            const float v = I8 ? ((float)__builtin_bit_cast(i32x4, acc[i][j])[r] * sa) * sw[r] : acc[i][j][r];
+            h[r] = (f16)(v + (float)bq[r]);
             if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
           }
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
@@ -1376,9 +1394,10 @@ static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register
 extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
                  (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
-                 variant == 201 || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123),
+                 variant == 201 || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123) ||
+                 (variant >= 130 && variant <= 134),
              "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200/201 halo conv, "
-             "300-304 ping-pong");
+             "300-304 ping-pong (int8: 130-134)");
   g_force = variant;
   return 0;
 }
@@ -1887,6 +1906,19 @@ static void launch_i8_v(const GemmArgs& p, hipStream_t st) {
   k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT, true><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
 }
 
+// int8 ping-pong 256 x BN (qd_gemm_force 130 + i, BN = kPpBn[i])
+static constexpr int kPpBn[] = {256, 320, 192, 160, 128};
+
+template <int AMODE, bool SPLIT>
+static void launch_pp_i8(const GemmArgs& p, int bn, hipStream_t st) {
+  const int nwg = ((p.M + 255) / 256) * ((p.N + bn - 1) / bn) * p.splits;
+  if (bn == 256) k_gemm_pp<256, 2, AMODE, SPLIT, true><<<nwg, 512, 0, st>>>(p);
+  else if (bn == 320) k_gemm_pp<320, 2, AMODE, SPLIT, true><<<nwg, 512, 0, st>>>(p);
+  else if (bn == 192) k_gemm_pp<192, 2, AMODE, SPLIT, true><<<nwg, 512, 0, st>>>(p);
+  else if (bn == 160) k_gemm_pp<160, 4, AMODE, SPLIT, true><<<nwg, 512, 0, st>>>(p);
+  else k_gemm_pp<128, 4, AMODE, SPLIT, true><<<nwg, 512, 0, st>>>(p);
+}
+
 template <int AMODE, bool SPLIT>
 static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
   switch (var) {
@@ -1900,6 +1932,21 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // variant: qd_gemm_force 110..113 (DMA variants 10-13, the 64-B-row family), else a default by
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu) {
+  if (g_force >= 130 && g_force <= 134) {
+    // ping-pong: wave rows 128 (BN >= 192) or 64 must lie in one sample for the amax epilogue
+    const int bnp = kPpBn[g_force - 130];
+    if (!amax || rows_per_sample % (bnp >= 192 ? 128 : 64) == 0) {
+      Plan pl{3, 256, bnp, 0, 1, Kh};
+      const long tiles_mn = (long)((M + 255) / 256) * ((N + bnp - 1) / bnp);
+      for (int sp = 2; sp <= 32 && !geglu && Kh % 32 == 0; ++sp) {
+        if ((Kh / 32) % sp != 0 || Kh / sp < 256) continue;
+        if (tiles_mn * sp > 256L) break;
+        pl.splits = sp;
+        pl.kps = Kh / sp;
+      }
+      return pl;
+    }
+  }
   int var = N % 160 == 0 ? 10 : 11;
   if (g_force >= 110 && g_force <= 113) var = g_force - 100;
   if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
@@ -1928,10 +1975,12 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   p.splits = pl.splits;
   p.kps = pl.kps;
   if (pl.splits == 1) {
-    launch_i8<AMODE, false>(p, pl.var, st);
+    if (pl.kind == 3) launch_pp_i8<AMODE, false>(p, pl.bn, st);
+    else launch_i8<AMODE, false>(p, pl.var, st);
   } else {
     p.part = ws;
-    launch_i8<AMODE, true>(p, pl.var, st);
+    if (pl.kind == 3) launch_pp_i8<AMODE, true>(p, pl.bn, st);
+    else launch_i8<AMODE, true>(p, pl.var, st);
     const int gx = (p.N + 255) / 256;
     if ((long)gx * ((p.M + 15) / 16) >= 512) k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
     else k_splitk_reduce<1><<<dim3(gx, (p.M + 3) / 4), 256, 0, st>>>(p);

@@ -399,7 +399,8 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 # ---------------------------------------------------------------- int8-MFMA W8A8 mode
 # int8 x int8 GEMMs (qd_linear_i8 / qd_conv2d_i8): exact int32 sums, so every tile variant and
 # split gives identical bits - the tuner below only picks the fastest.
-I8_VARIANTS = (110, 111, 112, 113)   # qd_gemm_force ids: LDS-DMA variants 10-13 (64-B rows)
+I8_VARIANTS = (110, 111, 112, 113,   # qd_gemm_force ids: LDS-DMA variants 10-13 (64-B rows)
+               130, 131, 132, 133, 134)  # ping-pong 256 x {256, 320, 192, 160, 128}
 
 
 def quant_rows_i8(x2d, out=None, scales=None):

@@ -16,6 +16,10 @@ def K():
     return kernels
 
 
+# tuned choice, the LDS-DMA variants and the 256-row ping-pong variants (kernels.I8_VARIANTS)
+I8_FORCE = [None, 110, 111, 112, 113, 130, 131, 132, 133, 134]
+
+
 def _bits(a):
     return np.ascontiguousarray(a).view(np.uint16)
 
@@ -47,7 +51,7 @@ def test_sample_codes(dev):
 
 @pytest.mark.parametrize("M,N,Kd", [(64, 64, 64), (200, 320, 320), (616, 640, 768), (4096, 2560, 320),
                                     (8, 1280, 1280), (1000, 64, 128), (256, 1280, 5120), (77, 320, 2560)])
-@pytest.mark.parametrize("variant", [None, 110, 111, 112, 113])
+@pytest.mark.parametrize("variant", I8_FORCE)
 def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
     k = K()
     rng = np.random.default_rng(M + N + Kd)
@@ -67,8 +71,17 @@ def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
     assert np.array_equal(_bits(y), _bits(ref)), np.abs(y.astype(np.float32) - ref.astype(np.float32)).max()
 
 
-def test_linear_i8_geglu_and_amax(dev):
+@pytest.mark.parametrize("variant", [None, 110, 130, 131, 133])
+def test_linear_i8_geglu_and_amax(variant, dev):
     k = K()
+    k.force_gemm(variant)
+    try:
+        _geglu_amax(k, dev)
+    finally:
+        k.force_gemm(None)
+
+
+def _geglu_amax(k, dev):
     rng = np.random.default_rng(9)
     M, I, Kd = 512, 640, 320
     x = rng.standard_normal((M, Kd)).astype(np.float16)
@@ -92,7 +105,7 @@ def test_linear_i8_geglu_and_amax(dev):
                                                         (128, 64, 1, 1, 8, False), (64, 64, 3, 1, 8, True),
                                                         (320, 320, 3, 1, 32, False), (640, 640, 3, 1, 16, False),
                                                         (1280, 1280, 3, 1, 8, False), (960, 320, 3, 1, 16, False)])
-@pytest.mark.parametrize("variant", [None, 110, 111, 112, 113])
+@pytest.mark.parametrize("variant", I8_FORCE)
 def test_conv2d_i8_bit_exact(cin, cout, ksz, stride, hw, ups, variant, dev):
     k = K()
     rng = np.random.default_rng(cin * 7 + cout + ksz)
