@@ -1388,6 +1388,8 @@ static constexpr DmaVar kDmaC[] = {
     {128, 128, 2, 2, 4, 0, 1.00, 32},  // 11: BK 32, 4 stages, 2 blocks / CU
     {128, 320, 2, 4, 4, 0, 1.00, 32},  // 12: BK 32, 4 stages, 1 block / CU
     {256, 256, 2, 4, 4, 0, 1.00, 32},  // 13: BK 32, 4 stages, 1 block / CU
+    {128, 64, 2, 2, 4, 0, 1.00, 32},   // 14: BK 32, 4 stages, small-M / short-K shapes
+    {64, 64, 2, 2, 4, 0, 1.00, 32},    // 15: BK 32, 4 stages, small-M / short-K shapes
 };
 static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
 
@@ -1514,7 +1516,9 @@ static void launch_dma(const GemmArgs& p, int var, hipStream_t st) {
     case 10: launch_dma_v<10, AMODE, SPLIT>(p, st); break;
     case 11: launch_dma_v<11, AMODE, SPLIT>(p, st); break;
     case 12: launch_dma_v<12, AMODE, SPLIT>(p, st); break;
-    default: launch_dma_v<13, AMODE, SPLIT>(p, st); break;
+    case 13: launch_dma_v<13, AMODE, SPLIT>(p, st); break;
+    case 14: launch_dma_v<14, AMODE, SPLIT>(p, st); break;
+    default: launch_dma_v<15, AMODE, SPLIT>(p, st); break;
   }
 }
 
@@ -1925,11 +1929,13 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
     case 10: launch_i8_v<10, AMODE, SPLIT>(p, st); break;
     case 12: launch_i8_v<12, AMODE, SPLIT>(p, st); break;
     case 13: launch_i8_v<13, AMODE, SPLIT>(p, st); break;
+    case 14: launch_i8_v<14, AMODE, SPLIT>(p, st); break;
+    case 15: launch_i8_v<15, AMODE, SPLIT>(p, st); break;
     default: launch_i8_v<11, AMODE, SPLIT>(p, st); break;
   }
 }
 
-// variant: qd_gemm_force 110..113 (DMA variants 10-13, the 64-B-row family), else a default by
+// variant: qd_gemm_force 110..115 (DMA variants 10-15, the 64-B-row family), else a default by
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu) {
   if (g_force >= 130 && g_force <= 134) {
@@ -1948,7 +1954,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
     }
   }
   int var = N % 160 == 0 ? 10 : 11;
-  if (g_force >= 110 && g_force <= 113) var = g_force - 100;
+  if (g_force >= 110 && g_force <= 115) var = g_force - 100;
   if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];

@@ -407,7 +407,7 @@ def forced_gemm():
     kernels.force_gemm(None)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 114)) + [200, 201, 300, 301, 302, 303, 304])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 116)) + [200, 201, 300, 301, 302, 303, 304])
 def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     """Every kernel family / tile (register-staged and LDS-DMA) on ragged shapes: rows past M,
     conv halo, stride 2, fused 2x upsample, the 4-channel conv_in (any-Ci decode), K tails,
