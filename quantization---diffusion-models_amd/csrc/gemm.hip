@@ -351,9 +351,14 @@ __device__ __forceinline__ void i8_scale(const GemmArgs& p, const i32x4 (&acc)[T
 
 // ---- shared epilogue ----------------------------------------------------------------------
 // acc[i][j]: C^T fragment (rows n = n0 + wn0 + 16j + 4fq + r, column m = m0 + wm0 + 16i + fr).
-template <int BM, int BN, int NT, int TM, int TN, bool SPLIT>
+// LDS halves the epilogue needs: the [BM][BN + 8] fp16 C tile + the per-wave-row column-max
+// slots of the amax combine (WGM x BN floats, WGM <= 8)
+constexpr int epi_lds_halves(int bm, int bn) { return bm * (bn + 8) + 16 * bn; }
+
+template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM][TN], f16* smem, int m0, int n0,
                                               int wm0, int wn0, int split) {
+  static_assert(SPLIT || epi_lds_halves(BM, BN) <= LDSH, "epilogue LDS exceeds the kernel's buffer");
   const int lane = threadIdx.x & 63;
   const int fr = lane & 15, fq = lane >> 4;
   if constexpr (SPLIT) {
@@ -380,6 +385,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
     const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
     const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+    // amax: the WGM wave rows of the block combine their column maxes in LDS first when the
+    // block's rows lie in one sample, so each (sample, column) address takes one atomic per
+    // block instead of one per wave row (same-line atomic chains bound this epilogue)
+    constexpr int WM = TM * 16, WGM = BM / WM;
+    static_assert(WGM <= 8, "column-max slots");
+    float* const cmx = reinterpret_cast<float*>(ct + BM * LP);
+    const bool blk_amax = do_amax && !geglu && WGM > 1 && p.rows_per_sample % BM == 0;
     {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -406,7 +418,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
 #pragma unroll
           for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
           const int row0 = m0 + wm0;
-          if (fr == 0 && col_ok && row0 < p.M) {
+          if (blk_amax) {
+            // rows past M contribute 0 (cm starts at 0, `ok` excludes them)
+            if (fr == 0) *reinterpret_cast<f32x4*>(cmx + (wm0 / WM) * BN + nl) = (f32x4){cm[0], cm[1], cm[2], cm[3]};
+          } else if (fr == 0 && col_ok && row0 < p.M) {
             float* a = p.amax + (long)(row0 / p.rows_per_sample) * p.N + n;
 #pragma unroll
             for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
@@ -415,6 +430,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
       }
     }
     __syncthreads();
+    if (blk_amax) {
+      for (int c = threadIdx.x; c < BN; c += NT) {
+        float m = cmx[c];
+#pragma unroll
+        for (int w = 1; w < WGM; ++w) m = fmaxf(m, cmx[w * BN + c]);
+        if (n0 + c < p.N && m0 < p.M) atomic_max_pos(p.amax + (long)(m0 / p.rows_per_sample) * p.N + n0 + c, m);
+      }
+    }
     // output tile: BN columns (BN / 2 with GEGLU) starting at n0 (n0 / 2).  GEGLU: weight rows
     // are interleaved in 16-row blocks [hidden 16 | gate 16] (BN % 32 == 0), so output columns
     // 16b + j of the tile read h = tile[32b + j], g = tile[32b + 16 + j]; diffusers GEGLU on the
@@ -526,7 +549,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN, 256, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
+  gemm_epilogue<BM, BN, 256, TM, TN, SPLIT, 2 * (ASZ + BSZ)>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // ---- LDS-DMA variant ----------------------------------------------------------------------
@@ -686,12 +709,12 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 //     MFMA(k, half 1) | read(k+1, half 0)
 //   (the stage written after the barrier held tile k-1, whose last reads precede it).
 constexpr int dma_lds_halves(int bm, int bn, int st, int bkt = 64) {
-  return st * (bm + bn) * bkt > bm * (bn + 8) ? st * (bm + bn) * bkt : bm * (bn + 8);
+  return st * (bm + bn) * bkt > epi_lds_halves(bm, bn) ? st * (bm + bn) * bkt : epi_lds_halves(bm, bn);
 }
 // fp8 stages carry the group-scale row (BN fp32, one 1-KB DMA wave-instruction) after the B tile
 constexpr int F8_SCL = 512;  // halves
 constexpr int dma_lds_halves_f8(int bm, int bn, int st) {
-  return st * ((bm + bn) * 64 + F8_SCL) > bm * (bn + 8) ? st * ((bm + bn) * 64 + F8_SCL) : bm * (bn + 8);
+  return st * ((bm + bn) * 64 + F8_SCL) > epi_lds_halves(bm, bn) ? st * ((bm + bn) * 64 + F8_SCL) : epi_lds_halves(bm, bn);
 }
 // minimum waves per SIMD for __launch_bounds__: (blocks that fit the 160 KB LDS) x waves / 4
 constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt, int bkt = 64) {
@@ -885,7 +908,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
       for (int j = 0; j < TN; ++j) acc[i][j] *= s;
     }
   }
-  gemm_epilogue<BM, BN, NT, TM, TN, SPLIT>(p, acc, smem, m0, n0, wm0, wn0, split);
+  gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // ---- ping-pong GEMM (256 x BN tile, 8 waves, BK 32, 4-stage LDS-DMA ring) ----------------
@@ -1150,7 +1173,7 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
   constexpr int WM = 64, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
   constexpr int HSZ = HALO_ROWS_MAX * BK;  // halves per halo buffer
   constexpr int BSZ = BN * BK;
-  constexpr int LDSZ = 2 * HSZ + 2 * BSZ > BM * (BN + 8) ? 2 * HSZ + 2 * BSZ : BM * (BN + 8);
+  constexpr int LDSZ = 2 * HSZ + 2 * BSZ > epi_lds_halves(BM, BN) ? 2 * HSZ + 2 * BSZ : epi_lds_halves(BM, BN);
   constexpr int HG = HALO_ROWS_MAX / 8;                     // halo wave-instruction groups (max)
   constexpr int HL = (HG + NW - 1) / NW;                    // per wave
   static_assert(HL <= 8, "halo rows must stage within the 8 tap steps of a chunk");
@@ -1256,8 +1279,8 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true>(p, acc, smem, m0, n0, wm0, wn0, split);
-  else gemm_epilogue<BM, BN, NT, TM, TN, false>(p, acc, smem, m0, n0, wm0, wn0, split);
+  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
+  else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // halo kernel applicability: 3x3 / stride 1 / pad 1, 64-channel chunks, whole-row 256-pixel tiles

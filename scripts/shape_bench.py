@@ -1,6 +1,7 @@
 """Per-variant GPU time of the SD1.5 CFG-batch-8 GEMM / conv shapes, launch overhead excluded:
 each (shape, variant) is captured as a HIP graph of `iters` back-to-back calls and replayed.
-usage: python scripts/shape_bench.py [--int8] [--iters 20] [--only conv|linear]"""
+usage: python scripts/shape_bench.py [--int8] [--iters 20] [--only conv|linear] [--amax]
+(--amax: the fp16 convs with the per-(sample, channel) output-amax epilogue of the W8A8 path)"""
 import argparse
 import os
 import sys
@@ -72,6 +73,7 @@ def main():
     ap.add_argument("--int8", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None, choices=["conv", "linear"])
+    ap.add_argument("--amax", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -93,8 +95,9 @@ def main():
                 res = run_variants(lambda: K.conv2d_i8(xq, sa, wq, sw, ci, s, k // 2, bias=b), variants, a.iters)
             else:
                 vs = variants + (list(K.HALO_VARIANTS) if k == 3 and s == 1 else [])
-                res = run_variants(lambda: K.conv2d_nhwc(x, wt, ci, s, k // 2, bias=b), vs, a.iters)
-            print(f"conv ({n},{h},{w},{ci},{co},{k}) x{cnt}: " + fmt(res, flops), flush=True)
+                am = torch.zeros(n * co, dtype=torch.float32, device=dev) if a.amax else None
+                res = run_variants(lambda: K.conv2d_nhwc(x, wt, ci, s, k // 2, bias=b, amax=am), vs, a.iters)
+            print(f"conv ({n},{h},{w},{ci},{co},{k}){' amax' if a.amax else ''} x{cnt}: " + fmt(res, flops), flush=True)
     if a.only != "conv":
         for (m, nn, kk, geglu, cnt) in LINS:
             x = torch.randn(m, kk, generator=g).half().to(dev)
