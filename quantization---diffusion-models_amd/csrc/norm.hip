@@ -411,6 +411,173 @@ __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int ro
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Single-kernel GroupNorm for the small UNet levels (hw <= 256): one block per (sample, set of
+// G groups whose channels form whole 16-B octets) does statistics, coefficients, the output
+// amax and the apply, reading its slice twice (the second time from L2) instead of three
+// stream-ordered launches whose fixed costs dominate there (8x8, 16x16: 17-20 us for a 1-5 MB
+// tensor vs a 3 us copy; at 32x32 the 3-launch path's wider grid wins).  Same arithmetic as k_gn_stats / k_gn_coeff / k_gn_apply
+// (shifted sums, the group's first element as the shift, monotone amax with the scan
+// fallback); only the fp32 summation order of the group sums differs.
+// ---------------------------------------------------------------------------------------
+constexpr int GNF_CW = 128;  // max channels per block (16 octets)
+
+template <int XF, int SILU, bool Q>
+__global__ void __launch_bounds__(256) k_gn_fused(GnIn in, int hw, int c, int cg, int G, float eps,
+                                                  const f16* __restrict__ gamma, const f16* __restrict__ beta,
+                                                  int qmax, f16* __restrict__ y) {
+  __shared__ float4 red[256][8];   // per thread and channel (s1, s2, min, max)
+  __shared__ float4 chs[GNF_CW];   // per channel (S1, S2, min, max) of the block's slice
+  __shared__ float2 gst[16];       // per group (mean, rstd)
+  __shared__ float2 kco[GNF_CW];   // per channel (scale, bias)
+  __shared__ float amx[GNF_CW];
+  __shared__ int flagged[GNF_CW];
+  __shared__ int nflag;
+  __shared__ float fmx[4];
+  const int CW = G * cg, CPP = CW / 8, PS = 256 / CPP;
+  const int t = threadIdx.x;
+  const int o = t % CPP, p0 = t / CPP;
+  const bool active = p0 < PS;
+  const int c0 = blockIdx.x * CW, ch = c0 + o * 8;
+  const long n = blockIdx.y;
+  if (t == 0) nflag = 0;
+
+  GnXf xf;
+  float s1[8], s2[8], sh[8], mn[8], mx[8];
+  if (active) gn_xf_init(in, c, n, ch, xf);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1[j] = s2[j] = 0.f;
+    mn[j] = INFINITY;
+    mx[j] = -INFINITY;
+    sh[j] = active ? gn_load1(in, c, n, n * hw, (ch + j) / cg * cg) : 0.f;
+  }
+  if (active) {
+    for (int rb = p0; rb < hw; rb += 8 * PS) {
+      f16x8 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * PS, hw - 1), ch);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) QD_PIN(v[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (rb + u * PS >= hw) break;
+        const f16x8 w = gn_xf8<XF>(in, v[u], xf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xv = (float)w[j];
+          const float a = xv - sh[j];
+          s1[j] += a;
+          s2[j] = fmaf(a, a, s2[j]);
+          mn[j] = fminf(mn[j], xv);
+          mx[j] = fmaxf(mx[j], xv);
+        }
+      }
+    }
+  }
+  // per-channel totals over the PS threads of each octet: one thread per channel, fixed order
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = make_float4(s1[j], s2[j], mn[j], mx[j]);
+  __syncthreads();
+  if (t < CW) {
+    const int oc = t >> 3, j = t & 7;
+    float4 a = red[oc][j];
+    for (int k = 1; k < PS; ++k) {
+      const float4 v = red[k * CPP + oc][j];
+      a.x += v.x;
+      a.y += v.y;
+      a.z = fminf(a.z, v.z);
+      a.w = fmaxf(a.w, v.w);
+    }
+    chs[t] = a;
+  }
+  __syncthreads();
+  if (t < G) {
+    float S1 = 0.f, S2 = 0.f;
+    for (int j = 0; j < cg; ++j) {
+      S1 += chs[t * cg + j].x;
+      S2 += chs[t * cg + j].y;
+    }
+    const float cnt = (float)cg * (float)hw;
+    const float m = S1 / cnt;
+    const float var = fmaxf(S2 / cnt - m * m, 0.f);
+    gst[t] = make_float2(m + gn_load1(in, c, n, n * hw, c0 + t * cg), 1.0f / sqrtf(var + eps));
+  }
+  __syncthreads();
+  if (t < CW) {
+    const int cc = c0 + t;
+    const float2 st = gst[t / cg];
+    const float sc = st.y * (float)gamma[cc];
+    const float2 k = make_float2(sc, fmaf(-sc, st.x, (float)beta[cc]));
+    kco[t] = k;
+    if (Q) {
+      const float4 e = chs[t];
+      const float lo = fabsf(gn_out(e.z, k, SILU)), hi = fabsf(gn_out(e.w, k, SILU));
+      const float top = fabsf(gn_out(sc >= 0.f ? e.w : e.z, k, SILU));
+      if (!SILU) amx[t] = fmaxf(lo, hi);
+      else if (top >= SILU_NEG_BOUND) amx[t] = top;
+      else flagged[atomicAdd(&nflag, 1)] = t;
+    }
+  }
+  __syncthreads();
+  if (Q) {
+    for (int f = 0; f < nflag; ++f) {  // rare: a full max |out| scan of the channel
+      const int cl = flagged[f];
+      const float2 k = kco[cl];
+      float m = 0.f;
+      for (int r = t; r < hw; r += 256) m = fmaxf(m, fabsf(gn_out(gn_load1(in, c, n, n * hw + r, c0 + cl), k, SILU)));
+      m = wave_max(m);
+      if ((t & 63) == 0) fmx[t >> 6] = m;
+      __syncthreads();
+      if (t == 0) amx[cl] = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));
+      __syncthreads();
+    }
+  }
+  if (!active) return;
+  float2 k[8];
+  float sq[8];
+  double rq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k[j] = kco[o * 8 + j];
+    if (Q) {
+      sq[j] = fq_scale(amx[o * 8 + j], qmax);
+      rq[j] = rcp_exact(sq[j]);
+    }
+  }
+  for (int rb = p0; rb < hw; rb += 4 * PS) {
+    f16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * PS, hw - 1), ch);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + u * PS >= hw) break;
+      const f16x8 w = gn_xf8<XF>(in, v[u], xf);
+      f16x8 out;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float val = gn_out((float)w[j], k[j], SILU);
+        if constexpr (Q) out[j] = fq_apply_r(val, sq[j], rq[j]);
+        else out[j] = (f16)val;
+      }
+      *reinterpret_cast<f16x8*>(y + (n * hw + rb + u * PS) * c + ch) = out;
+    }
+  }
+}
+
+// groups per fused block: the fewest whole groups spanning whole octets (0: not fused)
+static int gn_fused_groups(int n, int hw, int c, int groups) {
+  if (hw > 256 || getenv("QD_GN_UNFUSED")) return 0;
+  const int cg = c / groups;
+  for (int G = 1; G <= 16 && G * cg <= GNF_CW; ++G) {
+    if (groups % G || (G * cg) % 8) continue;
+    return G;
+  }
+  return 0;
+}
+
 extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
   const GnGeom g = gn_geom(n, hw, c);
   return 4 * n * g.zs * c + 2 * n * c + n * c + n * c;  // partials (float4), coef (float2), amax, spare
@@ -435,6 +602,25 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   float* amax_n = y8 ? amax + (long)n * c : nullptr;  // per-(n, group) maxima in the spare n * c floats
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
   const bool xf = in.qmax > 0 || in.cadd;
+  if (const int G = y8 ? 0 : gn_fused_groups(n, hw, c, groups)) {
+    const dim3 gf(groups / G, n);
+#define QD_GN_FUSED(XFV, SV, QV)                                                                               \
+  k_gn_fused<XFV, SV, QV><<<gf, 256, 0, st>>>(in, hw, c, cg, G, eps, (const f16*)gamma, (const f16*)beta, qmax, \
+                                              (f16*)y)
+    switch ((xf ? 4 : 0) | (silu ? 2 : 0) | (qmax > 0 ? 1 : 0)) {
+      case 0: QD_GN_FUSED(0, 0, false); break;
+      case 1: QD_GN_FUSED(0, 0, true); break;
+      case 2: QD_GN_FUSED(0, 1, false); break;
+      case 3: QD_GN_FUSED(0, 1, true); break;
+      case 4: QD_GN_FUSED(1, 0, false); break;
+      case 5: QD_GN_FUSED(1, 0, true); break;
+      case 6: QD_GN_FUSED(1, 1, false); break;
+      default: QD_GN_FUSED(1, 1, true); break;
+    }
+#undef QD_GN_FUSED
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
   const dim3 gs(g.gx, n, g.zs), bs(g.bx, g.bys);
   if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
   else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
