@@ -1165,6 +1165,9 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
 // Halo chunk c+1 is staged under chunk c's taps, 1/8 of its rows per tap step; weight tiles are
 // double-buffered one tap ahead.  Summation order over K differs from the tap-major kernels
 // (chunk-major), so its outputs may differ from theirs in the last fp16 bit.
+#ifndef QD_HALO_ABL  // diagnostic builds only (scripts/halo_ablate.sh): 1 no MFMA, 2 no weight DMA in the
+#define QD_HALO_ABL 0  // K loop, 4 no halo DMA in the K loop, 8 no barrier / wait (results are garbage)
+#endif
 constexpr int HALO_ROWS_MAX = 400;  // (RB + 2) * (W + 2) <= 396 for W in {16, 32, 64}
 
 template <int BN>
@@ -1252,12 +1255,16 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
   for (int s = 0; s < nsteps; ++s) {
     const int cl = s / 9, t = s - cl * 9;
     // own loads of weight tile s landed (halo rows issued after it in step s-1 may stay in flight)
-    wait_vm_rt(t >= 1 && cl + 1 < c_end - c_beg ? halo_cnt(t - 1) : 0);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (s + 1 < nsteps) b_issue(s + 1, bring + ((s + 1) & 1) * BSZ);
-    if (t < 8 && cl + 1 < c_end - c_beg) halo_issue(t, c_beg + cl + 1, halo0 + ((cl + 1) & 1) * HSZ);
+    if (!(QD_HALO_ABL & 8)) {
+      wait_vm_rt(t >= 1 && cl + 1 < c_end - c_beg ? halo_cnt(t - 1) : 0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (!(QD_HALO_ABL & 2))
+      if (s + 1 < nsteps) b_issue(s + 1, bring + ((s + 1) & 1) * BSZ);
+    if (!(QD_HALO_ABL & 4))
+      if (t < 8 && cl + 1 < c_end - c_beg) halo_issue(t, c_beg + cl + 1, halo0 + ((cl + 1) & 1) * HSZ);
     const f16* hb = halo0 + (cl & 1) * HSZ;
     const f16* Bs = bring + (s & 1) * BSZ;
     const int ky = t / 3, kx = t - ky * 3;
@@ -1269,11 +1276,185 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
       for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(hb + swz(hr0[i] + tap, ks * 4 + fq));
 #pragma unroll
       for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz(wn0 + j * 16 + fr, ks * 4 + fq));
+      if (QD_HALO_ABL & 1) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bf[j]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
+  else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
+}
+
+// ---- split-phase halo conv (variants 202 / 203) -------------------------------------------
+// The halo conv's tile and K order with its LDS reads taken off the MFMAs' critical path.
+// Ablation of the lock-step kernel (64x64 320->320, scripts/halo_ablate.py): 66.5 us; without
+// MFMAs 42.3; without DMA and barriers (LDS reads + MFMAs only) still 56.1; reads alone 26.5 -
+// the fragment reads and the MFMAs serialise (every wave reads its fragments right after the
+// step's barrier and waits for them).  Here the barrier sits between the two 32-deep halves of a
+// tap step and each half's fragments are read under the other half's MFMAs:
+//   read(s, half 1) | MFMA(s, half 0) -> wait(tile s+1 [+ next chunk's halo]) -> barrier ->
+//   issue tile s+2 (into the slot of s-1) + a halo row group -> read(s+1, half 0) | MFMA(s, half 1)
+// which needs a 3-deep weight ring (halo double buffer 100 KB + 3 x 20 KB = the whole 160 KB).
+// The 9 taps of a chunk are unrolled, so the ring slot (step % 3 == tap % 3) and the tap's
+// halo offset are compile-time constants (immediate ds_read offsets, few address VALU ops).
+// Hazards: tile s+1 is waited for (own vmcnt) before barrier s and read after it; tile s+2
+// overwrites the slot of s-1, whose last reads fed MFMA(s-1, half 1) before barrier s; halo rows
+// of chunk c+1 go into chunk c-1's buffer after barrier (c, tap 0), after the last reads of chunk
+// c-1 (MFMA(c-1, tap 8, half 1)).  Same K order as the lock-step kernel: identical bits.
+template <int BN>
+__global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
+  constexpr int BM = 256, NT = 512, NW = 8, WGN = 2;
+  constexpr int WM = 64, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  constexpr int HSZ = HALO_ROWS_MAX * BK;
+  constexpr int BSZ = BN * BK;
+  constexpr int LDSZ = 2 * HSZ + 3 * BSZ > epi_lds_halves(BM, BN) ? 2 * HSZ + 3 * BSZ : epi_lds_halves(BM, BN);
+  static_assert(LDSZ * 2 <= 163840, "halo + weight ring exceed the 160 KB of LDS");
+  constexpr int HG = HALO_ROWS_MAX / 8;
+  constexpr int HL = (HG + NW - 1) / NW;
+  static_assert(HL <= 8, "halo rows must stage within the 8 tap steps of a chunk");
+  using BL = BDma<BN, NT, 64>;
+  __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
+  f16* const halo0 = smem;
+  f16* const bring = smem + 2 * HSZ;
+
+  const int W = p.W, RB = BM / W, W2 = W + 2;
+  const int hrows = (RB + 2) * W2;
+  const int nbm = p.M / BM, nbn = p.N / BN;
+  const int ntile = nbm * nbn, nwg = ntile * p.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = wg / p.splits, split = wg - tile * p.splits;
+  const int bm = tile / nbn, bn = tile - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int img = m0 / (p.Ho * p.Wo), oh0 = (m0 - img * p.Ho * p.Wo) / W;
+  const int c_beg = split * p.kps, nch = p.kps;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t ars = rsrc(p.a, p.a_bytes);
+  const int gc = ((lane & 7) ^ (lane >> 3)) * 8;
+  unsigned hoff[HL];
+#pragma unroll
+  for (int j = 0; j < HL; ++j) {
+    const int hr = (j * NW + wid) * 8 + (lane >> 3);
+    const int hy = hr / W2, hx = hr - hy * W2;
+    const int ih = oh0 - 1 + hy, iw = hx - 1;
+    const bool ok = hr < hrows && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    const int sh = p.ups ? ih >> 1 : ih, sw = p.ups ? iw >> 1 : iw;
+    hoff[j] = ok ? (unsigned)(((img * p.Hs + sh) * p.Ws + sw) * p.Cip + gc) * 2u : OOB;
+  }
+  const int hgroups = (hrows + 7) / 8;
+  BL bl;
+  bl.init(p, n0, wid);
+  const int bcnt = BL::count(wid);
+  // the tap offset in halo rows depends on the runtime image width: ky * W2 + kx
+  int hr0[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm0 + i * 16 + fr;
+    const int r = ml / W, x = ml - r * W;
+    hr0[i] = r * W2 + x;
+  }
+  // B fragment offsets (halves) within a ring slot, per half
+  int bofs[2][TN];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bofs[ks][j] = swz(wn0 + j * 16 + fr, ks * 4 + fq);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = nch * 9;
+  // prologue: chunk 0's halo, weight tiles 0 and 1; wait for the halo and tile 0
+#pragma unroll
+  for (int j = 0; j < HL; ++j)
+    if (j * NW + wid < hgroups) glds16(ars, halo0 + (j * NW + wid) * 8 * BK, hoff[j] + (unsigned)(c_beg * BK * 2));
+  bl.issue(p, c_beg * BK, bring, wid);
+  if (nsteps > 1) bl.issue(p, p.Cip + c_beg * BK, bring + BSZ, wid);
+  wait_vm_rt(nsteps > 1 ? bcnt : 0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  f16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+  // fragment reads in the order the next half's MFMAs (i-major) consume them: A0, B0..B4, A1..A3
+  auto read_a1 = [&](const f16* hb, int tap, int ks, int i, f16x8& af) {
+    int h = hr0[i];
+    asm volatile("" : "+v"(h));  // keep the per-tap address math here (hoisted: 72 VGPRs, spills)
+    af = *reinterpret_cast<const f16x8*>(hb + swz(h + tap, ks * 4 + fq));
+  };
+  auto read_frags = [&](const f16* hb, int tap, int slot, int ks, f16x8 (&af)[TM], f16x8 (&bf)[TN]) {
+    read_a1(hb, tap, ks, 0, af[0]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(bring + slot * BSZ + bofs[ks][j]);
+#pragma unroll
+    for (int i = 1; i < TM; ++i) read_a1(hb, tap, ks, i, af[i]);
+  };
+  auto mfmas = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+  };
+  // one fragment read per two MFMAs: the reads of the next half go out under this half's MFMAs
+  // (left to itself the scheduler clusters them and waits for them right before their use)
+  auto interleave = [&]() {
+#pragma unroll
+    for (int k = 0; k < TM + TN; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - 2 * (TM + TN), 0);
+  };
+  read_frags(halo0, 0, 0, 0, a0, b0);
+#pragma nounroll
+  for (int cl = 0; cl < nch; ++cl) {
+    const f16* hb = halo0 + (cl & 1) * HSZ;
+    f16* const hnext = halo0 + ((cl + 1) & 1) * HSZ;
+    const bool more = cl + 1 < nch;
+    const int s0 = cl * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t % 3;
+      read_frags(hb, ky * W2 + kx, t % 3, 1, a1, b1);
+      mfmas(a0, b0);
+      interleave();
+      if (t < 8 || more) {
+        // own loads of tile s+1 landed (issued in the middle of step s-1, followed only by
+        // that step's halo row group); at a chunk's last tap also the next chunk's halo
+        wait_vm_rt(t >= 1 && t <= 8 && t - 1 < HL && more && (t - 1) * NW + wid < hgroups && t < 8 ? 1 : 0);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const int s2 = s0 + t + 2;  // weight tile s + 2: tap (t + 2) % 9 of chunk cl + (t + 2) / 9
+        if (s2 < nsteps) bl.issue(p, ((t + 2) % 9) * p.Cip + (c_beg + cl + (t + 2) / 9) * BK, bring + ((t + 2) % 3) * BSZ, wid);
+        if (t < HL && more && t * NW + wid < hgroups)
+          glds16(ars, hnext + (t * NW + wid) * 8 * BK, hoff[t] + (unsigned)((c_beg + cl + 1) * BK * 2));
+        if (t < 8) read_frags(hb, ((t + 1) / 3) * W2 + (t + 1) % 3, (t + 1) % 3, 0, a0, b0);
+        else read_frags(hnext, 0, 0, 0, a0, b0);
+      }
+      mfmas(a1, b1);
+      interleave();
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1418,10 +1599,9 @@ static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register
 
 extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
-                 (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || variant == 200 ||
-                 variant == 201 || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123) ||
+                 (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (variant >= 200 && variant <= 203) || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123) ||
                  (variant >= 130 && variant <= 134),
-             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200/201 halo conv, "
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200-203 halo conv, "
              "300-304 ping-pong (int8: 130-134)");
   g_force = variant;
   return 0;
@@ -1457,13 +1637,14 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       }
     }
   }
-  if ((g_force == 200 || g_force == 201) && !quant_w && !geglu && K % 576 == 0) {
-    // halo conv (applicability is checked at launch; the split only needs the chunk count)
-    const int bn = g_force == 200 ? 160 : 128;
+  if (g_force >= 200 && g_force <= 203 && !quant_w && !geglu && K % 576 == 0) {
+    // halo conv (applicability is checked at launch; the split only needs the chunk count):
+    // 200 / 201 BN 160 / 128 lock-step, 202 / 203 the same tiles split-phase
+    const int bn = (g_force & 1) ? 128 : 160;
     if (N % bn == 0 && M % 256 == 0) {
       const long tiles_mn = (long)(M / 256) * (N / bn);
       const int nc = K / 576;
-      best = {2, 256, bn, 0, 1, nc};
+      best = {2, 256, bn, g_force >= 202 ? 1 : 0, 1, nc};
       for (int sp = 2; sp <= nc; ++sp) {
         if (nc % sp != 0) continue;
         if (tiles_mn * sp > 256) break;
@@ -1556,8 +1737,13 @@ static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t 
     else k_gemm_pp<128, 4, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
   } else if (pl.kind == 2) {
     const int nwg = (p.M / 256) * (p.N / pl.bn) * p.splits;
-    if (pl.bn == 160) k_conv_halo<160><<<nwg, 512, 0, st>>>(p);
-    else k_conv_halo<128><<<nwg, 512, 0, st>>>(p);
+    if (pl.var == 1) {
+      if (pl.bn == 160) k_conv_halo2<160><<<nwg, 512, 0, st>>>(p);
+      else k_conv_halo2<128><<<nwg, 512, 0, st>>>(p);
+    } else {
+      if (pl.bn == 160) k_conv_halo<160><<<nwg, 512, 0, st>>>(p);
+      else k_conv_halo<128><<<nwg, 512, 0, st>>>(p);
+    }
   } else if (pl.kind == 1) launch_dma<AMODE, SPLIT>(p, pl.var, st);
   else if (pl.bm == 128 && pl.bn == 160) launch_fmt<128, 160, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128 && pl.bn == 128) launch_fmt<128, 128, AMODE, SPLIT>(p, fmt, st);

@@ -166,7 +166,7 @@ def conv_weight_khwc(w, ci_pad):
 REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
 DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 114, 115,   # LDS-DMA variants (fp16 weights)
                 300, 301, 302, 303, 304)                        # ping-pong 256-row
-HALO_VARIANTS = (200, 201)  # 3x3 conv with the activation halo staged once per channel chunk
+HALO_VARIANTS = (200, 201, 202, 203)  # 3x3 conv with the activation halo staged once per channel chunk
 _TUNE = {}
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
 _OVERRIDE = None  # benchmarking: force every GEMM onto one qd_gemm_force id (see force_gemm)

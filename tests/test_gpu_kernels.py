@@ -407,7 +407,7 @@ def forced_gemm():
     kernels.force_gemm(None)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 116)) + [200, 201, 300, 301, 302, 303, 304])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 116)) + [200, 201, 202, 203, 300, 301, 302, 303, 304])
 def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     """Every kernel family / tile (register-staged and LDS-DMA) on ragged shapes: rows past M,
     conv halo, stride 2, fused 2x upsample, the 4-channel conv_in (any-Ci decode), K tails,
@@ -505,7 +505,7 @@ def test_fast_reciprocal_fake_quant_is_exact(dev):
     assert counts.tolist() == [0, 0]
 
 
-@pytest.mark.parametrize("variant", [200, 201])
+@pytest.mark.parametrize("variant", [200, 201, 202, 203])
 def test_conv_halo_kernel(variant, forced_gemm, dev):
     """Halo-staged 3x3 conv: 16/32/64-wide images, fused 2x upsample, split-K over channel
     chunks (ragged 64-channel chunk counts), bias + amax + residual epilogues."""
@@ -535,6 +535,28 @@ def test_conv_halo_kernel(variant, forced_gemm, dev):
             assert_fp16_close(got, pre, ulps=2.0, atol=1e-3)
         # amax is of the pre-residual output (the conv output the reference fake-quantizes)
         assert torch.allclose(amax.view(n, cout).cpu(), pre.abs().amax(dim=(2, 3)), rtol=2e-3, atol=1e-3)
+
+
+def test_conv_halo_split_phase_bit_identical(forced_gemm, dev):
+    """The split-phase halo conv (202 / 203) changes only when tiles are loaded and read, not the K
+    order: its outputs equal the lock-step halo kernel's (200 / 201) bit for bit, on the SD1.5 64x64 shape at
+    full width (every pipeline position of a 5-chunk, 45-step K loop) and a split-K shape."""
+    k = K()
+    g = torch.Generator().manual_seed(31)
+    for n, hw, cin, cout in ((8, 64, 320, 320), (2, 16, 1280, 1280), (2, 32, 640, 640)):
+        x = torch.randn(n, hw, hw, cin, generator=g).half().to(dev)
+        wk = (torch.randn(cout, 3, 3, cin, generator=g) / (cin * 9) ** 0.5).half().to(dev)
+        b = torch.randn(cout, generator=g).half().to(dev)
+        for vs in ((200, 202), (201, 203)):
+            outs = []
+            for v in vs:
+                forced_gemm(v)
+                amax = torch.empty(n * cout, dtype=torch.float32, device=dev)
+                y = k.conv2d_nhwc(x, wk, cin, 1, 1, False, bias=b, amax=amax)
+                outs.append((y, amax))
+            for o, v in zip(outs[1:], vs[1:]):
+                assert torch.equal(outs[0][0], o[0]), (n, hw, cin, cout, v)
+                assert torch.equal(outs[0][1], o[1]), (n, hw, cin, cout, v)
 
 
 @pytest.mark.parametrize("variant", [-1, 0, 100, 106, 300, 301, 303])
