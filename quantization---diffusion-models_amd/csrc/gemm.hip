@@ -1411,6 +1411,13 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
     for (int i = 1; i < TM; ++i) read_a1(hb, tap, ks, i, af[i]);
   };
   auto mfmas = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
+    if (QD_HALO_ABL & 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bf[j]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1442,13 +1449,15 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
       if (t < 8 || more) {
         // own loads of tile s+1 landed (issued in the middle of step s-1, followed only by
         // that step's halo row group); at a chunk's last tap also the next chunk's halo
-        wait_vm_rt(t >= 1 && t <= 8 && t - 1 < HL && more && (t - 1) * NW + wid < hgroups && t < 8 ? 1 : 0);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+        if (!(QD_HALO_ABL & 8)) {
+          wait_vm_rt(t >= 1 && t < 8 && t - 1 < HL && more && (t - 1) * NW + wid < hgroups ? 1 : 0);
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
         const int s2 = s0 + t + 2;  // weight tile s + 2: tap (t + 2) % 9 of chunk cl + (t + 2) / 9
-        if (s2 < nsteps) bl.issue(p, ((t + 2) % 9) * p.Cip + (c_beg + cl + (t + 2) / 9) * BK, bring + ((t + 2) % 3) * BSZ, wid);
-        if (t < HL && more && t * NW + wid < hgroups)
+        if (!(QD_HALO_ABL & 2) && s2 < nsteps) bl.issue(p, ((t + 2) % 9) * p.Cip + (c_beg + cl + (t + 2) / 9) * BK, bring + ((t + 2) % 3) * BSZ, wid);
+        if (!(QD_HALO_ABL & 4) && t < HL && more && t * NW + wid < hgroups)
           glds16(ars, hnext + (t * NW + wid) * 8 * BK, hoff[t] + (unsigned)((c_beg + cl + 1) * BK * 2));
         if (t < 8) read_frags(hb, ((t + 1) / 3) * W2 + (t + 1) % 3, (t + 1) % 3, 0, a0, b0);
         else read_frags(hnext, 0, 0, 0, a0, b0);
