@@ -153,7 +153,7 @@ class AwqQuantizer:
                                              n_bits_A=self.a_bit, group_size_W=self.group_size,
                                              codeBookQuantInd=self.codeBookQuantInd,
                                              int8_mfma=i8 and layer.in_features % 64 == 0,
-                                             fp8_act=self.fp8_act)
+                                             fp8_act=getattr(self, "fp8_act", False))
                 setattr(parent, name, fake)
             elif isinstance(layer, nn.Conv2d):
                 fake = WxAxConv2d.from_float(layer, weight_quant=self.weight_quant_conv_type,
