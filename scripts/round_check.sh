@@ -2,7 +2,7 @@
 # (test failures (pytest rc 1) are recorded and the check goes on; a crash, abort or time limit ends it)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/rc_tests.log 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf > gpurun_out/rc_tests.log 2>&1
 rc=$?
 echo "[rc] tests rc=$rc"
 [ $rc -le 1 ] || exit $rc
