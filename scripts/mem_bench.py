@@ -27,8 +27,10 @@ for (n, h, w, c) in ((8, 64, 64, 320), (8, 32, 32, 640), (8, 16, 16, 1280)):
         ("layernorm", lambda: K.layernorm(x.view(-1, c), 1e-5, gam, bet, out=y.view(-1, c)), 2),
         ("groupnorm+silu+fq", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8, out=y), 3),
         ("groupnorm", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, out=y), 3),
+        ("gn+silu+fq fq_in", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8, out=y,
+                                                    fq_in=(amax, 8, None)), 3),
     ]
     print(f"[{n},{h},{w},{c}] {mb:.1f} MB per tensor")
     for name, fn, passes in rows:
         us = graph_time(fn, 20)
-        print(f"  {name:20s} {us:7.1f} us  {passes * mb / us / 1e3:5.2f} TB/s ({passes} tensor passes)", flush=True)
+        print(f"  {name:20s} {us:7.1f} us  {passes * mb / us:5.2f} TB/s ({passes} tensor passes)", flush=True)

@@ -295,7 +295,9 @@ def test_groupnorm_i8_equals_quantized_groupnorm(dev, silu, concat, fq):
     """GroupNorm(+SiLU) with fused int8 output == per-sample codes of the fp16 GroupNorm output."""
     k = K()
     g = torch.Generator().manual_seed(5)
-    n, h, w, c1, c2 = 2, 16, 16, 320, 320 if concat else 0
+    # 32x32: the streaming (stats -> apply) path, which the int8 output always takes (the fp16
+    # output of hw <= 256 runs the single-kernel GroupNorm, whose group sums add in another order)
+    n, h, w, c1, c2 = 2, 32, 32, 320, 320 if concat else 0
     x = (torch.randn(n, h, w, c1, generator=g) * 3).half().to(dev)
     x2 = (torch.randn(n, h, w, c2, generator=g)).half().to(dev) if concat else None
     c = c1 + c2

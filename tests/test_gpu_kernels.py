@@ -322,6 +322,38 @@ def test_groupnorm_fused(c, hw, silu, q, dev):
         assert_fp16_close(got, ref, ulps=2.0, atol=2e-3)
 
 
+@pytest.mark.parametrize("c,hw,silu,q", [(320, 4096, True, 8), (640, 1024, True, 8), (960, 1024, False, 8),
+                                         (1280, 1024, True, 8), (640, 4096, True, 0)])
+def test_groupnorm_streaming_path(c, hw, silu, q, dev):
+    """hw > 256: the two streaming passes (statistics -> coefficients -> apply) against torch,
+    with channels whose tiny gamma / negative beta keep the SiLU output below the extremes
+    bound (the fallback amax scan)."""
+    k = K()
+    g = torch.Generator().manual_seed(c + hw + q)
+    n = 2
+    x = (torch.randn(n, c, hw, generator=g) * 2 + 0.5).half()
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
+    bet = (0.1 * torch.randn(c, generator=g)).half()
+    gam[::37] = 0.01
+    bet[::37] = -0.5
+    xh = x.transpose(1, 2).contiguous().to(dev)
+    ref = F.group_norm(x.view(n, c, hw, 1), 32, gam, bet, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    if q:
+        ref = FT.per_channel(ref, q)
+    y = k.groupnorm_nhwc(xh, 32, 1e-5, gam.to(dev), bet.to(dev), silu=silu, q_bits=q)
+    assert torch.equal(y, k.groupnorm_nhwc(xh, 32, 1e-5, gam.to(dev), bet.to(dev), silu=silu, q_bits=q))
+    got = y.cpu().transpose(1, 2).reshape(n, c, hw, 1)
+    if q:
+        step = ref.float().abs().amax(dim=(2, 3), keepdim=True) / (2 ** (q - 1) - 1)
+        err = (got.float() - ref.float()).abs()
+        assert (err <= step * 1.01 + 1e-3).all()
+        assert (err <= 1e-3).float().mean() > 0.995
+    else:
+        assert_fp16_close(got, ref, ulps=2.0, atol=2e-3)
+
+
 def test_groupnorm_two_sources(dev):
     k = K()
     g = torch.Generator().manual_seed(5)
@@ -453,14 +485,15 @@ def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     assert ((fused - ref).abs() <= tol).all(), (variant, (fused - ref).abs().max().item())
 
 
-@pytest.mark.parametrize("bits,with_cadd", [(8, True), (0, True), (8, False), (4, True)])
-def test_groupnorm_fq_in_matches_finalize_then_norm(bits, with_cadd, dev):
+@pytest.mark.parametrize("bits,with_cadd,hw", [(8, True, 256), (0, True, 256), (8, False, 256), (4, True, 256),
+                                               (8, True, 1024), (0, False, 1024)])
+def test_groupnorm_fq_in_matches_finalize_then_norm(bits, with_cadd, hw, dev):
     """GroupNorm on a raw conv output with the output quant + temb add applied on the fly equals
     fq_finalize followed by GroupNorm, bit for bit; includes channels whose SiLU output stays
     below the extremes bound (tiny gamma, negative beta) so the fallback amax scan runs."""
     k = K()
-    g = torch.Generator().manual_seed(bits * 3 + with_cadd)
-    n, hw, c = 2, 256, 640
+    g = torch.Generator().manual_seed(bits * 3 + with_cadd + hw)
+    n, c = 2, 640
     y = (torch.randn(n, hw, c, generator=g) * 1.5).half().to(dev)
     amax = y.float().abs().amax(dim=1).reshape(-1).contiguous() if bits else None
     big = (torch.randn(n, 2 * c, generator=g) * 0.3).half().to(dev)
