@@ -105,6 +105,10 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 #define QD_EPI_GELU_TANH 32  /* out = half(gelu_tanh(half(y + bias))): diffusers GELU(approximate="tanh")
                                 (SD3 FeedForward net.0) applied to the rounded projection output;
                                 no residual / amax / GEGLU with it */
+#define QD_EPI_AMAX_POST 64  /* with QD_EPI_AMAX | QD_EPI_RESIDUAL: the amax is of the FINAL output
+                                half(half(y + bias) + residual) - the per-(sample, channel) input amax
+                                of the quantized conv that consumes it (fake_quant.py:125 reduction),
+                                so no separate column-max pass; never split-K or ping-pong tiles */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.

@@ -385,6 +385,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
     const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
     const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+    // post-residual amax: the residual is added to the fragments (8-B loads per lane) before the
+    // column maxes, and the coalesced pass below stores the tile as it stands
+    const bool post = has_res && do_amax && (p.epi & QD_EPI_AMAX_POST) && !geglu && !gtanh;
     // amax: the WGM wave rows of the block combine their column maxes in LDS first when the
     // block's rows lie in one sample, so each (sample, column) address takes one atomic per
     // block instead of one per wave row (same-line atomic chains bound this epilogue)
@@ -407,10 +410,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           const bool ok = m0 + ml < p.M && col_ok;
           f16x4 h;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
-            if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+          for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
+          if (post && ok) {
+            const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)(m0 + ml) * p.ldy + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
           }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
         }
         if (do_amax && !geglu) {
@@ -456,7 +464,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           const f16x8 hv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc);
           const f16x8 gv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc + 16);
 #pragma unroll
-          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)hv[r] * (float)(f16)gelu_f((float)gv[r]));
+          for (int r = 0; r < 8; r += 2) {
+            const f32x2 gg = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+            v[r] = (f16)((float)hv[r] * (float)(f16)gg.x);
+            v[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)gg.y);
+          }
         } else {
           v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
           if (gtanh) {
@@ -464,7 +476,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
             for (int r = 0; r < 8; ++r) v[r] = (f16)gelu_tanh_f((float)v[r]);
           }
         }
-        if (has_res) {
+        if (has_res && !post) {
           const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
@@ -1134,7 +1146,11 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
           const f16x8 hv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc);
           const f16x8 gv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc + 16);
 #pragma unroll
-          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)hv[r] * (float)(f16)gelu_f((float)gv[r]));
+          for (int r = 0; r < 8; r += 2) {
+            const f32x2 gg = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+            v[r] = (f16)((float)hv[r] * (float)(f16)gg.x);
+            v[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)gg.y);
+          }
         } else {
           v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
           if (gtanh) {
@@ -1619,7 +1635,8 @@ extern "C" int qd_gemm_force(int variant) {
 // Cost model (seconds): a CU runs ~4 TFLOP/s of this kernel with 2 resident blocks, ~3 with
 // one; tile efficiency eff; a launch takes ceil(blocks / 512) rounds of 2 blocks per CU.
 // Splits add the fp32 slab round trip (~5 TB/s) and one reduction launch.
-static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bool amax, bool geglu = false) {
+static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bool amax, bool geglu = false,
+                      bool post = false) {
   struct T {
     int bm, bn;
     double eff;
@@ -1635,7 +1652,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
     const long tiles_mn = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
     for (int s = 1; s <= 32; ++s) {
       // split K into s equal runs of whole 64-deep steps, each >= 8 steps
-      if (s > 1 && (K % 64 != 0 || (K / 64) % s != 0 || K / s < 512 || geglu)) continue;
+      if (s > 1 && (K % 64 != 0 || (K / 64) % s != 0 || K / s < 512 || geglu || post)) continue;
       const long blocks = tiles_mn * s;
       const double blk = 2.0 * t.bm * t.bn * ((double)K / s) / t.eff;  // flop of one block
       double tm = blocks <= 256 ? blk / 3e12 : (double)((blocks + 511) / 512) * 2.0 * blk / 4e12;
@@ -1661,7 +1678,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         best.kps = nc / sp;
       }
     }
-  } else if (g_force >= 300 && g_force <= 304 && !quant_w) {
+  } else if (g_force >= 300 && g_force <= 304 && !quant_w && !post) {  // (own epilogue: no post-residual amax)
     // ping-pong 256 x {256, 320, 192} tiles (2x4 waves, wave rows 128) and 256 x {160, 128}
     // (4x2 waves, wave rows 64); amax needs whole-sample wave tiles
     static const int kBn[] = {256, 320, 192, 160, 128};
@@ -1685,7 +1702,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
       const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
       const int per_cu = std::max(1, std::min(by_lds, by_waves));
-      for (int sp = 2; sp <= 32 && !geglu && K % 64 == 0; ++sp) {
+      for (int sp = 2; sp <= 32 && !geglu && !post && K % 64 == 0; ++sp) {
         if ((K / 64) % sp != 0 || K / sp < 512) continue;
         if (tiles_mn * sp > 256L * per_cu) break;
         best.splits = sp;
@@ -1949,13 +1966,14 @@ static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 
 
 template <int AMODE>
 static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t st) {
+  const bool post = (p.epi & QD_EPI_AMAX_POST) != 0;
   Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
-                      (p.epi & QD_EPI_GEGLU) != 0);
+                      (p.epi & QD_EPI_GEGLU) != 0, post);
   if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn))) {  // halo conv not applicable
     const int f = g_force;
     g_force = -1;
     pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
-                   (p.epi & QD_EPI_GEGLU) != 0);
+                   (p.epi & QD_EPI_GEGLU) != 0, post);
     g_force = f;
   }
   if (pl.kind == 2 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N)) && pl.splits > 1) {
@@ -2002,6 +2020,9 @@ static int check_common(const GemmArgs& p, int fmt) {
              "GEGLU epilogue: N % 32 == 0, no residual / amax");
   QD_REQUIRE(!(p.epi & QD_EPI_GELU_TANH) || !(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL | QD_EPI_GEGLU)),
              "GELU-tanh epilogue: no residual / amax / GEGLU");
+  QD_REQUIRE(!(p.epi & QD_EPI_AMAX_POST) || ((p.epi & QD_EPI_AMAX) && (p.epi & QD_EPI_RESIDUAL) &&
+                                             !(p.epi & (QD_EPI_GEGLU | QD_EPI_GELU_TANH))),
+             "post-residual amax needs QD_EPI_AMAX | QD_EPI_RESIDUAL, no GEGLU / GELU-tanh");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
@@ -2012,7 +2033,7 @@ static int check_common(const GemmArgs& p, int fmt) {
 
 extern "C" long qd_gemm_workspace(int M, int N, int K, int wfmt, int rows_per_sample, int epi) {
   const Plan pl = plan_gemm(M, N, K, wfmt != QD_WFMT_F16, rows_per_sample, (epi & QD_EPI_AMAX) != 0,
-                            (epi & QD_EPI_GEGLU) != 0);
+                            (epi & QD_EPI_GEGLU) != 0, (epi & QD_EPI_AMAX_POST) != 0);
   return split_ws_elems(pl, M, N);
 }
 
@@ -2223,6 +2244,9 @@ static int check_i8(const GemmArgs& p) {
              "GEGLU epilogue: N % 32 == 0, no residual / amax");
   QD_REQUIRE(!(p.epi & QD_EPI_GELU_TANH) || !(p.epi & (QD_EPI_AMAX | QD_EPI_RESIDUAL | QD_EPI_GEGLU)),
              "GELU-tanh epilogue: no residual / amax / GEGLU");
+  QD_REQUIRE(!(p.epi & QD_EPI_AMAX_POST) || ((p.epi & QD_EPI_AMAX) && (p.epi & QD_EPI_RESIDUAL) &&
+                                             !(p.epi & (QD_EPI_GEGLU | QD_EPI_GELU_TANH))),
+             "post-residual amax needs QD_EPI_AMAX | QD_EPI_RESIDUAL, no GEGLU / GELU-tanh");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");

@@ -21,6 +21,7 @@ EPI_BIAS, EPI_RESIDUAL, EPI_AMAX = 1, 2, 4
 EPI_AMAX_ZEROED = 16
 EPI_GEGLU = 8
 EPI_GELU_TANH = 32
+EPI_AMAX_POST = 64
 GRAN_ZEROED = 0x100
 
 
@@ -283,11 +284,14 @@ def _cands(ops):
 
 
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
-           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None, gelu_tanh=False):
+           amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None, gelu_tanh=False,
+           amax_post=False):
     """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K).
     geglu: W rows (and bias) interleaved in 16-row [hidden | gate] blocks (geglu_interleave);
     returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue).
     gelu_tanh: returns half(gelu_tanh(half(x . W^T + b))) (SD3 FeedForward GELU(approximate="tanh")).
+    amax_post (with amax and residual): the per-(sample, column) amax is of the final output
+    half(y + residual) - the input amax of the quantized conv that consumes it.
     weight_f16: the same weight's fp16 dequantized buffer (bit-identical to dequantizing the
     codes); when given, the kernel search also considers the fp16 LDS-DMA family."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
@@ -300,7 +304,8 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
         out = _empty((M, N // 2 if geglu else N), torch.float16, x2d.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
-          (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0)
+          (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0) | \
+          (EPI_AMAX_POST if amax_post and amax is not None and residual is not None else 0)
     if residual is not None:
         _chk(residual, "residual")
     ops = [(weight, wfmt, scales, group)]

@@ -21,6 +21,7 @@ implements the forward itself, MI355X-first:
 Architecture restated from diffusers' published UNet2DConditionModel (parity of the third-party
 architecture is UNPINNED: diffusers is not installed; see DESIGN.md and oracle/unet_ref.py).
 """
+import os
 from dataclasses import dataclass, field
 from typing import Optional, Sequence, Tuple, Union
 
@@ -421,9 +422,10 @@ def _conv_weight(layer, co_pad=None):
 
 
 def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=False, c_valid=0, co_pad=None,
-             defer=False):
+             defer=False, in_amax=None):
     """NHWC conv of an nn.Conv2d or WxAxConv2d with the reference's act fake-quant semantics:
     q_x = act_quant(x) -> y = conv(q_x) + b -> q_y = act_quant(y) -> [+ residual | + temb].
+    in_amax: x's per-(n, c) amax, already reduced by its producer (the GEMM epilogue).
     defer=True (no residual): return (y_raw, (amax, bits, chan_add)) instead of finalizing, for
     a consumer that applies the output quant + add on the fly (groupnorm_nhwc fq_in); the spec
     is None when y is already final."""
@@ -442,7 +444,7 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         y = _conv_via_module(layer, x, residual, chan_add, upsample, co_pad)
         return (y, None) if defer else y
     if q and not prequant:
-        amax = K.act_absmax(x, "per_channel", K.NHWC)
+        amax = in_amax if in_amax is not None else K.act_absmax(x, "per_channel", K.NHWC)
         x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
     if q:
         n = x.shape[0]
@@ -661,11 +663,19 @@ def transformer_fwd(tm, x, ctx_kv):
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias),
                              q_bits=max(q, 0))
         t = run_conv(tm.proj_in, h, prequant=q > 0).view(-1, c)
-    for blk in tm.transformer_blocks:
-        t = block_fwd(blk, t, n, hh * ww, ctx_kv)
+    # the last block's feed-forward output GEMM reduces proj_out's per-(n, c) input amax in its
+    # epilogue (post-residual) when proj_out quantizes per channel through the fp16 path
+    q_out = 0 if tm.linear_proj or conv_i8(tm.proj_out) else conv_qbits(tm.proj_out)
+    want = AMAX_POST and q_out > 0 and n * hh * ww >= AMAX_POST_MIN_ROWS and (hh * ww) % 64 == 0
+    in_amax = None
+    for bi, blk in enumerate(tm.transformer_blocks):
+        last = bi == len(tm.transformer_blocks) - 1
+        t = block_fwd(blk, t, n, hh * ww, ctx_kv, want_amax=want and last)
+        if isinstance(t, tuple):
+            t, in_amax = t
     if tm.linear_proj:
         return run_linear(tm.proj_out, t, residual=x.view(-1, c)).view(n, hh, ww, c)
-    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x)
+    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x, in_amax=in_amax)
 
 
 def _qkv_operand(attn):
@@ -737,8 +747,10 @@ def self_attn_qkv(attn, h, n, s):
     return y[:, :, :c], y[:, :, c:2 * c], y[:, :, 2 * c:]
 
 
-def block_fwd(blk, t, n, s, ctx_kv):
-    """BasicTransformerBlock: self-attn, cross-attn, GEGLU feed-forward, each + residual."""
+def block_fwd(blk, t, n, s, ctx_kv, want_amax=False):
+    """BasicTransformerBlock: self-attn, cross-attn, GEGLU feed-forward, each + residual.
+    want_amax: return (t, amax) - the output's per-(sample, channel) amax reduced in the epilogue of
+    the feed-forward output GEMM after its residual add - when that linear runs the plain fp16 GEMM."""
     c = t.shape[1]
     a1 = blk.attn1
     # int8-MFMA mode: each LayerNorm emits its consumer's per-token int8 codes directly
@@ -757,4 +769,36 @@ def block_fwd(blk, t, n, s, ctx_kv):
     t = run_linear(a2.to_out[0], o.view(-1, c), residual=t)
     h = ln(blk.norm3, lin_i8(blk.ff.net[0].proj) and blk.ff.net[0].proj.output_quant_name == "None")
     g = ff_geglu(blk.ff.net[0].proj, h)
-    return run_linear(blk.ff.net[2], g, residual=t)
+    fo = blk.ff.net[2]
+    op = _fake_quant_gemm_operand(fo) if want_amax and not isinstance(g, tuple) and g.shape[0] >= I8_MIN_ROWS else None
+    if op is not None:
+        w, fmt, sc, gr, wf = op
+        amax, zeroed = A.zeroed_f32(n * c, t.device)
+        out = K.linear(g, w, fmt, sc, gr, bias=fo.bias, residual=t, weight_f16=wf, amax=amax, rows_per_sample=s,
+                       amax_zeroed=zeroed, amax_post=True)
+        return out, amax
+    return run_linear(fo, g, residual=t)
+
+
+# the post-residual amax epilogue runs unsplit (no split-K slabs): used where M is large enough
+# that the GEMM would not split anyway (the 64x64 and 32x32 levels of SD1.5 at CFG batch 8)
+AMAX_POST_MIN_ROWS = 8192
+AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
+
+
+def _fake_quant_gemm_operand(layer):
+    """(weight, fmt, scales, group, fp16 weight) when run_linear(layer, x) is exactly one K.linear
+    on x (an nn.Linear, or a WxAxLinear without act / output quant, int8-MFMA / fp8 operands or a
+    calibration hook), else None."""
+    if getattr(layer, "_qd_hook", None) is not None:
+        return None
+    if isinstance(layer, WxAxLinear):
+        if layer.quantize_act or layer.output_quant_name != "None":
+            return None
+        if layer.i8_operand() is not None or layer.f8_operand() is not None:
+            return None
+        w, fmt, sc, g = layer.gemm_weight()
+        return w, fmt, sc, g, (layer.weight if fmt != "f16" else None)
+    if isinstance(layer, nn.Linear):
+        return _f16(layer.weight), "f16", None, 0, None
+    return None

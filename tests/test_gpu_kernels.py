@@ -194,6 +194,29 @@ def test_linear_skinny_m_gemv(M, N, Kd, fmt, dev):
     assert ((yt - ref_t).abs() <= tol_t).all(), (yt - ref_t).abs().max().item()
 
 
+def test_geglu_epilogue_packed_gelu_bit_exact(dev):
+    """The GEMM epilogue's packed-fp32 GELU (gelu2_f) equals the scalar gelu_f of the standalone
+    GEGLU kernel bit for bit on every finite fp16 gate value: an exact identity projection
+    ([h | g] = x) feeds both, h = 1."""
+    k = K()
+    allg = torch.arange(-32768, 32768, dtype=torch.int32).to(torch.int16).view(torch.float16)
+    allg = allg[torch.isfinite(allg)]
+    n = (allg.numel() + 63) // 64 * 64
+    g = torch.zeros(n, dtype=torch.float16)
+    g[: allg.numel()] = allg
+    M, I = n // 64, 64
+    x = torch.cat([torch.ones(M, I, dtype=torch.float16), g.view(M, I)], 1).to(dev)  # K = 128
+    w = torch.zeros(2 * I, 2 * I, dtype=torch.float16)
+    w[torch.arange(2 * I), torch.arange(2 * I)] = 1.0
+    w = w.to(dev)
+    y = k.linear(x, w, "f16")
+    assert torch.equal(y, x)
+    perm = k.geglu_interleave_rows(2 * I, dev)
+    fused = k.linear(x, w[perm].contiguous(), "f16", geglu=True)
+    unfused = k.geglu(y)
+    assert torch.equal(fused, unfused)
+
+
 @pytest.mark.parametrize("M,I,Kd,fmt", [(256, 1280, 320, "f16"), (1000, 640, 640, "i8"), (64, 2560, 1280, "i4")])
 def test_linear_geglu_epilogue(M, I, Kd, fmt, dev):
     k = K()
@@ -437,6 +460,39 @@ def forced_gemm():
         kernels.force_gemm(None if v is None or v < 0 else v)
     yield force
     kernels.force_gemm(None)
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 1, 3] + list(range(100, 116)) + [300, 301])
+@pytest.mark.parametrize("fmt", ["f16", "i8"])
+def test_linear_post_residual_amax(variant, fmt, forced_gemm, dev):
+    """QD_EPI_AMAX_POST: the epilogue adds the residual to the fragments and reduces the
+    per-(sample, column) amax of the FINAL output (the consuming conv's input amax).  Output as
+    the plain residual epilogue's, amax equal to the exact max of that output (ping-pong and
+    split-K plans fall back to unsplit tiles that support it)."""
+    k = K()
+    g = torch.Generator().manual_seed(11)
+    M, N, Kd, rps = 4 * 1024, 320, 1280, 1024
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+    b = torch.randn(N, generator=g).half().to(dev)
+    r = (torch.randn(M, N, generator=g) * 2).half().to(dev)
+    if fmt == "i8":
+        codes, scales, wdq = k.weight_quant(w, 128, 8)
+        op, sc, grp, wf = codes, scales, 128, wdq
+    else:
+        op, sc, grp, wf = w, None, 0, None
+    forced_gemm(variant)
+    plain = k.linear(x, op, fmt, sc, grp, bias=b, residual=r, weight_f16=wf)
+    amax = torch.full((M // rps * N,), 123.0, device=dev)  # the call zeroes it (amax_zeroed=False)
+    got = k.linear(x, op, fmt, sc, grp, bias=b, residual=r, weight_f16=wf, amax=amax, rows_per_sample=rps,
+                   amax_post=True)
+    # (the plain call may split K - another fp32 summation order - where the post-residual one
+    # never does: the outputs agree to the fp16 rounding of the projection, an ulp of which can
+    # exceed an ulp of the output where the residual cancels it)
+    gc, pc, rc = got.cpu().float(), plain.cpu().float(), r.cpu().float()
+    assert ((gc - pc).abs() <= 2 * ulp16(pc.abs() + rc.abs()) + 1e-3).all()
+    ref = got.float().abs().view(M // rps, rps, N).amax(1).reshape(-1)
+    assert torch.equal(amax, ref)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 116)) + [200, 201, 202, 203, 300, 301, 302, 303, 304])
