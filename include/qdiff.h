@@ -217,6 +217,12 @@ int qd_groupnorm_workspace(int n, int hw, int c, int groups);
 /* LayerNorm over the last dim C of [rows, C]. */
 int qd_layernorm(const void* x, int rows, int c, float eps, const void* gamma, const void* beta,
                  void* y, void* stream);
+/* LayerNorm of a conv output whose per-(sample, channel) output fake-quant is pending
+ * (Transformer2DModel proj_in -> BasicTransformerBlock norm1): t_out = fq(x; amax[n][c], n_bits)
+ * (qd_fq_finalize arithmetic, the block's residual stream) and y = LayerNorm(t_out) in one pass.
+ * rows_per_sample % 4 == 0 (row r belongs to sample r / rows_per_sample); C <= 2048. */
+int qd_layernorm_fq(const void* x, const float* amax, int n_bits, int rows, int rows_per_sample, int c,
+                    float eps, const void* gamma, const void* beta, void* t_out, void* y, void* stream);
 /* GEGLU (diffusers): h[M, 2I] -> out[M, I] = h[:, :I] * gelu(h[:, I:]). */
 int qd_geglu(const void* h, int m, int inner, void* out, void* stream);
 /* out = silu(x) elementwise (count elements). */

@@ -29,6 +29,15 @@ namespace qd {
 // half(1e-5): the fp16 image of clamp_(min=1e-5) (no fp16 lies strictly between 1e-5 and it).
 __device__ __forceinline__ float clamp_min_f16() { return (float)(f16)1e-5f; }
 
+// f32 -> f16 with the f32 value materialised first.  Left alone, the backend folds the producing
+// fma / mul into v_fma_mixlo_f16, which rounds the exact result to f16 once instead of to f32 and
+// then to f16 (torch's op-boundary rounding); the two differ when the f32 rounding moves the value
+// onto or across an f16 rounding midpoint (measured: 1 GroupNorm output in 655k moved by 1 ulp).
+__device__ __forceinline__ f16 to_f16(float x) {
+  asm volatile("" : "+v"(x));
+  return (f16)x;
+}
+
 // s = half( half(max(amax, 1e-5)) / qmax )     fake_quant.py:44-46, 114-116, 127-129
 __device__ __forceinline__ float fq_scale(float amax, int qmax) {
   float a = fmaxf(amax, clamp_min_f16());

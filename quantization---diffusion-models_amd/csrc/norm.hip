@@ -83,7 +83,7 @@ __device__ __forceinline__ f16x8 gn_xf8(const GnIn& in, f16x8 v, const GnXf& t) 
     for (int j = 0; j < 8; ++j) {
       f16 o = v[j];
       if (q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
-      if (a) o = (f16)((float)o + t.ca[j]);
+      if (a) o = to_f16((float)o + t.ca[j]);
       v[j] = o;
     }
   }
@@ -100,7 +100,7 @@ __device__ __forceinline__ f16x8 gn_load8(const GnIn& in, int c, long row, int c
     for (int j = 0; j < 8; ++j) {
       f16 o = v[j];
       if (q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
-      if (a) o = (f16)((float)o + t.ca[j]);
+      if (a) o = to_f16((float)o + t.ca[j]);
       v[j] = o;
     }
   }
@@ -115,7 +115,7 @@ __device__ __forceinline__ float gn_load1(const GnIn& in, int c, long n, long ro
     const float s = fq_scale(in.amax[n * c + ch], in.qmax);
     v = fq_apply_r((float)v, s, rcp_exact(s));
   }
-  if (in.cadd) v = (f16)((float)v + (float)in.cadd[n * in.cadd_ld + ch]);
+  if (in.cadd) v = to_f16((float)v + (float)in.cadd[n * in.cadd_ld + ch]);
   return (float)v;
 }
 
@@ -142,8 +142,8 @@ static GnGeom gn_geom(int n, int hw, int c) {
 }
 
 __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
-  f16 o = (f16)fmaf(xv, k.x, k.y);
-  if (silu) o = (f16)silu_f((float)o);
+  f16 o = to_f16(fmaf(xv, k.x, k.y));
+  if (silu) o = to_f16(silu_f((float)o));
   return (float)o;
 }
 
@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, lo
           const f16x8 b = *reinterpret_cast<const f16x8*>(beta + j * 8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            o[i][e] = (f16)fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[e], (float)b[e]);
+            o[i][e] = to_f16(fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[e], (float)b[e]));
             m = fmaxf(m, fabsf((float)o[i][e]));
           }
         }
@@ -782,7 +782,7 @@ __global__ void __launch_bounds__(256) k_layernorm(const f16* __restrict__ x, lo
         const f16x8 b = *reinterpret_cast<const f16x8*>(beta + j * 8);
         f16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (f16)fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[e], (float)b[e]);
+        for (int e = 0; e < 8; ++e) o[e] = to_f16(fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[e], (float)b[e]));
         *reinterpret_cast<f16x8*>(y + (row0 + r) * c + j * 8) = o;
       }
     }
@@ -798,6 +798,117 @@ static void launch_ln(const f16* x, long rows, int c, float eps, const f16* g, c
   if (r >= 4) k_layernorm<PER, 4, I8><<<(int)((rows + 15) / 16), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
   else if (r >= 2) k_layernorm<PER, 2, I8><<<(int)((rows + 7) / 8), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
   else k_layernorm<PER, 1, I8><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
+}
+
+// LayerNorm of a conv output whose per-(sample, channel) output fake-quant is still pending
+// (Transformer2DModel proj_in -> BasicTransformerBlock norm1): t = fq(y; amax[n][c]) is written
+// (the block's residual stream, k_finalize's arithmetic) and LayerNorm(t) (k_layernorm's) in the
+// same pass, so the finalize launch and its re-read disappear.  A wave owns RPW consecutive rows
+// of one sample (rows_per_sample % RPW == 0), all their loads issued together: its lanes'
+// fake-quant scales are computed once per RPW rows (16 rows per wave: too few waves in flight).
+constexpr int LNFQ_RPW = 4;
+template <int PER, int R>
+__global__ void __launch_bounds__(256) k_fq_layernorm(const f16* __restrict__ x, long rows, int c, int rps,
+                                                      const float* __restrict__ amax, int qmax, float eps,
+                                                      const f16* __restrict__ gamma, const f16* __restrict__ beta,
+                                                      f16* __restrict__ t_out, f16* __restrict__ y) {
+  const long rbeg = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * LNFQ_RPW;
+  if (rbeg >= rows) return;
+  const long rend = rbeg + LNFQ_RPW < rows ? rbeg + LNFQ_RPW : rows;
+  const long n = rbeg / rps;
+  const int lane = threadIdx.x & 63;
+  const int chunks = c >> 3;
+  float sc[PER][8];
+  double rs[PER][8];
+  f16x8 g[PER], b[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + i * 64;
+    if (j < chunks) {
+      fq_scales8(amax + n * c + j * 8, qmax, sc[i], rs[i]);
+      g[i] = *reinterpret_cast<const f16x8*>(gamma + j * 8);
+      b[i] = *reinterpret_cast<const f16x8*>(beta + j * 8);
+    }
+  }
+  for (long row0 = rbeg; row0 < rend; row0 += R) {
+    f16x8 v[R][PER];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int j = lane + i * 64;
+        v[r][i] = (row0 + r < rend && j < chunks) ? *reinterpret_cast<const f16x8*>(x + (row0 + r) * c + j * 8)
+                                                  : (f16x8){};
+      }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (row0 + r >= rend) break;
+      // t = fq(y): the finalized value, stored as the residual stream
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int j = lane + i * 64;
+        if (j < chunks) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[r][i][e] = fq_apply_r((float)v[r][i][e], sc[i][e], rs[i][e]);
+          *reinterpret_cast<f16x8*>(t_out + (row0 + r) * c + j * 8) = v[r][i];
+        }
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)v[r][i][e];
+      const float mean = wave_sum(s) / (float)c;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        if (lane + i * 64 < chunks) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float a = (float)v[r][i][e] - mean;
+            q = fmaf(a, a, q);
+          }
+        }
+      }
+      const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)c + eps);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int j = lane + i * 64;
+        if (j < chunks) {
+          f16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = to_f16(fmaf(((float)v[r][i][e] - mean) * rstd, (float)g[i][e], (float)b[i][e]));
+          *reinterpret_cast<f16x8*>(y + (row0 + r) * c + j * 8) = o;
+        }
+      }
+    }
+  }
+}
+
+extern "C" int qd_layernorm_fq(const void* x, const float* amax, int n_bits, int rows, int rows_per_sample, int c,
+                               float eps, const void* gamma, const void* beta, void* t_out, void* y, void* stream) {
+  QD_REQUIRE(x && amax && gamma && beta && t_out && y, "null pointer");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "bad n_bits");
+  QD_REQUIRE(c % 8 == 0 && c <= 2048, "LayerNorm-fq needs C % 8 == 0, C <= 2048");
+  QD_REQUIRE(rows_per_sample > 0 && rows_per_sample % LNFQ_RPW == 0 && rows % rows_per_sample == 0,
+             "LayerNorm-fq needs rows_per_sample % 4 == 0 and whole samples");
+  QD_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(t_out) |
+               reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
+               reinterpret_cast<uintptr_t>(amax)) & 15) == 0, "LayerNorm-fq operands must be 16-B aligned");
+  if (rows == 0) return 0;
+  const int per = (c / 8 + 63) / 64;
+  const int grid = (int)((rows + 4L * LNFQ_RPW - 1) / (4L * LNFQ_RPW));
+  const int qm = (1 << (n_bits - 1)) - 1;
+  hipStream_t st = S(stream);
+  const f16 *xp = (const f16*)x, *g = (const f16*)gamma, *b = (const f16*)beta;
+#define QD_LNFQ(P, RR) \
+  k_fq_layernorm<P, RR><<<grid, 256, 0, st>>>(xp, rows, c, rows_per_sample, amax, qm, eps, g, b, (f16*)t_out, (f16*)y)
+  if (per <= 1) QD_LNFQ(1, 4);
+  else if (per <= 2) QD_LNFQ(2, 4);
+  else QD_LNFQ(4, 2);
+#undef QD_LNFQ
+  QD_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int qd_layernorm_i8(const void* x, int rows, int c, float eps, const void* gamma, const void* beta,
@@ -868,7 +979,7 @@ extern "C" int qd_geglu(const void* h, int m, int inner, void* out, void* stream
 
 __global__ void k_silu(const f16* __restrict__ x, f16* __restrict__ y, long count) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e < count) y[e] = (f16)silu_f((float)x[e]);
+  if (e < count) y[e] = to_f16(silu_f((float)x[e]));
 }
 
 extern "C" int qd_silu(const void* x, void* y, int64_t count, void* stream) {

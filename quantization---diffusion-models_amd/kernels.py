@@ -667,6 +667,18 @@ def layernorm(x, eps, gamma, beta, out=None):
     return o
 
 
+def layernorm_fq(y, amax, n_bits, rows_per_sample, eps, gamma, beta):
+    """(t, h): t = the per-(sample, channel) fake-quant of the raw conv output y [rows, C] with its
+    amax [rows / rows_per_sample, C] (fq_finalize), h = layernorm(t) - one pass (qd_layernorm_fq)."""
+    _chk(y, "y")
+    rows, c = y.shape
+    t = _empty((rows, c), torch.float16, y.device)
+    h = _empty((rows, c), torch.float16, y.device)
+    _lib.call("qd_layernorm_fq", _p(y), _p(amax), n_bits, rows, rows_per_sample, c, float(eps), _p(gamma), _p(beta),
+              _p(t), _p(h), _stream())
+    return t, h
+
+
 def geglu(h, out=None):
     _chk(h, "h")
     inner = h.shape[-1] // 2

@@ -652,6 +652,7 @@ def _resnet_tail(res, h, temb_silu, tp, sc):
 def transformer_fwd(tm, x, ctx_kv):
     """diffusers Transformer2DModel (continuous input) + BasicTransformerBlock(s)."""
     n, hh, ww, c = x.shape
+    t_fq = None  # pending output fake-quant of t (amax, bits, chan_add)
     if tm.linear_proj:
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
         t = run_linear(tm.proj_in, h.view(-1, c))
@@ -662,7 +663,9 @@ def transformer_fwd(tm, x, ctx_kv):
         q = conv_qbits(tm.proj_in)
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias),
                              q_bits=max(q, 0))
-        t = run_conv(tm.proj_in, h, prequant=q > 0).view(-1, c)
+        # proj_in's output fake-quant is left to the first block's norm1 (fused finalize + LayerNorm)
+        t, t_fq = run_conv(tm.proj_in, h, prequant=q > 0, defer=True)
+        t = t.view(-1, c)
     # the last block's feed-forward output GEMM reduces proj_out's per-(n, c) input amax in its
     # epilogue (post-residual) when proj_out quantizes per channel through the fp16 path
     q_out = 0 if tm.linear_proj or conv_i8(tm.proj_out) else conv_qbits(tm.proj_out)
@@ -670,7 +673,7 @@ def transformer_fwd(tm, x, ctx_kv):
     in_amax = None
     for bi, blk in enumerate(tm.transformer_blocks):
         last = bi == len(tm.transformer_blocks) - 1
-        t = block_fwd(blk, t, n, hh * ww, ctx_kv, want_amax=want and last)
+        t = block_fwd(blk, t, n, hh * ww, ctx_kv, want_amax=want and last, t_fq=t_fq if bi == 0 else None)
         if isinstance(t, tuple):
             t, in_amax = t
     if tm.linear_proj:
@@ -747,17 +750,30 @@ def self_attn_qkv(attn, h, n, s):
     return y[:, :, :c], y[:, :, c:2 * c], y[:, :, 2 * c:]
 
 
-def block_fwd(blk, t, n, s, ctx_kv, want_amax=False):
+def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
     """BasicTransformerBlock: self-attn, cross-attn, GEGLU feed-forward, each + residual.
     want_amax: return (t, amax) - the output's per-(sample, channel) amax reduced in the epilogue of
-    the feed-forward output GEMM after its residual add - when that linear runs the plain fp16 GEMM."""
+    the feed-forward output GEMM after its residual add - when that linear runs the plain fp16 GEMM.
+    t_fq = (amax, bits, chan_add): t is a raw conv output whose output fake-quant is pending; it is
+    applied together with norm1 (qd_layernorm_fq) or, where that does not apply, by fq_finalize."""
     c = t.shape[1]
     a1 = blk.attn1
     # int8-MFMA mode: each LayerNorm emits its consumer's per-token int8 codes directly
     big = t.shape[0] >= I8_MIN_ROWS
     ln = lambda norm, i8: (K.layernorm_i8 if i8 and big else K.layernorm)(t, norm.eps, _f16(norm.weight),
                                                                            _f16(norm.bias))
-    h = ln(blk.norm1, _qkv_operand_i8(a1) is not None)
+    i8_qkv = _qkv_operand_i8(a1) is not None
+    if t_fq is not None:
+        amax, bits, cadd = t_fq
+        if LN_FQ and amax is not None and bits > 0 and cadd is None and not (i8_qkv and big) and s % 4 == 0 \
+                and c <= 2048:
+            t, h = K.layernorm_fq(t, amax, bits, s, blk.norm1.eps, _f16(blk.norm1.weight), _f16(blk.norm1.bias))
+        else:
+            if amax is not None or cadd is not None:
+                t = K.fq_finalize(t.view(n, s, c), amax, bits, chan_add=cadd, out=t.view(n, s, c)).view(-1, c)
+            h = ln(blk.norm1, i8_qkv)
+    else:
+        h = ln(blk.norm1, i8_qkv)
     q, k, v = self_attn_qkv(a1, h, n, s)
     o = K.attention(q, k, v, a1.heads)
     t = run_linear(a1.to_out[0], o.view(-1, c), residual=t)
@@ -784,6 +800,7 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False):
 # that the GEMM would not split anyway (the 64x64 and 32x32 levels of SD1.5 at CFG batch 8)
 AMAX_POST_MIN_ROWS = 8192
 AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
+LN_FQ = not os.environ.get("QD_NO_LN_FQ")  # A/B switch: proj_in finalize as its own pass before norm1
 
 
 def _fake_quant_gemm_operand(layer):

@@ -25,6 +25,9 @@ for (n, h, w, c) in ((8, 64, 64, 320), (8, 32, 32, 640), (8, 16, 16, 1280)):
         ("act_absmax per-ch", lambda: K.act_absmax(x, "per_channel", K.NHWC), 1),
         ("act_apply per-ch", lambda: K.act_apply_nhwc(x, amax, 8, out=y), 2),
         ("layernorm", lambda: K.layernorm(x.view(-1, c), 1e-5, gam, bet, out=y.view(-1, c)), 2),
+        ("finalize+layernorm", lambda: K.layernorm(K.fq_finalize(x, amax, 8, out=r).view(-1, c), 1e-5, gam, bet,
+                                                   out=y.view(-1, c)), 5),
+        ("layernorm_fq", lambda: K.layernorm_fq(x.view(-1, c), amax, 8, h * w, 1e-5, gam, bet), 3),
         ("groupnorm+silu+fq", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8, out=y), 3),
         ("groupnorm", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, out=y), 3),
         ("gn+silu+fq fq_in", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8, out=y,

@@ -377,6 +377,25 @@ def test_groupnorm_streaming_path(c, hw, silu, q, dev):
         assert_fp16_close(got, ref, ulps=2.0, atol=2e-3)
 
 
+@pytest.mark.parametrize("rps,c,bits", [(4096, 320, 8), (1024, 640, 8), (256, 1280, 8), (64, 1280, 4)])
+def test_layernorm_fq_equals_finalize_then_layernorm(rps, c, bits, dev):
+    """The fused proj_in output fake-quant + norm1 (qd_layernorm_fq) writes the same residual
+    stream and LayerNorm output as qd_fq_finalize followed by qd_layernorm, bit for bit."""
+    k = K()
+    g = torch.Generator().manual_seed(rps + c)
+    n = 2
+    y = (torch.randn(n, rps, c, generator=g) * 3).half().to(dev)
+    amax = y.float().abs().amax(1).reshape(-1).contiguous()
+    amax[::7] *= 0.5  # some channels clip
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half().to(dev)
+    bet = (0.1 * torch.randn(c, generator=g)).half().to(dev)
+    t_ref = k.fq_finalize(y, amax, bits)
+    h_ref = k.layernorm(t_ref.view(-1, c), 1e-5, gam, bet)
+    t, h = k.layernorm_fq(y.view(-1, c), amax, bits, rps, 1e-5, gam, bet)
+    assert torch.equal(t, t_ref.view(-1, c))
+    assert torch.equal(h, h_ref)
+
+
 def test_groupnorm_two_sources(dev):
     k = K()
     g = torch.Generator().manual_seed(5)
