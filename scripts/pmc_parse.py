@@ -1,0 +1,48 @@
+"""Reduce scripts/pmc_dominant.sh output (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)
+to profiles/<tag>_pmc_dominant.json: HBM bytes per launch of the dominant conv per GEMM variant,
+with the MI355X_MICROARCH.md gfx950 corrections (FETCH_SIZE x2: it reports half of the 16-B/lane
+streaming reads; WRITE_SIZE as is; KB = 1024 B).
+usage: python scripts/pmc_parse.py gpurun_out/pmc_TAG OUT.json "202 203" """
+import csv
+import glob
+import json
+import os
+import sys
+
+d, out, variants = sys.argv[1], sys.argv[2], sys.argv[3].split()
+
+
+def per_launch(path, counter):
+    files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    tot, names, disp = {}, {}, set()
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            k = r["Kernel_Name"]
+            if "k_gemm" not in k and "k_conv_halo" not in k:
+                continue
+            tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
+            disp.add((k, r.get("Dispatch_Id", r.get("Correlation_Id", ""))))
+    if not tot:
+        return None, None, 0
+    k = max(tot, key=tot.get)
+    n = len([1 for kk, _ in disp if kk == k])
+    return k, tot[k] / n, n
+
+
+res = {"shape": "conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880)",
+       "correction": "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE reports 1/2 of 16-B/lane "
+                     "streaming reads); WRITE_SIZE as is; KB = 1024 B",
+       "algorithmic_bytes_per_launch": 8 * 64 * 64 * 320 * 2 + 320 * 9 * 320 * 2 + 8 * 64 * 64 * 320 * 2,
+       "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 scripts/roof_kernel.py 10 <variant>",
+       "by_variant": {}}
+for v in variants:
+    kf, fetch, nf = per_launch(os.path.join(d, f"fetch_{v}"), "FETCH_SIZE")
+    kw, write, nw = per_launch(os.path.join(d, f"write_{v}"), "WRITE_SIZE")
+    if fetch is None or write is None:
+        continue
+    res["by_variant"][v] = {"FETCH_SIZE_KB_per_launch": fetch, "WRITE_SIZE_KB_per_launch": write, "launches": nf,
+                            "kernel_name": kf, "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024))}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
