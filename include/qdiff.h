@@ -339,8 +339,9 @@ int qd_smooth_fold(void* ln_w, void* ln_b, void* const* fc_w, const int* fc_rows
 
 /* ---------------- self-tests (test infrastructure) ---------------------------------- */
 /* Exhaustive check of the reciprocal shortcut used by every fake-quant apply kernel against the
- * IEEE-division form (all fp16 scales, values around every quantization midpoint): counts[0] =
- * reciprocal errors > 1 ulp, counts[1] = differing fake-quant results (device int[2]). */
+ * IEEE-division form (all fp16 scales): counts[0] = reciprocal errors > 1 ulp, counts[1] =
+ * differing fake-quant results at the values around every quantization midpoint, counts[2] =
+ * differing f16 quotients over every finite fp16 x (device int[3]). */
 int qd_selftest_recip(int* counts, void* stream);
 
 /* ---------------- SD3 / SD3.5 MMDiT -------------------------------------------------------

@@ -572,7 +572,8 @@ extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, i
 // every non-negative finite fp16 scale s, and for each s the fp16 values x next to every
 // quantization midpoint (k + 1/2) s, |k| <= 130, plus the midpoint images themselves.
 // counts[0] = scales whose rcp_exact differs from 1 / (double)s by more than 1 f64 ulp,
-// counts[1] = (s, x) pairs whose fake-quant results differ.  Test infrastructure only.
+// counts[1] = (s, x) pairs whose fake-quant results differ, counts[2] = (s, x) pairs over ALL
+// finite fp16 x whose f16 quotients differ.  Test infrastructure only.
 __global__ void k_selftest_recip(int* counts) {
   const unsigned short sb = (unsigned short)(blockIdx.x);
   const f16 sh = __builtin_bit_cast(f16, sb);
@@ -598,12 +599,23 @@ __global__ void k_selftest_recip(int* counts) {
     }
   }
   if (bad) atomicAdd(&counts[1], bad);
+  // every finite fp16 x: the f16 quotient of the shortcut == half(IEEE f32 x / s)
+  int badq = 0;
+  for (int xb = threadIdx.x; xb < 65536; xb += blockDim.x) {
+    const float xf = (float)__builtin_bit_cast(f16, (unsigned short)xb);
+    if (__builtin_isnan(xf) || __builtin_isinf(xf)) continue;
+    const f16 a = (f16)(xf / s), b = (f16)(float)((double)xf * r);
+    if (__builtin_bit_cast(unsigned short, a) != __builtin_bit_cast(unsigned short, b) &&
+        !(__builtin_isnan((float)a) && __builtin_isnan((float)b)))
+      ++badq;
+  }
+  if (badq) atomicAdd(&counts[2], badq);
 }
 
 extern "C" int qd_selftest_recip(int* counts, void* stream) {
   QD_REQUIRE(counts, "null pointer");
   hipStream_t st = S(stream);
-  qd_zero_f32(reinterpret_cast<float*>(counts), 2, st);  // int 0 == f32 +0 bits
+  qd_zero_f32(reinterpret_cast<float*>(counts), 3, st);  // int 0 == f32 +0 bits
   k_selftest_recip<<<65536, 64, 0, st>>>(counts);
   QD_CHECK_LAUNCH();
   return 0;
