@@ -358,7 +358,13 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
   // head_dim 49..64 (SD3.5 / SDXL): 4 waves x 2 groups (accumulators partly in AGPRs, 2 blocks
   // per CU) - scripts/attn_sweep.sh: 626 -> 543 us on SD3.5-L's joint attention, 272 -> 234 us
   // on SDXL's 64x64 level; at head_dim 40 (SD1.5) 8 x 2 stays ahead (304 vs 370 us).
-  if (sq >= 512 && DV > 48 && DV <= 80) {
+  if (sq >= 512 && DV > 80 && DV <= 112) {
+    // head_dim 65-96 (SD1.5's 32x32 level, d = 80): 8 waves x 2 query groups even below 512 blocks
+    // (scripts/attn_bench.py: 43.7 -> 36-38 us at b 8, 1024 tokens, 8 heads; profiles/r02w_attn.log)
+    const int grid = ((sq + 255) / 256) * b * heads;
+    k_attn<DP, DV, NB, 8, 2><<<grid, 512, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
+                                                  (f16*)o, ldo, heads, sq, skv, d, sl2);
+  } else if (sq >= 512 && DV > 48 && DV <= 80) {
     const int grid = ((sq + 127) / 128) * b * heads;
     k_attn<DP, DV, NB, 4, 2><<<grid, 256, 0, st>>>((const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv,
                                                   (f16*)o, ldo, heads, sq, skv, d, sl2);

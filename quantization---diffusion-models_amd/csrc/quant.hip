@@ -578,7 +578,7 @@ __global__ void k_selftest_recip(int* counts) {
   const unsigned short sb = (unsigned short)(blockIdx.x);
   const f16 sh = __builtin_bit_cast(f16, sb);
   const float s = (float)sh;
-  if (!(s >= 0.f) || __builtin_isinf(s)) return;
+  if ((sb & 0x8000u) || __builtin_isnan(s) || __builtin_isinf(s)) return;  // scales are >= +0 (fq_scale)
   const double r = rcp_exact(s), e = 1.0 / (double)s;
   if (threadIdx.x == 0 && s > 0.f) {
     const double ulp = __builtin_fabs(e) * 2.220446049250313e-16;

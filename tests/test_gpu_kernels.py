@@ -608,7 +608,7 @@ def test_fast_reciprocal_fake_quant_is_exact(dev):
     """rcp_exact + fq_apply_r (all apply kernels) == the IEEE-division fake-quant, for every fp16
     scale and the values next to every quantization midpoint; and the f16 quotient of the shortcut
     == half(IEEE x / s) for every finite fp16 x (a 3-op f32 Markstein division from RN(1/s) was
-    tried instead of the f64 product and failed this on 158715 of the ~4e9 pairs)."""
+    tried instead of the f64 product and failed this on 95229 of the ~4e9 pairs)."""
     from qdiff import _lib
     counts = torch.zeros(3, dtype=torch.int32, device=dev)
     _lib.call("qd_selftest_recip", counts.data_ptr(), torch.cuda.current_stream().cuda_stream)
