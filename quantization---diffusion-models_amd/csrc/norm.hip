@@ -42,6 +42,8 @@ struct GnIn {
   int qmax;          // ... and its fake-quant qmax (0: no quantization)
   const f16* cadd;   // ... + cadd[n * cadd_ld + c] (null: none)
   int cadd_ld;
+  const f16* res;    // ... + res[row][c] (the block's residual; null: none) - XF 2: the statistics
+  f16* xout;         // pass writes the finalized input x to xout, which the apply pass then reads
 };
 
 // per-channel input transform state of one 8-channel chunk of sample n
@@ -73,6 +75,18 @@ __device__ __forceinline__ void gn_xf_init(const GnIn& in, int c, long n, int ch
 __device__ __forceinline__ f16x8 gn_raw8(const GnIn& in, int c, long row, int ch) {
   const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
   return *reinterpret_cast<const f16x8*>(p);
+}
+
+// XF 2: output quant (if in.qmax) then + the residual row chunk r
+__device__ __forceinline__ f16x8 gn_fin8(const GnIn& in, f16x8 v, const GnXf& t, f16x8 r) {
+  const bool q = in.qmax > 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f16 o = v[j];
+    if (q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
+    v[j] = to_f16((float)o + (float)r[j]);
+  }
+  return v;
 }
 
 template <int XF>
@@ -116,6 +130,7 @@ __device__ __forceinline__ float gn_load1(const GnIn& in, int c, long n, long ro
     v = fq_apply_r((float)v, s, rcp_exact(s));
   }
   if (in.cadd) v = to_f16((float)v + (float)in.cadd[n * in.cadd_ld + ch]);
+  if (in.res) v = to_f16((float)v + (float)in.res[row * c + ch]);
   return (float)v;
 }
 
@@ -175,12 +190,23 @@ __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg
       // unconditional loads (row clamped): a guarded load makes hipcc wait per load
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * by, r1 - 1), ch);
+      f16x8 rr[8];
+      if constexpr (XF == 2) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rr[u] = *reinterpret_cast<const f16x8*>(in.res + (n * hw + min(rb + u * by, r1 - 1)) * c + ch);
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) QD_PIN(v[u]);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         if (rb + u * by >= r1) break;
-        const f16x8 w = gn_xf8<XF>(in, v[u], xf);
+        f16x8 w;
+        if constexpr (XF == 2) {
+          w = gn_fin8(in, v[u], xf, rr[u]);
+          *reinterpret_cast<f16x8*>(in.xout + (n * hw + rb + u * by) * c + ch) = w;
+        } else {
+          w = gn_xf8<XF>(in, v[u], xf);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xv = (float)w[j];
@@ -545,6 +571,7 @@ __global__ void __launch_bounds__(256) k_gn_fused(GnIn in, int hw, int c, int cg
       rq[j] = rcp_exact(sq[j]);
     }
   }
+  // XF 2: this block's statistics pass wrote its rows of x to xout (visible after the barriers)
   for (int rb = p0; rb < hw; rb += 4 * PS) {
     f16x8 v[4];
 #pragma unroll
@@ -601,8 +628,11 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
   float* amax_n = y8 ? amax + (long)n * c : nullptr;  // per-(n, group) maxima in the spare n * c floats
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
-  const bool xf = in.qmax > 0 || in.cadd;
-  if (const int G = y8 ? 0 : gn_fused_groups(n, hw, c, groups)) {
+  const bool fin = in.res != nullptr;  // XF 2: finalize + residual, x materialised to in.xout
+  QD_REQUIRE(!fin || (in.xout && !in.x2 && !in.cadd && !y8), "residual input: xout needed, no concat / temb / int8 output");
+  const bool xf = !fin && (in.qmax > 0 || in.cadd);
+  // (the residual-input form always takes the streaming passes: its statistics pass writes x)
+  if (const int G = y8 || fin ? 0 : gn_fused_groups(n, hw, c, groups)) {
     const dim3 gf(groups / G, n);
 #define QD_GN_FUSED(XFV, SV, QV)                                                                               \
   k_gn_fused<XFV, SV, QV><<<gf, 256, 0, st>>>(in, hw, c, cg, G, eps, (const f16*)gamma, (const f16*)beta, qmax, \
@@ -622,11 +652,23 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
     return 0;
   }
   const dim3 gs(g.gx, n, g.zs), bs(g.bx, g.bys);
-  if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
+  if (fin) k_gn_stats<2><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
+  else if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
   else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
+  // (the coefficient stage recomputes its shift / fallback elements from the raw sources; the
+  // apply pass reads the materialised x)
   k_gn_coeff<<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta, silu,
                                          qmax > 0 || y8, coef, amax, amax_n);
   const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
+  if (fin) {
+    const GnIn inx{in.xout, nullptr, c, nullptr, 0, nullptr, 0, nullptr, nullptr};
+    if (silu && qmax > 0) k_gn_apply<0, 1, true><<<ga, ba, 0, st>>>(inx, hw, c, g.rpb, coef, qmax, amax, (f16*)y);
+    else if (silu) k_gn_apply<0, 1, false><<<ga, ba, 0, st>>>(inx, hw, c, g.rpb, coef, qmax, amax, (f16*)y);
+    else if (qmax > 0) k_gn_apply<0, 0, true><<<ga, ba, 0, st>>>(inx, hw, c, g.rpb, coef, qmax, amax, (f16*)y);
+    else k_gn_apply<0, 0, false><<<ga, ba, 0, st>>>(inx, hw, c, g.rpb, coef, qmax, amax, (f16*)y);
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
   if (y8) {  // (the qmax argument carries the group count of amax_n[n][group])
     if (xf && silu) k_gn_apply<1, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
     else if (xf) k_gn_apply<1, 0, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
@@ -658,7 +700,7 @@ extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw
                             void* y, float* ws, void* stream) {
   if (x2) QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c, "bad concat split (must be a multiple of 8)");
   else c1 = c;
-  GnIn in{(const f16*)x, (const f16*)x2, c1, nullptr, 0, nullptr, 0};
+  GnIn in{(const f16*)x, (const f16*)x2, c1, nullptr, 0, nullptr, 0, nullptr, nullptr};
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
 }
 
@@ -676,7 +718,8 @@ extern "C" int qd_groupnorm_i8(const void* x, const void* x2, int c1, const floa
   QD_REQUIRE(in_bits == 0 || (in_bits >= 2 && in_bits <= 16 && in_amax), "bad input quant bits / amax");
   if (cadd_ld <= 0) cadd_ld = c;
   QD_REQUIRE(!cadd || (cadd_ld >= c && cadd_ld % 8 == 0), "bad cadd leading dim");
-  GnIn in{(const f16*)x, (const f16*)x2, c1, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld};
+  GnIn in{(const f16*)x, (const f16*)x2, c1, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld,
+          nullptr, nullptr};
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, 0, nullptr, ws, S(stream), y8, scales);
 }
 
@@ -686,7 +729,19 @@ extern "C" int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int i
   QD_REQUIRE(in_bits == 0 || (in_bits >= 2 && in_bits <= 16 && in_amax), "bad input quant bits / amax");
   if (cadd_ld <= 0) cadd_ld = c;
   QD_REQUIRE(!cadd || (cadd_ld >= c && cadd_ld % 8 == 0), "bad cadd leading dim");
-  GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld};
+  GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld,
+          nullptr, nullptr};
+  return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
+}
+
+extern "C" int qd_groupnorm_fin(const void* y_raw, const float* in_amax, int in_bits, const void* residual,
+                                void* x_out, int n, int hw, int c, int groups, float eps, const void* gamma,
+                                const void* beta, int silu, int q_bits, void* y, float* ws, void* stream) {
+  QD_REQUIRE(y_raw && residual && x_out, "null pointer");
+  QD_REQUIRE(in_bits == 0 || (in_bits >= 2 && in_bits <= 16 && in_amax), "bad input quant bits / amax");
+  QD_REQUIRE(x_out != y_raw && x_out != residual, "x_out must not alias the sources (other blocks still read them)");
+  GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, nullptr, 0,
+          (const f16*)residual, (f16*)x_out};
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
 }
 

@@ -355,27 +355,30 @@ class UNet2DConditionModel(nn.Module):
 
         h = run_conv(self.conv_in, x, c_valid=cfg.in_channels)
         skips = [h]
+        # block outputs travel as Pending (conv2 / proj_out output quant + residual deferred) so a
+        # following GroupNorm materialises them in its statistics pass; other consumers _get()
         for blk in self.down_blocks:
             for i, res in enumerate(blk.resnets):
-                h = resnet_fwd(res, h, temb_silu, tp=tps.get(id(res)))
+                h = resnet_fwd(res, h, temb_silu, tp=tps.get(id(res)), pend=True)
                 if blk.attentions is not None:
-                    h = transformer_fwd(blk.attentions[i], h, ctx_kv)
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True)
                 skips.append(h)
             if blk.downsamplers is not None:
-                h = run_conv(blk.downsamplers[0].conv, h)
+                h = run_conv(blk.downsamplers[0].conv, _get(h))
                 skips.append(h)
         mb = self.mid_block
-        h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])))
-        h = transformer_fwd(mb.attentions[0], h, ctx_kv)
-        h = resnet_fwd(mb.resnets[1], h, temb_silu, tp=tps.get(id(mb.resnets[1])))
+        h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])), pend=True)
+        h = transformer_fwd(mb.attentions[0], h, ctx_kv, pend=True)
+        h = resnet_fwd(mb.resnets[1], h, temb_silu, tp=tps.get(id(mb.resnets[1])), pend=True)
         for blk in self.up_blocks:
             for i, res in enumerate(blk.resnets):
                 skip = skips.pop()
-                h = resnet_fwd(res, h, temb_silu, skip=skip, tp=tps.get(id(res)))
+                h = resnet_fwd(res, h, temb_silu, skip=skip, tp=tps.get(id(res)), pend=True)
                 if blk.attentions is not None:
-                    h = transformer_fwd(blk.attentions[i], h, ctx_kv)
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True)
             if blk.upsamplers is not None:
-                h = run_conv(blk.upsamplers[0].conv, h, upsample=True)
+                h = run_conv(blk.upsamplers[0].conv, _get(h), upsample=True)
+        h = _get(h)
         q = conv_qbits(self.conv_out)
         h = K.groupnorm_nhwc(h, self.conv_norm_out.num_groups, self.conv_norm_out.eps,
                              _f16(self.conv_norm_out.weight), _f16(self.conv_norm_out.bias), silu=True, q_bits=q)
@@ -383,6 +386,34 @@ class UNet2DConditionModel(nn.Module):
 
 
 # ------------------------------------------------------------------ fused layer helpers
+class Pending:
+    """A conv output y whose output fake-quant and residual add are still pending: the block
+    output x = half(fq(y; amax, bits) + res).  A GroupNorm consumer materialises x in its
+    statistics pass (K.groupnorm_fin); any other consumer calls get() (fq_finalize in place)."""
+    __slots__ = ("y", "amax", "bits", "res", "x")
+
+    def __init__(self, y, amax, bits, res):
+        self.y, self.amax, self.bits, self.res, self.x = y, amax, bits, res, None
+
+    def get(self):
+        if self.x is None:
+            self.x = K.fq_finalize(self.y, self.amax, self.bits, residual=self.res, out=self.y)
+        return self.x
+
+
+def _get(h):
+    return h.get() if isinstance(h, Pending) else h
+
+
+# the GroupNorm-consumer finalize runs on the streaming (> 256 pixels) GroupNorm; smaller levels
+# keep finalize + the single-kernel GroupNorm (fewer launches there)
+GN_FIN = not os.environ.get("QD_NO_GN_FIN")  # A/B switch (scripts/ab_env.sh)
+
+
+def _gn_fin_ok(p):
+    return GN_FIN and isinstance(p, Pending) and p.x is None and p.y.shape[1] * p.y.shape[2] > 256
+
+
 def _f16(t):
     if t is None:
         return None
@@ -422,13 +453,13 @@ def _conv_weight(layer, co_pad=None):
 
 
 def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=False, c_valid=0, co_pad=None,
-             defer=False, in_amax=None):
+             defer=False, in_amax=None, pend=False):
     """NHWC conv of an nn.Conv2d or WxAxConv2d with the reference's act fake-quant semantics:
     q_x = act_quant(x) -> y = conv(q_x) + b -> q_y = act_quant(y) -> [+ residual | + temb].
     in_amax: x's per-(n, c) amax, already reduced by its producer (the GEMM epilogue).
     defer=True (no residual): return (y_raw, (amax, bits, chan_add)) instead of finalizing, for
     a consumer that applies the output quant + add on the fly (groupnorm_nhwc fq_in); the spec
-    is None when y is already final."""
+    is None when y is already final.  pend (with residual): return a Pending block output."""
     if isinstance(layer, WxAxConv2d):
         layer._check_supported()
         i8 = layer.i8_operand()
@@ -460,6 +491,8 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
             y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)
         if defer and residual is None:
             return y, (amax, q, chan_add)
+        if pend and residual is not None and chan_add is None:
+            return Pending(y, amax, q, residual)
         return K.fq_finalize(y, amax, q, residual=residual, chan_add=chan_add, out=y)
     if chan_add is None:
         y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, residual=residual)
@@ -607,19 +640,30 @@ def _geglu_operand_i8(layer, i8):
     return op
 
 
-def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
+def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False):
     """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1).
     tp: this block's time_emb_proj(silu(temb)) when precomputed by temb_projections().
     The up-block skip concat is never materialised in fp16: norm1 reads both sources and a
-    quantized conv_shortcut receives the per-(n, c) fake-quant of the concat directly."""
+    quantized conv_shortcut receives the per-(n, c) fake-quant of the concat directly.
+    x may be a Pending block output: norm1 then materialises it (K.groupnorm_fin).  pend: return
+    this block's output as a Pending (its conv2 output quant + residual add deferred)."""
     qs = conv_qbits(res.conv_shortcut) if res.conv_shortcut is not None else 0
+    q1 = conv_qbits(res.conv1)
+    if skip is None and not conv_i8(res.conv1) and _gn_fin_ok(x):
+        xin, h = K.groupnorm_fin(x.y, x.amax, x.bits, x.res, res.norm1.num_groups, res.norm1.eps,
+                                 _f16(res.norm1.weight), _f16(res.norm1.bias), silu=True, q_bits=max(q1, 0))
+        x.x = xin
+        if tp is None:
+            tp = run_linear(res.time_emb_proj, temb_silu)
+        sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
+        return _resnet_tail(res, h, temb_silu, tp, sc, pend)
+    x, skip = _get(x), _get(skip)
     if skip is not None and qs > 0:
         sc = run_conv(res.conv_shortcut, K.act_quant_cat_nhwc(x, skip, qs), prequant=True)
         h = K.groupnorm_nhwc(x, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
                              silu=True, q_bits=max(conv_qbits(res.conv1), 0), x2=skip)
-        return _resnet_tail(res, h, temb_silu, tp, sc)
+        return _resnet_tail(res, h, temb_silu, tp, sc, pend)
     xin = K.concat_c(x, skip) if skip is not None else x
-    q1 = conv_qbits(res.conv1)
     if conv_i8(res.conv1):  # int8-MFMA mode: GroupNorm + SiLU emits conv1's int8 codes
         h = K.groupnorm_nhwc_i8(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight),
                                 _f16(res.norm1.bias), silu=True)
@@ -629,10 +673,10 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None):
     if tp is None:
         tp = run_linear(res.time_emb_proj, temb_silu)
     sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
-    return _resnet_tail(res, h, temb_silu, tp, sc)
+    return _resnet_tail(res, h, temb_silu, tp, sc, pend)
 
 
-def _resnet_tail(res, h, temb_silu, tp, sc):
+def _resnet_tail(res, h, temb_silu, tp, sc, pend=False):
     """conv1 (+ temb) -> norm2 + SiLU -> conv2 + shortcut, h = silu(norm1(x)) [quantized]."""
     q1 = conv_qbits(res.conv1)
     if tp is None:
@@ -646,14 +690,26 @@ def _resnet_tail(res, h, temb_silu, tp, sc):
     else:
         h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                              silu=True, q_bits=max(q2, 0), fq_in=spec)
-    return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc)
+    return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc, pend=pend)
 
 
-def transformer_fwd(tm, x, ctx_kv):
-    """diffusers Transformer2DModel (continuous input) + BasicTransformerBlock(s)."""
-    n, hh, ww, c = x.shape
+def transformer_fwd(tm, x, ctx_kv, pend=False):
+    """diffusers Transformer2DModel (continuous input) + BasicTransformerBlock(s).  x may be a
+    Pending block output (the GroupNorm materialises it); pend: return the output as a Pending."""
     t_fq = None  # pending output fake-quant of t (amax, bits, chan_add)
-    if tm.linear_proj:
+    fin = not tm.linear_proj and not conv_i8(tm.proj_in) and _gn_fin_ok(x)
+    if not fin:
+        x = _get(x)
+    n, hh, ww, c = (x.y if fin else x).shape
+    if fin:
+        q = conv_qbits(tm.proj_in)
+        xm, h = K.groupnorm_fin(x.y, x.amax, x.bits, x.res, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight),
+                                _f16(tm.norm.bias), q_bits=max(q, 0))
+        x.x = xm
+        x = xm
+        t, t_fq = run_conv(tm.proj_in, h, prequant=q > 0, defer=True)
+        t = t.view(-1, c)
+    elif tm.linear_proj:
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
         t = run_linear(tm.proj_in, h.view(-1, c))
     elif conv_i8(tm.proj_in):
@@ -678,7 +734,7 @@ def transformer_fwd(tm, x, ctx_kv):
             t, in_amax = t
     if tm.linear_proj:
         return run_linear(tm.proj_out, t, residual=x.view(-1, c)).view(n, hh, ww, c)
-    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x, in_amax=in_amax)
+    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x, in_amax=in_amax, pend=pend)
 
 
 def _qkv_operand(attn):

@@ -396,6 +396,30 @@ def test_layernorm_fq_equals_finalize_then_layernorm(rps, c, bits, dev):
     assert torch.equal(h, h_ref)
 
 
+@pytest.mark.parametrize("hw,c,q,silu", [(1024, 640, 8, True), (4096, 320, 8, True), (1024, 320, 0, False),
+                                         (4096, 320, 8, False)])
+def test_groupnorm_fin_equals_finalize_then_groupnorm(hw, c, q, silu, dev):
+    """GroupNorm on a pending block output (conv output + output fake-quant + residual add): the
+    materialised x and the GroupNorm output equal fq_finalize followed by groupnorm_nhwc, bit for
+    bit (tiny-gamma channels exercise the fallback amax scan, which reads the raw sources)."""
+    k = K()
+    g = torch.Generator().manual_seed(hw + c + q)
+    n = 2
+    y = (torch.randn(n, hw, c, generator=g) * 1.5).half().to(dev)
+    r = torch.randn(n, hw, c, generator=g).half().to(dev)
+    amax = y.float().abs().amax(dim=1).reshape(-1).contiguous()
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
+    bet = (0.1 * torch.randn(c, generator=g)).half()
+    gam[::37] = 0.01
+    bet[::37] = -0.5
+    gam, bet = gam.to(dev), bet.to(dev)
+    x_ref = k.fq_finalize(y, amax, 8, residual=r)
+    h_ref = k.groupnorm_nhwc(x_ref, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
+    x, h = k.groupnorm_fin(y, amax, 8, r, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
+    assert torch.equal(x, x_ref)
+    assert torch.equal(h, h_ref)
+
+
 def test_groupnorm_two_sources(dev):
     k = K()
     g = torch.Generator().manual_seed(5)
