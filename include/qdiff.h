@@ -212,13 +212,15 @@ int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, in
 int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int in_bits, const void* cadd, int cadd_ld,
                        int n, int hw, int c, int groups, float eps, const void* gamma, const void* beta,
                        int silu, int q_bits, void* y, float* ws, void* stream);
-/* GroupNorm (+SiLU)(+output fake-quant) of x = half(fq(y_raw; in_amax, in_bits) + residual) - a
- * conv output whose output quant (fake_quant.py:340) and the block's residual add are pending -
- * whose statistics pass also writes x to x_out (the block output the later consumers read), so
- * the separate finalize pass disappears.  x_out must not alias y_raw / residual. */
-int qd_groupnorm_fin(const void* y_raw, const float* in_amax, int in_bits, const void* residual, void* x_out,
-                     int n, int hw, int c, int groups, float eps, const void* gamma, const void* beta, int silu,
-                     int q_bits, void* y, float* ws, void* stream);
+/* GroupNorm (+SiLU)(+output fake-quant) of x = half(fq(y_raw; in_amax, in_bits) + residual) (or
+ * + cadd[n * cadd_ld + c], the time-embedding add) - a conv output whose output quant
+ * (fake_quant.py:340) and add are pending - whose statistics pass also writes x to x_out (the
+ * block output the later consumers read; for conv1 -> norm2 a scratch the apply pass re-reads
+ * instead of recomputing the fake-quant), so the separate finalize pass disappears.  x_out must
+ * not alias y_raw / residual; residual and cadd are exclusive. */
+int qd_groupnorm_fin(const void* y_raw, const float* in_amax, int in_bits, const void* residual, const void* cadd,
+                     int cadd_ld, void* x_out, int n, int hw, int c, int groups, float eps, const void* gamma,
+                     const void* beta, int silu, int q_bits, void* y, float* ws, void* stream);
 /* fp32 elements of the qd_groupnorm workspace for this shape. */
 int qd_groupnorm_workspace(int n, int hw, int c, int groups);
 /* LayerNorm over the last dim C of [rows, C]. */

@@ -36,7 +36,7 @@ SIGNATURES = {
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, I, P, P],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_groupnorm_fq_in": [P, P, I, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
-    "qd_groupnorm_fin": [P, P, I, P, P, I, I, I, I, F, P, P, I, I, P, P, P],
+    "qd_groupnorm_fin": [P, P, I, P, P, I, P, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_layernorm": [P, I, I, F, P, P, P, P],
     "qd_layernorm_fq": [P, P, I, I, I, I, F, P, P, P, P, P],
     "qd_geglu": [P, I, I, P, P],

@@ -192,8 +192,10 @@ __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg
       for (int u = 0; u < 8; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * by, r1 - 1), ch);
       f16x8 rr[8];
       if constexpr (XF == 2) {
+        if (in.res) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) rr[u] = *reinterpret_cast<const f16x8*>(in.res + (n * hw + min(rb + u * by, r1 - 1)) * c + ch);
+          for (int u = 0; u < 8; ++u) rr[u] = *reinterpret_cast<const f16x8*>(in.res + (n * hw + min(rb + u * by, r1 - 1)) * c + ch);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) QD_PIN(v[u]);
@@ -202,7 +204,7 @@ __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg
         if (rb + u * by >= r1) break;
         f16x8 w;
         if constexpr (XF == 2) {
-          w = gn_fin8(in, v[u], xf, rr[u]);
+          w = in.res ? gn_fin8(in, v[u], xf, rr[u]) : gn_xf8<1>(in, v[u], xf);
           *reinterpret_cast<f16x8*>(in.xout + (n * hw + rb + u * by) * c + ch) = w;
         } else {
           w = gn_xf8<XF>(in, v[u], xf);
@@ -628,8 +630,10 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
   float* amax_n = y8 ? amax + (long)n * c : nullptr;  // per-(n, group) maxima in the spare n * c floats
   const int qmax = q_bits ? (1 << (q_bits - 1)) - 1 : 0;
-  const bool fin = in.res != nullptr;  // XF 2: finalize + residual, x materialised to in.xout
-  QD_REQUIRE(!fin || (in.xout && !in.x2 && !in.cadd && !y8), "residual input: xout needed, no concat / temb / int8 output");
+  // XF 2: the finalized input x (output quant + residual, or + temb) is written to in.xout by the
+  // statistics pass and read back by the apply pass
+  const bool fin = in.xout != nullptr;
+  QD_REQUIRE(!fin || (!in.x2 && !(in.res && in.cadd) && !y8), "materialised input: no concat / int8 output, residual or temb");
   const bool xf = !fin && (in.qmax > 0 || in.cadd);
   // (the residual-input form always takes the streaming passes: its statistics pass writes x)
   if (const int G = y8 || fin ? 0 : gn_fused_groups(n, hw, c, groups)) {
@@ -735,12 +739,16 @@ extern "C" int qd_groupnorm_fq_in(const void* y_raw, const float* in_amax, int i
 }
 
 extern "C" int qd_groupnorm_fin(const void* y_raw, const float* in_amax, int in_bits, const void* residual,
-                                void* x_out, int n, int hw, int c, int groups, float eps, const void* gamma,
-                                const void* beta, int silu, int q_bits, void* y, float* ws, void* stream) {
-  QD_REQUIRE(y_raw && residual && x_out, "null pointer");
+                                const void* cadd, int cadd_ld, void* x_out, int n, int hw, int c, int groups,
+                                float eps, const void* gamma, const void* beta, int silu, int q_bits, void* y,
+                                float* ws, void* stream) {
+  QD_REQUIRE(y_raw && x_out, "null pointer");
+  QD_REQUIRE(!(residual && cadd), "residual or temb add, not both");
   QD_REQUIRE(in_bits == 0 || (in_bits >= 2 && in_bits <= 16 && in_amax), "bad input quant bits / amax");
   QD_REQUIRE(x_out != y_raw && x_out != residual, "x_out must not alias the sources (other blocks still read them)");
-  GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, nullptr, 0,
+  if (cadd_ld <= 0) cadd_ld = c;
+  QD_REQUIRE(!cadd || (cadd_ld >= c && cadd_ld % 8 == 0), "bad cadd leading dim");
+  GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld,
           (const f16*)residual, (f16*)x_out};
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
 }

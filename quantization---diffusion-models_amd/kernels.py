@@ -658,19 +658,25 @@ def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, o
     return out
 
 
-def groupnorm_fin(y, amax, bits, residual, groups, eps, gamma, beta, silu=False, q_bits=0):
-    """(x, h): x = half(fq(y; amax, bits) + residual) (fq_finalize semantics, written by the
-    statistics pass into a new buffer) and h = groupnorm_nhwc(x, ...) - one pass fewer than
-    fq_finalize followed by groupnorm_nhwc."""
+def groupnorm_fin(y, amax, bits, residual, groups, eps, gamma, beta, silu=False, q_bits=0, cadd=None):
+    """(x, h): x = half(fq(y; amax, bits) + residual) - or + cadd[n, c] (the temb add) - with
+    fq_finalize semantics, written by the statistics pass into a new buffer, and
+    h = groupnorm_nhwc(x, ...): one pass fewer than fq_finalize followed by groupnorm_nhwc."""
     _chk(y, "y")
-    _chk(residual, "residual")
+    if residual is not None:
+        _chk(residual, "residual")
+    ld = 0
+    if cadd is not None:
+        if cadd.dim() != 2 or cadd.stride(1) != 1 or cadd.dtype != torch.float16:
+            raise ValueError("cadd must be an fp16 [N, C] tensor with unit column stride")
+        ld = cadd.stride(0)
     n, c = y.shape[0], y.shape[-1]
     hw = y.numel() // (n * c)
     x = _empty(y.shape, torch.float16, y.device)
     h = _empty(y.shape, torch.float16, y.device)
     ws = _empty((_lib.load().qd_groupnorm_workspace(n, hw, c, groups),), torch.float32, y.device)
-    _lib.call("qd_groupnorm_fin", _p(y), _p(amax), bits, _p(residual), _p(x), n, hw, c, groups, float(eps),
-              _p(gamma), _p(beta), 1 if silu else 0, q_bits, _p(h), _p(ws), _stream())
+    _lib.call("qd_groupnorm_fin", _p(y), _p(amax), bits, _p(residual), _p(cadd), ld, _p(x), n, hw, c, groups,
+              float(eps), _p(gamma), _p(beta), 1 if silu else 0, q_bits, _p(h), _p(ws), _stream())
     return x, h
 
 

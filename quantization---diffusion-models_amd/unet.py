@@ -687,6 +687,12 @@ def _resnet_tail(res, h, temb_silu, tp, sc, pend=False):
     if conv_i8(res.conv2):
         h = K.groupnorm_nhwc_i8(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                                 silu=True, fq_in=spec)
+    elif GN_FIN and spec is not None and spec[0] is not None and h.shape[1] * h.shape[2] > 256:
+        # streaming levels: the statistics pass writes the finalized conv1 output to a scratch the
+        # apply pass re-reads, instead of both passes recomputing the fake-quant + temb add
+        amax, bits, cadd = spec
+        _, h = K.groupnorm_fin(h, amax, bits, None, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight),
+                               _f16(res.norm2.bias), silu=True, q_bits=max(q2, 0), cadd=cadd)
     else:
         h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                              silu=True, q_bits=max(q2, 0), fq_in=spec)

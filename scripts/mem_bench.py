@@ -32,6 +32,8 @@ for (n, h, w, c) in ((8, 64, 64, 320), (8, 32, 32, 640), (8, 16, 16, 1280)):
         ("groupnorm", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, out=y), 3),
         ("gn+silu+fq fq_in", lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8, out=y,
                                                     fq_in=(amax, 8, None)), 3),
+        ("gn+silu+fq fin", lambda: K.groupnorm_fin(x, amax, 8, None, 32, 1e-5, gam, bet, silu=True, q_bits=8), 4),
+        ("gn+silu+fq fin+res", lambda: K.groupnorm_fin(x, amax, 8, r, 32, 1e-5, gam, bet, silu=True, q_bits=8), 5),
     ]
     print(f"[{n},{h},{w},{c}] {mb:.1f} MB per tensor")
     for name, fn, passes in rows:

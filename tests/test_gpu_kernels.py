@@ -396,9 +396,10 @@ def test_layernorm_fq_equals_finalize_then_layernorm(rps, c, bits, dev):
     assert torch.equal(h, h_ref)
 
 
-@pytest.mark.parametrize("hw,c,q,silu", [(1024, 640, 8, True), (4096, 320, 8, True), (1024, 320, 0, False),
-                                         (4096, 320, 8, False)])
-def test_groupnorm_fin_equals_finalize_then_groupnorm(hw, c, q, silu, dev):
+@pytest.mark.parametrize("hw,c,q,silu,temb", [(1024, 640, 8, True, False), (4096, 320, 8, True, False),
+                                              (1024, 320, 0, False, False), (4096, 320, 8, False, False),
+                                              (4096, 320, 8, True, True), (1024, 640, 8, True, True)])
+def test_groupnorm_fin_equals_finalize_then_groupnorm(hw, c, q, silu, temb, dev):
     """GroupNorm on a pending block output (conv output + output fake-quant + residual add): the
     materialised x and the GroupNorm output equal fq_finalize followed by groupnorm_nhwc, bit for
     bit (tiny-gamma channels exercise the fallback amax scan, which reads the raw sources)."""
@@ -413,9 +414,18 @@ def test_groupnorm_fin_equals_finalize_then_groupnorm(hw, c, q, silu, dev):
     gam[::37] = 0.01
     bet[::37] = -0.5
     gam, bet = gam.to(dev), bet.to(dev)
-    x_ref = k.fq_finalize(y, amax, 8, residual=r)
-    h_ref = k.groupnorm_nhwc(x_ref, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
-    x, h = k.groupnorm_fin(y, amax, 8, r, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
+    if temb:  # conv1 -> norm2: + the time-embedding projection per (n, c) (a row-strided view)
+        big = (torch.randn(n, 3 * c, generator=g) * 0.3).half().to(dev)
+        cadd = big[:, c: 2 * c]
+        x_ref = k.fq_finalize(y, amax, 8, chan_add=cadd)
+        h_ref = k.groupnorm_nhwc(x_ref, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
+        x, h = k.groupnorm_fin(y, amax, 8, None, 32, 1e-5, gam, bet, silu=silu, q_bits=q, cadd=cadd)
+        # and the fq_in path (both passes recompute the transform) gives the same output
+        assert torch.equal(k.groupnorm_nhwc(y, 32, 1e-5, gam, bet, silu=silu, q_bits=q, fq_in=(amax, 8, cadd)), h_ref)
+    else:
+        x_ref = k.fq_finalize(y, amax, 8, residual=r)
+        h_ref = k.groupnorm_nhwc(x_ref, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
+        x, h = k.groupnorm_fin(y, amax, 8, r, 32, 1e-5, gam, bet, silu=silu, q_bits=q)
     assert torch.equal(x, x_ref)
     assert torch.equal(h, h_ref)
 
