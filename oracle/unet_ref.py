@@ -395,7 +395,7 @@ def euler_tables(num_inference_steps, num_train=1000, beta_start=0.00085, beta_e
     ac = torch.cumprod(1.0 - betas, dim=0)
     ratio = num_train // num_inference_steps
     ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.float32) + steps_offset
-    sig = np.array(((1 - ac) / ac) ** 0.5)
+    sig = (((1 - ac) / ac) ** 0.5).numpy()
     sig = np.interp(ts, np.arange(0, len(sig)), sig)
     sigmas = torch.from_numpy(np.concatenate([sig, [0.0]]).astype(np.float32))
     return torch.from_numpy(ts), sigmas, (sigmas.max() ** 2 + 1) ** 0.5

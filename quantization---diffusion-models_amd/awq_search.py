@@ -33,7 +33,16 @@ from .fake_quant import quantize_weight_absmax, shrink_group
 N_GRID = 20
 MAX_SHRINK = 0.5
 N_SAMPLE_TOKEN = 512
+# quantizer.py:788-791 skips the q / k projections ("due to qk bmm, it is hard to clip precisely")
+# by LLM substrings; diffusers names them attn*.to_q / to_k (UNet) and add_q_proj / add_k_proj
+# (MMDiT), matched on the final name component
 AVOID_CLIP = ("q_", "k_", "query", "key", "Wqkv")
+AVOID_CLIP_LEAF = ("to_q", "to_k", "add_q_proj", "add_k_proj")
+
+
+def clip_avoided(lname):
+    leaf = lname.split(".")[-1]
+    return any(a in lname for a in AVOID_CLIP) or leaf in AVOID_CLIP_LEAF
 
 
 class InputCapture:
@@ -184,7 +193,7 @@ def run_awq_search(adapter, n_bits, group_size, calibration=None, clip=True):
             report["scales"][f"{bname}.{names[id(ln)]}"] = {"ratio": r, "loss": hist[r], "loss_ratio0": hist[0.0]}
     if clip:
         for (bname, lname), (sub, cap) in caps.items():
-            if any(a in lname for a in AVOID_CLIP):
+            if clip_avoided(lname):
                 continue
             x = cap.data()
             if id(sub) in folded:   # the fold divided this layer's input by s (and scaled W by s)
@@ -195,4 +204,4 @@ def run_awq_search(adapter, n_bits, group_size, calibration=None, clip=True):
 
 
 __all__ = ["run_awq_search", "search_scale", "search_clip", "apply_scale_ln", "apply_clip", "InputCapture",
-           "scale_groups", "N_GRID", "AVOID_CLIP"]
+           "scale_groups", "N_GRID", "AVOID_CLIP", "clip_avoided"]

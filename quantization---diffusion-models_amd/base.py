@@ -314,7 +314,13 @@ class BaseAWQForDiffusion(nn.Module):
                 c, sc = awq_unpack_linear(awq[f"{name}.qweight"], awq[f"{name}.qzeros"], awq[f"{name}.scales"],
                                           qc["group_size"] if m.in_features % qc["group_size"] == 0 else
                                           m.in_features // awq[f"{name}.scales"].shape[0])
-                m.set_codes(c.to(device), sc.to(device), m.in_features // sc.shape[1], 4)
+                # kept only if the codes dequantize to the stored fp16 buffer bit for bit (a foreign
+                # or mismatched AWQ file would otherwise make the GEMM operand differ from `weight`)
+                g = m.in_features // sc.shape[1]
+                c, sc = c.to(device), sc.to(device)
+                deq = (c.float() * sc.float().repeat_interleave(g, dim=1)).to(torch.float16)
+                if not (torch.equal(deq.float(), m.weight.float()) and m.set_codes(c, sc, g, 4)):
+                    m.drop_codes()  # the fp16 buffer (the reference's own operand)
             else:
                 # a reference-written checkpoint holds only the dequantized fp16 buffers: re-derive
                 # the integer codes and keep them only if they reproduce the buffer bit for bit
@@ -352,6 +358,7 @@ def _attach_conv_i8(m, codes, sw):
         return False
     m.i8_w, m.i8_sw = codes.contiguous(), sw.contiguous()
     m._i8_ver = (m.weight.data_ptr(), m.weight._version)
+    m._fq_saved = (m.quantise_act, m.output_quant_name, m.output_quant)
     m.quantise_act = False
     m.output_quant_name = "None"
     m.output_quant = lambda x: x

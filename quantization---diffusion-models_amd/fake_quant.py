@@ -184,6 +184,25 @@ class WxAxLinear(nn.Module):
             self.output_quant_name = "None"
             self.output_quant = _identity
 
+    def _apply(self, fn, *args, **kwargs):
+        """Module.to / .cuda / .half: codes that describe ``weight`` before the move still describe
+        it after (same values, new storage), so they are re-stamped instead of being dropped as
+        stale (which would silently leave the int8-MFMA / fp8 mode); the fp8 operand, held outside
+        the buffer set, follows the weight's device."""
+        codes_fresh = self.qcodes is not None and \
+            getattr(self, "_codes_ver", None) == (self.weight.data_ptr(), self.weight._version)
+        f8 = getattr(self, "_f8", None)
+        f8_fresh = f8 is not None and f8[0] == (self.weight.data_ptr(), self.weight._version)
+        out = super()._apply(fn, *args, **kwargs)
+        ver = (self.weight.data_ptr(), self.weight._version)
+        if codes_fresh:
+            self._codes_ver = ver
+        if f8_fresh:
+            dev = self.weight.device
+            self._f8 = (ver, f8[1].to(dev), f8[2].to(dev))
+        self._i8_sw = None
+        return out
+
     # the fused-GEMM weight operand: (tensor, fmt, scales, group)
     def gemm_weight(self):
         """Integer codes while they still describe ``weight``; after a load_state_dict or an
@@ -386,6 +405,18 @@ class WxAxConv2d(nn.Module):
     def ci_pad(self):
         return (self.in_channels + 7) // 8 * 8
 
+    def _apply(self, fn, *args, **kwargs):
+        """Module.to / .cuda / .half: int8-mode codes that describe ``weight`` before the move are
+        re-stamped after it (and their fp32 scales kept fp32) instead of going stale - a stale
+        code set would drop the conv to an A16 fp16 conv, since set_int8 turned the fake-quant off."""
+        i8_fresh = self.i8_w is not None and \
+            getattr(self, "_i8_ver", None) == (self.weight.data_ptr(), self.weight._version)
+        out = super()._apply(fn, *args, **kwargs)
+        if i8_fresh:
+            self.i8_sw = self.i8_sw.float()
+            self._i8_ver = (self.weight.data_ptr(), self.weight._version)
+        return out
+
     def gemm_weight(self):
         """[Co][kh][kw][Ci_pad] fp16 view of ``weight`` (rebuilt if the buffer changed)."""
         ver = (self.weight.data_ptr(), self.weight._version)
@@ -401,7 +432,12 @@ class WxAxConv2d(nn.Module):
         if self.i8_w is None:
             return None
         if getattr(self, "_i8_ver", None) != (self.weight.data_ptr(), self.weight._version):
+            # the buffer was edited / reloaded: back to the reference's fake-quant conv on it, with
+            # the activation quant set_int8 switched off restored
             self.i8_w = self.i8_sw = None
+            saved = getattr(self, "_fq_saved", None)
+            if saved is not None:
+                self.quantise_act, self.output_quant_name, self.output_quant = saved
             return None
         return self.i8_w, self.i8_sw
 
@@ -420,6 +456,7 @@ class WxAxConv2d(nn.Module):
         self.i8_w = codes.view(co, kh, kw, cip).contiguous()
         self.i8_sw = scales.float().view(-1).contiguous()
         self._i8_ver = (self.weight.data_ptr(), self.weight._version)
+        self._fq_saved = (self.quantise_act, self.output_quant_name, self.output_quant)
         self.quantise_act = False
         self.output_quant_name = "None"
         self.output_quant = _identity

@@ -110,8 +110,15 @@ def config_from_diffusers(d):
         kw["skip_prk_steps"] = d["skip_prk_steps"]
     if d.get("prediction_type", "epsilon") != "epsilon":
         raise NotImplementedError(f"prediction_type {d['prediction_type']}: the SD pipelines use epsilon")
-    if name == "EulerDiscreteScheduler" and d.get("timestep_spacing", "leading") != "leading":
-        raise NotImplementedError("EulerDiscreteScheduler timestep_spacing other than 'leading'")
+    # the device step kernels implement "leading" spacing without sample clipping / dynamic
+    # thresholding: a config asking for anything else would silently run another schedule than
+    # DiffusionPipeline.from_pretrained builds from the same file
+    if d.get("timestep_spacing", "leading") != "leading":
+        raise NotImplementedError(f"{name} timestep_spacing {d['timestep_spacing']!r} (only 'leading')")
+    if d.get("thresholding", False):
+        raise NotImplementedError(f"{name} thresholding=True (dynamic thresholding) has no device kernel")
+    if name == "DDIMScheduler" and d.get("clip_sample", True):  # diffusers' DDIM default is True
+        raise NotImplementedError("DDIMScheduler clip_sample=True has no device kernel (SD checkpoints set False)")
     return cls(**kw)
 
 
@@ -126,8 +133,9 @@ def config_to_diffusers(cfg):
          "set_alpha_to_one": cfg.set_alpha_to_one, "prediction_type": "epsilon"}
     if isinstance(cfg, PNDMConfig):
         d["skip_prk_steps"] = cfg.skip_prk_steps
-    if isinstance(cfg, EulerDiscreteConfig):
-        d["timestep_spacing"] = "leading"
+    d["timestep_spacing"] = "leading"
+    if name == "DDIMScheduler":
+        d["clip_sample"] = False
     return d
 
 
@@ -146,7 +154,7 @@ def euler_discrete_tables(num_inference_steps, cfg: EulerDiscreteConfig = EulerD
     ratio = cfg.num_train_timesteps // num_inference_steps
     ts = (np.arange(0, num_inference_steps) * ratio).round()[::-1].copy().astype(np.float32)
     ts += cfg.steps_offset
-    sig_all = np.array(((1 - ac) / ac) ** 0.5)
+    sig_all = np.asarray((((1 - ac) / ac) ** 0.5).numpy() if torch.is_tensor(ac) else ((1 - ac) / ac) ** 0.5)
     sig = np.interp(ts, np.arange(0, len(sig_all)), sig_all)
     sigmas = torch.from_numpy(np.concatenate([sig, [0.0]]).astype(np.float32))
     dscale = (sigmas ** 2 + 1) ** 0.5

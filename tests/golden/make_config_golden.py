@@ -1,7 +1,7 @@
 """Oracle outputs at BASELINE.json's full-size configs (TEST FIXTURES; run in the build container,
 whose AVX512-FP16 CPU runs the half oracle's torch-CPU Half kernels at speed):
 
-    python tests/golden/make_config_golden.py [c1 c3 c4]
+    python tests/golden/make_config_golden.py [c1 c2 c3 c4]
 
 For every case of oracle/config_cases.py: the synthetic checkpoint's UNet (CPU generator,
 seed 0), the half and fp32 oracle results on the case's seeded inputs, and the weights'
@@ -55,6 +55,10 @@ def main(names):
             print(f"{name} {variant}: {tuple(y.shape)} in {time.time() - t0:.1f}s "
                   f"finite {bool(torch.isfinite(y.float()).all())}", flush=True)
             tensors[f"{name}.{variant}"] = y.to(torch.float16).contiguous()
+        if "sq_alpha" in c:  # the SmoothQuant activation statistics the fold used
+            for p, (a1, a3) in CC.sq_acts(name, cfg).items():
+                tensors[f"{name}.act.{p}.norm1"] = a1.contiguous()
+                tensors[f"{name}.act.{p}.norm3"] = a3.contiguous()
         meta[name] = json.dumps({"fingerprint": fp, "case": c, "threads": torch.get_num_threads()})
     save_file(tensors, OUT, metadata=meta)
     print("wrote", OUT)

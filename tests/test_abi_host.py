@@ -244,3 +244,33 @@ def test_cpu_baseline_census_covers_the_unet():
     assert count == {"conv2d": 98, "linear": 184, "sdpa": 32, "group_norm": 61, "layer_norm": 48}
     assert abs(flop["conv2d"] / 2e9 - 443.9) < 1 and abs(flop["linear"] / 2e9 - 233.3) < 1
     assert abs(flop["sdpa"] / 2e9 - 126.1) < 1
+
+
+def test_scheduler_configs_rejected_when_unsupported():
+    """a DDIM / PNDM scheduler_config.json asking for trailing / linspace spacing,
+    sample clipping or thresholding is refused rather than silently run as 'leading'."""
+    import pytest
+    from qdiff.scheduler import DDIMConfig, PNDMConfig, config_from_diffusers, config_to_diffusers
+    base = {"beta_start": 0.00085, "beta_end": 0.012, "beta_schedule": "scaled_linear", "steps_offset": 1,
+            "set_alpha_to_one": False}
+    assert isinstance(config_from_diffusers({"_class_name": "DDIMScheduler", "clip_sample": False, **base}), DDIMConfig)
+    assert isinstance(config_from_diffusers({"_class_name": "PNDMScheduler", "skip_prk_steps": True, **base}),
+                      PNDMConfig)
+    for bad in ({"_class_name": "DDIMScheduler", **base},                      # diffusers default clip_sample=True
+                {"_class_name": "DDIMScheduler", "clip_sample": False, "timestep_spacing": "trailing", **base},
+                {"_class_name": "PNDMScheduler", "timestep_spacing": "linspace", **base},
+                {"_class_name": "DDIMScheduler", "clip_sample": False, "thresholding": True, **base}):
+        with pytest.raises(NotImplementedError):
+            config_from_diffusers(bad)
+    for cfg in (DDIMConfig(), PNDMConfig()):  # what save_pretrained writes reloads
+        assert type(config_from_diffusers(config_to_diffusers(cfg))) is type(cfg)
+
+
+def test_awq_clip_avoids_diffusers_qk_names():
+    """the clip search skips the q / k projections under diffusers' names too
+    (quantizer.py:788-791 avoids them by LLM substrings)."""
+    from qdiff.awq_search import clip_avoided
+    for n in ("attn1.to_q", "attn2.to_k", "attn.add_q_proj", "attn.add_k_proj", "self_attn.q_proj"):
+        assert clip_avoided(n), n
+    for n in ("attn1.to_v", "attn1.to_out.0", "ff.net.0.proj", "ff.net.2", "attn.add_v_proj"):
+        assert not clip_avoided(n), n

@@ -326,3 +326,35 @@ def test_layernorm_i8_and_rows_equal_oracle(dev, rows, c):
     assert np.array_equal(q.cpu().numpy(), q_ref) and np.array_equal(s.cpu().numpy(), s_ref)
     q2, s2 = k.quant_rows_i8(ref16)
     assert np.array_equal(q2.cpu().numpy(), q_ref) and np.array_equal(s2.cpu().numpy(), s_ref)
+
+
+def test_int8_codes_survive_device_moves():
+    """model.to(...) after quantize(int8_mfma=True) keeps every layer in the int8-MFMA mode (the
+    codes are re-stamped, not dropped as stale) and gives identical outputs."""
+    from qdiff.fake_quant import WxAxConv2d, WxAxLinear
+    from qdiff.models import StableDiffusion1_x
+    model = StableDiffusion1_x.from_pretrained("synthetic:tiny", device="cuda:0", seed=21)
+    cfg = model.pipeline.unet.config
+    model.quantize(quant_config=dict(QC8), quantUnet=True, int8_mfma=True)
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(2, 4, cfg.sample_size, cfg.sample_size, generator=g).half()
+    ctx = torch.randn(2, 77, cfg.cross_attention_dim, generator=g).half()
+
+    def n_int8():
+        mods = list(model.pipeline.unet.modules())
+        return (sum(isinstance(m, WxAxConv2d) and m.i8_operand() is not None for m in mods),
+                sum(isinstance(m, WxAxLinear) and m.i8_operand() is not None for m in mods))
+
+    before, counts = _one_eval(model, x, 701, ctx), n_int8()
+    assert counts[0] > 0 and counts[1] > 0
+    model.to("cpu")
+    model.to("cuda:0")
+    assert n_int8() == counts
+    assert all(m.i8_sw.dtype == torch.float32 for m in model.pipeline.unet.modules()
+               if isinstance(m, WxAxConv2d) and m.i8_sw is not None)
+    assert torch.equal(_one_eval(model, x, 701, ctx), before)
+    # an in-place edit of a buffer does make the codes stale: that conv returns to the reference's
+    # fake-quant W8A8 (input + output activation quant restored), not to an A16 conv
+    conv = model.pipeline.unet.down_blocks[0].resnets[0].conv1
+    conv.weight.mul_(1.0)
+    assert conv.i8_operand() is None and conv.quantise_act and conv.output_quant_name == "per_channel"
