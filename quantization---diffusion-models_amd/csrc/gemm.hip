@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 using namespace qd;
 
@@ -312,6 +313,7 @@ __device__ __forceinline__ float rowgroup_max(float v) {
 }
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ i32x8 f8_operand(f16x8 lo, f16x8 hi) {
@@ -332,10 +334,17 @@ __device__ __forceinline__ void i8_scale(const GemmArgs& p, const i32x4 (&acc)[T
       for (int j = 0; j < TN; ++j) out[i][j] = __builtin_bit_cast(f32x4, acc[i][j]);
   } else {
     float sa[TM];
+    if (p.sa_rps && p.sa_rps % (TM * 16) == 0) {
+      // per-sample scales (conv): the wave tile's rows lie in one sample - one scalar index
+      const float s = p.sa[min(m0 + wm0, p.M - 1) / p.sa_rps];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = min(m0 + wm0 + i * 16 + fr, p.M - 1);
-      sa[i] = p.sa[p.sa_rps ? m / p.sa_rps : m];
+      for (int i = 0; i < TM; ++i) sa[i] = s;
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = min(m0 + wm0 + i * 16 + fr, p.M - 1);
+        sa[i] = p.sa[p.sa_rps ? m / p.sa_rps : m];
+      }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -407,18 +416,23 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int ml = wm0 + i * 16 + fr;
-          const bool ok = m0 + ml < p.M && col_ok;
           f16x4 h;
 #pragma unroll
           for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
-          if (post && ok) {
-            const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)(m0 + ml) * p.ldy + n);
+          if (post) {
+            const bool ok = m0 + ml < p.M && col_ok;
+            if (ok) {
+              const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)(m0 + ml) * p.ldy + n);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
+              for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
+            }
           }
+          if (do_amax) {  // (uniform) the column maxes only when an amax is reduced
+            const bool ok = m0 + ml < p.M && col_ok;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+            for (int r = 0; r < 4; ++r)
+              if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+          }
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
         }
         if (do_amax && !geglu) {
@@ -450,40 +464,52 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // are interleaved in 16-row blocks [hidden 16 | gate 16] (BN % 32 == 0), so output columns
     // 16b + j of the tile read h = tile[32b + j], g = tile[32b + 16 + j]; diffusers GEGLU on the
     // fp16 projection outputs: out = half(h * half(gelu(g))).
+    // 16-B chunks per output row are a compile-time constant in each branch (no runtime
+    // division); stores / residual loads are 32-bit-offset buffer ops (rows past M fall off the
+    // end of the buffer range and are dropped / read 0).
     static_assert(BN % 32 == 0 || BN % 16 == 0, "tile width");
-    const int cpr = geglu ? BN / 16 : BN / 8;
-    const int on0 = geglu ? n0 >> 1 : n0, oN = geglu ? p.N >> 1 : p.N;
+    const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
+    const __amdgpu_buffer_rsrc_t yrs = rsrc(p.y, ybytes);
+    const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res && !post ? p.res : p.y, has_res && !post ? ybytes : 0u);
+    auto pass2 = [&](auto cpr_c, auto geglu_c) {
+      constexpr int CPR = decltype(cpr_c)::value;
+      constexpr bool GG = decltype(geglu_c)::value;
+      const int on0 = GG ? n0 >> 1 : n0, oN = GG ? p.N >> 1 : p.N;
 #pragma unroll 2
-    for (int e = threadIdx.x; e < BM * cpr; e += NT) {
-      const int row = e / cpr, c = e - row * cpr;
-      const int m = m0 + row, n = on0 + c * 8;
-      if (m < p.M && n < oN) {
-        f16x8 v;
-        if (geglu) {
-          const int tc = (c >> 1) * 32 + (c & 1) * 8;
-          const f16x8 hv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc);
-          const f16x8 gv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc + 16);
+      for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+        const int row = e / CPR, c = e - row * CPR;
+        const int n = on0 + c * 8;
+        if (n < oN) {
+          const unsigned off = ((unsigned)(m0 + row) * (unsigned)p.ldy + (unsigned)n) * 2u;
+          f16x8 v;
+          if constexpr (GG) {
+            const int tc = (c >> 1) * 32 + (c & 1) * 8;
+            const f16x8 hv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc);
+            const f16x8 gv = *reinterpret_cast<const f16x8*>(ct + row * LP + tc + 16);
 #pragma unroll
-          for (int r = 0; r < 8; r += 2) {
-            const f32x2 gg = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
-            v[r] = (f16)((float)hv[r] * (float)(f16)gg.x);
-            v[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)gg.y);
+            for (int r = 0; r < 8; r += 2) {
+              const f32x2 gg = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+              v[r] = (f16)((float)hv[r] * (float)(f16)gg.x);
+              v[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)gg.y);
+            }
+          } else {
+            v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+            if (gtanh) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) v[r] = (f16)gelu_tanh_f((float)v[r]);
+            }
           }
-        } else {
-          v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
-          if (gtanh) {
+          if (has_res && !post) {
+            const f16x8 rq = bload(rrs, m0 + row < p.M ? off : OOB);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = (f16)gelu_tanh_f((float)v[r]);
+            for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
           }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
         }
-        if (has_res && !post) {
-          const f16x8 rq = *reinterpret_cast<const f16x8*>(p.res + (long)m * p.ldy + n);
-#pragma unroll
-          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
-        }
-        *reinterpret_cast<f16x8*>(p.y + (long)m * p.ldy + n) = v;
       }
-    }
+    };
+    if (geglu) pass2(std::integral_constant<int, BN / 16>{}, std::true_type{});
+    else pass2(std::integral_constant<int, BN / 8>{}, std::false_type{});
   }
 }
 
@@ -697,6 +723,22 @@ struct BDma {
       if (G % NW == 0 || j * NW + wid < G) glds16(rs, sb + (j * NW + wid) * RPW * BKT, rowoff[j] + ko);
   }
 };
+
+// vmcnt of a value the caller's unrolling makes a compile-time constant (folds to one s_waitcnt)
+__device__ __forceinline__ void wait_vm_c(int n) {
+  if (n <= 0) wait_vm<0>();
+  else if (n == 1) wait_vm<1>();
+  else if (n == 2) wait_vm<2>();
+  else if (n == 3) wait_vm<3>();
+  else if (n == 4) wait_vm<4>();
+  else if (n == 5) wait_vm<5>();
+  else if (n == 6) wait_vm<6>();
+  else if (n == 7) wait_vm<7>();
+  else if (n == 8) wait_vm<8>();
+  else if (n == 9) wait_vm<9>();
+  else if (n == 10) wait_vm<10>();
+  else wait_vm<0>();
+}
 
 #define QD_VM_CASE(n) \
   case n:             \
@@ -1182,8 +1224,8 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
 // double-buffered one tap ahead.  Summation order over K differs from the tap-major kernels
 // (chunk-major), so its outputs may differ from theirs in the last fp16 bit.
 #ifndef QD_HALO_ABL  // diagnostic builds only (scripts/halo_ablate.sh): 1 no MFMA, 2 no weight DMA in the
-#define QD_HALO_ABL 0  // K loop, 4 no halo DMA in the K loop, 8 no barrier / wait (results are garbage)
-#endif
+#define QD_HALO_ABL 0  // K loop, 4 no halo DMA in the K loop, 8 no barrier / wait (results are garbage);
+#endif                 // int8 halo conv also: 16 no fragment reads in the K loop, 32 no epilogue
 constexpr int HALO_ROWS_MAX = 400;  // (RB + 2) * (W + 2) <= 396 for W in {16, 32, 64}
 
 template <int BN>
@@ -1489,9 +1531,283 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
   else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
+// ---- int8 halo conv (int8-MFMA mode, qd_gemm_force 140 / 141) -------------------------------
+// The halo conv's tile (256 output pixels = whole image rows x BN channels, 8 waves, wave tile
+// 64 x BN/2) and K order (64-channel chunk major, the 9 taps inside a chunk) on int8 codes in the
+// "half view" (two codes per fp16 slot, p.Cip = Ci_pad / 2).  A chunk is 64 codes = one 64-B LDS
+// row per halo pixel / weight row, so one 16-B fragment read is the i32x4 operand of one
+// v_mfma_i32_16x16x64_i8: half the LDS bytes per MFMA flop of the fp16 halo kernels, twice their
+// MFMA rate.  What bounds a kernel of this shape is instruction issue (an MFMA holds its SIMD's
+// issue for half of its 16 cycles; the rest must carry the reads, the DMA and the bookkeeping of
+// both waves), so the K loop is built to issue almost nothing but MFMAs and fragment reads:
+//  * W is a template parameter and the halo is stored with a row pitch of W2P = roundup(W + 2, 8)
+//    pixels: the XOR swizzle of an A fragment row (row >> 1 & 3) then depends only on (lane, kx),
+//    so every fragment read is one per-(kx) base VGPR + a compile-time immediate offset - no
+//    address VALU in the loop (the B fragments likewise, the ring slot being tap % 3);
+//  * every wave issues the same DMA instructions each step (the surplus halo / weight groups of
+//    the uneven wave split load out-of-range offsets into a scratch LDS slot), so every vmcnt is a
+//    compile-time constant, and the K offsets of a step ride in the scalar soffset;
+//  * the MFMAs of step s start before its barrier: phase 1 (fragment rows 0..TM/2-1) -> wait(own
+//    loads of tile s+1 [+ the next chunk's halo at a chunk's last tap]) -> barrier -> DMA tile s+2
+//    into the slot of s-1 (read in step s-2, consumed by MFMA(s-1) before this barrier) + one halo
+//    group of chunk c+1 into chunk c-1's buffer (last read in step (c-1, 7)) -> phase 2 (rows
+//    TM/2..TM-1) with the fragment reads of step s+1 interleaved one per MFMA.
+// Exact int32 sums: identical bits to every other int8 variant (k_gemm_dma<I8>, k_gemm_pp<I8>).
+__device__ __forceinline__ void glds16s(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, (int)voff, soff, 0, 0);
+}
+typedef __attribute__((address_space(3))) char lds_char_t;
+typedef __attribute__((address_space(3))) const f16x8 lds_f16x8_t;
+// 32-bit LDS byte offset of a __shared__ object, and a 16-B read at one (constant parts of the
+// offset fold into the ds_read_b128 immediate)
+__device__ __forceinline__ int lds_addr(const void* p) { return (int)(uintptr_t)(lds_char_t*)p; }
+__device__ __forceinline__ f16x8 lds_read16(int addr) { return *(lds_f16x8_t*)(uintptr_t)(unsigned)addr; }
+
+template <int BN, int W, int RING>
+__global__ void __launch_bounds__(512, 1) k_conv_halo_i8(GemmArgs p) {
+  constexpr int BM = 256, NT = 512, NW = 8, WGN = 2;
+  constexpr int WM = 64, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  constexpr int RB = BM / W;                  // image rows per tile
+  constexpr int W2P = (W + 2 + 7) / 8 * 8;    // halo row pitch in pixels (multiple of 8)
+  constexpr int RS = 64;                      // bytes per LDS row: one 64-code chunk
+  constexpr int HROWS = (RB + 2) * W2P;
+  constexpr int HG = (HROWS + 15) / 16;       // 16-row halo DMA groups
+  constexpr int HL = (HG + NW - 1) / NW;      // halo DMA slots per wave (uniform)
+  constexpr int G = BN / 16;                  // 16-row weight DMA groups
+  constexpr int BL = (G + NW - 1) / NW;       // weight DMA slots per wave (uniform)
+  constexpr int HB = HROWS * RS, BB = BN * RS, SCR = 1024;
+  constexpr int LOOPB = 2 * HB + RING * BB + SCR;
+  constexpr int EPIB = epi_lds_halves(BM, BN) * 2;
+  constexpr int LDSB = LOOPB > EPIB ? LOOPB : EPIB;
+  static_assert(LDSB <= 163840, "halo + weight ring exceed the 160 KB of LDS");
+  // the next chunk's halo groups (taps 0 .. HL-1) must be older than the weight tile a chunk's
+  // last tap waits for (issued at tap 10 - RING); the previous chunk's last taps issue none
+  static_assert(RING >= 3 && HL >= 1 && HL <= 10 - RING, "halo staging vs weight ring depth");
+  static_assert(W % 16 == 0 && 64 % W == 0 && WN % 8 == 0, "tile geometry");
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  char* const halo = smem;
+  char* const ring = smem + 2 * HB;
+  char* const scratch = smem + 2 * HB + RING * BB;
+
+  const int nbm = p.M / BM, nbn = p.N / BN;
+  const int ntile = nbm * nbn, nwg = ntile * p.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = wg / p.splits, split = wg - tile * p.splits;
+  const int bm = tile / nbn, bn = tile - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int img = m0 / (p.Ho * W), oh0 = (m0 - img * p.Ho * W) / W;
+  const int c_beg = split * p.kps, nch = p.kps;  // 64-code chunks of this split
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // DMA lane map (1 KB per wave-instruction = 16 rows of 64 B): lane -> row (lane >> 2) of the
+  // group, LDS chunk lane & 3 holding K chunk (lane & 3) ^ ((row >> 1) & 3)
+  const int gcl = (lane & 3) ^ ((lane >> 3) & 3);
+  const __amdgpu_buffer_rsrc_t ars = rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t brs = rsrc(p.b, p.b_bytes);
+  unsigned hoff[HL];
+  char* hdst[HL];
+#pragma unroll
+  for (int j = 0; j < HL; ++j) {
+    const int g = j * NW + wid;
+    const int r = g * 16 + (lane >> 2);
+    const int hy = r / W2P, hx = r - hy * W2P;
+    const int ih = oh0 - 1 + hy, iw = hx - 1;
+    const bool ok = g < HG && r < HROWS && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)W;
+    const int sh = p.ups ? ih >> 1 : ih, sw = p.ups ? iw >> 1 : iw;
+    hoff[j] = ok ? (unsigned)((((img * p.Hs + sh) * p.Ws + sw) * p.Cip + gcl * 8) * 2) : OOB;
+    hdst[j] = g < HG ? halo + g * 16 * RS : scratch;  // + the buffer offset of the chunk
+  }
+  unsigned boff[BL];
+  int bdst[BL];
+#pragma unroll
+  for (int j = 0; j < BL; ++j) {
+    const int g = j * NW + wid;
+    const int n = n0 + g * 16 + (lane >> 2);
+    boff[j] = g < G ? (unsigned)(((long)n * p.K + gcl * 8) * 2) : OOB;
+    bdst[j] = g < G ? g * 16 * RS : -1;
+  }
+  const int nsteps = nch * 9;
+  // weight tile of step s = (chunk c, tap t) -> ring slot s % RING; K offset (bytes) in soffset;
+  // the steps past the end re-load the last tile (into a slot nobody reads again)
+  auto b_issue = [&](int s, int slot) {
+    const int ss = s < nsteps ? s : nsteps - 1;
+    const int c = c_beg + ss / 9, t = ss - (ss / 9) * 9;
+    const int soff = (t * p.Cip + c * 32) * 2;
+#pragma unroll
+    for (int j = 0; j < BL; ++j) glds16s(brs, bdst[j] >= 0 ? ring + slot * BB + bdst[j] : scratch, boff[j], soff);
+  };
+  auto h_issue = [&](int j, int chunk, int buf) {
+    glds16s(ars, hdst[j] == scratch ? scratch : hdst[j] + buf * HB, hoff[j], chunk * RS);
+  };
+
+  // fragment addresses: A of (tap ky,kx), fragment i = abase[buf][kx] + ((ky + 16i / W) * W2P + 16i % W) * RS
+  int abase[2][3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const int lo = (fr + kx) * RS + ((fq ^ (((fr + kx) >> 1) & 3)) << 4);
+    abase[0][kx] = lds_addr(halo) + (wm0 / W) * W2P * RS + lo;
+    abase[1][kx] = abase[0][kx] + HB;
+  }
+  const int bbase = lds_addr(ring) + (wn0 + fr) * RS + ((fq ^ ((fr >> 1) & 3)) << 4);
+
+  i32x4 iacc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) iacc[i][j] = (i32x4){0, 0, 0, 0};
+
+  // prologue: chunk 0's halo and weight tiles 0 .. RING-2; wait for the halo and tile 0
+#pragma unroll
+  for (int j = 0; j < HL; ++j) h_issue(j, c_beg, 0);
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u) b_issue(u, u);
+  wait_vm<BL * (RING - 2)>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  f16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+  // reads of step (tap t, ring slot `slot`, halo buffer hbuf) in the order phase 1 / 2 consume them
+  auto read_frags = [&](int hbuf, int t, int slot, f16x8 (&af)[TM], f16x8 (&bf)[TN], int k) {
+    if (QD_HALO_ABL & 16) return;  // diagnostic build: no fragment reads in the K loop
+    // k-th read of the step: B0..B(TN-1) first (phase 1 uses all columns), then A0..A(TM-1)
+    const int ky = t / 3, kx = t % 3;
+    if (k < TN) bf[k] = lds_read16(bbase + slot * BB + k * 16 * RS);
+    else {
+      const int i = k - TN;
+      af[i] = lds_read16(abase[hbuf][kx] + ((ky + 16 * i / W) * W2P + (16 * i) % W) * RS);
+    }
+  };
+  auto mfma = [&](int i, int j, const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
+    if (QD_HALO_ABL & 1) {  // diagnostic build: operands kept live, no MFMA
+      asm volatile("" ::"v"(af[i]), "v"(bf[j]));
+      return;
+    }
+    iacc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, bf[j]),
+                                                       __builtin_bit_cast(i32x4, af[i]), iacc[i][j], 0, 0, 0);
+  };
+  // halo instructions issued (after tile s+1) in steps s-RING+2 .. s-1: taps t-RING+2 .. t-1 < HL
+  auto hwin = [](int t) {
+    int n = 0;
+    for (int k = 1; k <= RING - 2; ++k) n += (t - k >= 0 && t - k < HL) ? 1 : 0;
+    return n;
+  };
+  // one step: fragments of step s in (ca, cb); reads of step s+1 into (na, nb).  The A fragments
+  // of step s+1 come from the current chunk's halo (landed and published at the previous chunk's
+  // last barrier) except at a chunk's last tap, so they are read in phase 1, before the barrier;
+  // the B fragments (weight tile s+1) after it - the LDS reads spread over both phases.
+  auto step = [&](int cl, int t, f16x8 (&ca)[TM], f16x8 (&cb)[TN], f16x8 (&na)[TM], f16x8 (&nb)[TN]) {
+    const int s = cl * 9 + t;
+    const bool next = t < 8 || cl + 1 < nch;
+    const int nbuf = t < 8 ? (cl & 1) : ((cl + 1) & 1), nt = t < 8 ? t + 1 : 0;
+    const int nslot = 9 % RING == 0 ? (t + 1) % RING : (s + 1) % RING;
+    // phase 1: rows 0 .. TM/2-1, then the A reads of step s+1 within a chunk (their registers
+    // overlap the fragments phase 1 has just consumed)
+#pragma unroll
+    for (int i = 0; i < TM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma(i, j, ca, cb);
+    if (t < 8) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) read_frags(nbuf, nt, nslot, na, nb, TN + i);
+    }
+    int k = 0;
+    if (next) {
+      // own loads of tile s+1 landed (issued in step s-RING+2); younger: the tiles s+2 .. s+RING-2
+      // and the halo groups of the steps since (taps t-RING+2 .. t-1 of this chunk, if < HL)
+      if (!(QD_HALO_ABL & 8)) {
+        wait_vm_c(BL * (RING - 3) + hwin(t));
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (!(QD_HALO_ABL & 2))
+        b_issue(s + RING - 1, RING % 9 == 0 || 9 % RING == 0 ? (t + RING - 1) % RING : (s + RING - 1) % RING);
+      if (!(QD_HALO_ABL & 4) && t < HL) h_issue(t, c_beg + cl + 1, (cl + 1) & 1);
+      // phase 2: rows TM/2 .. TM-1, the B reads of step s+1 (+ its A reads at a chunk's last tap)
+      constexpr int NR2 = TN + TM;
+      const int nr = t < 8 ? TN : NR2;
+      k = 0;
+#pragma unroll
+      for (int i = TM / 2; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (k < nr) {
+            read_frags(nbuf, nt, nslot, na, nb, k);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          }
+          ++k;
+          mfma(i, j, ca, cb);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        }
+#pragma unroll
+      for (; k < nr; ++k) read_frags(nbuf, nt, nslot, na, nb, k);
+    } else {
+#pragma unroll
+      for (int i = TM / 2; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma(i, j, ca, cb);
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < TM + TN; ++k) read_frags(0, 0, 0, a0, b0, k);
+#pragma nounroll
+  for (int cl = 0; cl < nch; ++cl) {
+    step(cl, 0, a0, b0, a1, b1);
+    step(cl, 1, a1, b1, a0, b0);
+    step(cl, 2, a0, b0, a1, b1);
+    step(cl, 3, a1, b1, a0, b0);
+    step(cl, 4, a0, b0, a1, b1);
+    step(cl, 5, a1, b1, a0, b0);
+    step(cl, 6, a0, b0, a1, b1);
+    step(cl, 7, a1, b1, a0, b0);
+    step(cl, 8, a0, b0, a1, b1);
+    // 9 steps per chunk: the next chunk's first fragments are in set 1
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a0[i] = a1[i];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b0[j] = b1[j];
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  f32x4 acc[TM][TN];
+  f16* const esm = reinterpret_cast<f16*>(smem);
+  if (QD_HALO_ABL & 32) {  // diagnostic build: no epilogue (one store keeps the sums live)
+    int v = 0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) v ^= iacc[i][j][0] ^ iacc[i][j][3];
+    if (v == 0x7fffffff) p.y[threadIdx.x] = (f16)1.f;
+    return;
+  }
+  if (p.splits > 1) {
+    i8_scale<TM, TN, true>(p, iacc, acc, m0, n0, wm0, wn0);
+    gemm_epilogue<BM, BN, NT, TM, TN, true, LDSB / 2>(p, acc, esm, m0, n0, wm0, wn0, split);
+  } else {
+    i8_scale<TM, TN, false>(p, iacc, acc, m0, n0, wm0, wn0);
+    gemm_epilogue<BM, BN, NT, TM, TN, false, LDSB / 2>(p, acc, esm, m0, n0, wm0, wn0, split);
+  }
+}
+
+template <int BN, int RING>
+static void launch_halo_i8(const GemmArgs& p, hipStream_t st) {
+  const int nwg = (p.M / 256) * (p.N / BN) * p.splits;
+  if (p.W == 64) k_conv_halo_i8<BN, 64, RING><<<nwg, 512, 0, st>>>(p);
+  else if (p.W == 32) k_conv_halo_i8<BN, 32, RING><<<nwg, 512, 0, st>>>(p);
+  else k_conv_halo_i8<BN, 16, RING><<<nwg, 512, 0, st>>>(p);
+}
+
 // halo kernel applicability: 3x3 / stride 1 / pad 1, 64-channel chunks, whole-row 256-pixel tiles
-static bool halo_ok(const GemmArgs& p, int bn) {
-  return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && p.Cip % 64 == 0 && p.N % bn == 0 &&
+static bool halo_ok(const GemmArgs& p, int bn, int chunk = 64) {
+  return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && p.Cip % chunk == 0 && p.N % bn == 0 &&
          (p.W == 16 || p.W == 32 || p.W == 64) && p.Ho == p.H && p.Wo == p.W && p.H % (256 / p.W) == 0 &&
          (p.rows_per_sample % 64 == 0);
 }
@@ -1625,9 +1941,9 @@ static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register
 extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
                  (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (variant >= 200 && variant <= 203) || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123) ||
-                 (variant >= 130 && variant <= 134),
+                 (variant >= 130 && variant <= 134) || (variant >= 140 && variant <= 144),
              "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200-203 halo conv, "
-             "300-304 ping-pong (int8: 130-134)");
+             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-144)");
   g_force = variant;
   return 0;
 }
@@ -1787,6 +2103,7 @@ static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t 
 // Dequant is the tile loaders' half(q * s) and the epilogue rounds like gemm_epilogue
 // (half(acc + bias) -> GELU-tanh -> + residual); only the fp32 summation order differs.
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef f16 f16x2 __attribute__((ext_vector_type(2)));
 
 template <int BFMT>
@@ -2024,6 +2341,7 @@ static int check_common(const GemmArgs& p, int fmt) {
                                              !(p.epi & (QD_EPI_GEGLU | QD_EPI_GELU_TANH))),
              "post-residual amax needs QD_EPI_AMAX | QD_EPI_RESIDUAL, no GEGLU / GELU-tanh");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
+  QD_REQUIRE((double)p.M * p.ldy * 2 < 2147483648.0, "output exceeds the 2 GiB buffer-addressing range");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
   const double wbytes = (double)p.N * p.K * (fmt == QD_WFMT_F16 ? 2 : fmt == QD_WFMT_I8 ? 1 : 0.5);
@@ -2177,6 +2495,24 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // variant: qd_gemm_force 110..115 (DMA variants 10-15, the 64-B-row family), else a default by
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu) {
+  if (g_force >= 140 && g_force <= 144 && !geglu && Kh % 288 == 0) {
+    // int8 halo conv (applicability checked at launch): 140 BN 160 / 141 BN 128 (3-slot weight
+    // ring), 142 / 143 / 144 BN 160 with 4 / 5 / 6 slots; K splits over whole 64-code chunks
+    // while the blocks fit one resident round (1 block / CU)
+    const int bn = g_force == 141 ? 128 : 160;
+    if (N % bn == 0 && M % 256 == 0) {
+      const long tiles_mn = (long)(M / 256) * (N / bn);
+      const int nc = Kh / 288;
+      Plan pl{2, 256, bn, g_force - 140, 1, nc};
+      for (int sp = 2; sp <= nc; ++sp) {
+        if (nc % sp != 0) continue;
+        if (tiles_mn * sp > 256) break;
+        pl.splits = sp;
+        pl.kps = nc / sp;
+      }
+      return pl;
+    }
+  }
   if (g_force >= 130 && g_force <= 134) {
     // ping-pong: wave rows 128 (BN >= 192) or 64 must lie in one sample for the amax epilogue
     const int bnp = kPpBn[g_force - 130];
@@ -2213,18 +2549,33 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
 template <int AMODE>
 static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0);
+  if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 32))) {  // int8 halo conv not applicable
+    const int f = g_force;
+    g_force = -1;
+    pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0);
+    g_force = f;
+  }
   if (pl.splits > 1 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N))) {
     pl.splits = 1;
-    pl.kps = p.K;
+    pl.kps = pl.kind == 2 ? p.K / 288 : p.K;
   }
   p.splits = pl.splits;
   p.kps = pl.kps;
+  auto halo = [&]() {  // the kernel reads p.splits itself (int32 slabs when split)
+    if (pl.var == 2) launch_halo_i8<160, 4>(p, st);
+    else if (pl.var == 3) launch_halo_i8<160, 5>(p, st);
+    else if (pl.var == 4) launch_halo_i8<160, 6>(p, st);
+    else if (pl.bn == 160) launch_halo_i8<160, 3>(p, st);
+    else launch_halo_i8<128, 3>(p, st);
+  };
   if (pl.splits == 1) {
-    if (pl.kind == 3) launch_pp_i8<AMODE, false>(p, pl.bn, st);
+    if (pl.kind == 2) halo();
+    else if (pl.kind == 3) launch_pp_i8<AMODE, false>(p, pl.bn, st);
     else launch_i8<AMODE, false>(p, pl.var, st);
   } else {
     p.part = ws;
-    if (pl.kind == 3) launch_pp_i8<AMODE, true>(p, pl.bn, st);
+    if (pl.kind == 2) halo();
+    else if (pl.kind == 3) launch_pp_i8<AMODE, true>(p, pl.bn, st);
     else launch_i8<AMODE, true>(p, pl.var, st);
     const int gx = (p.N + 255) / 256;
     if ((long)gx * ((p.M + 15) / 16) >= 512) k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
@@ -2248,6 +2599,7 @@ static int check_i8(const GemmArgs& p) {
                                              !(p.epi & (QD_EPI_GEGLU | QD_EPI_GELU_TANH))),
              "post-residual amax needs QD_EPI_AMAX | QD_EPI_RESIDUAL, no GEGLU / GELU-tanh");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(p.y) & 15) == 0, "y must be 16-B aligned");
+  QD_REQUIRE((double)p.M * p.ldy * 2 < 2147483648.0, "output exceeds the 2 GiB buffer-addressing range");
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
   QD_REQUIRE((double)p.N * p.K * 2 < 2147483648.0, "weight exceeds the 2 GiB buffer-addressing range");

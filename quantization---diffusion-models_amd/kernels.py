@@ -407,6 +407,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 # split gives identical bits - the tuner below only picks the fastest.
 I8_VARIANTS = (110, 111, 112, 113, 114, 115,   # qd_gemm_force ids: LDS-DMA variants 10-15 (64-B rows)
                130, 131, 132, 133, 134)  # ping-pong 256 x {256, 320, 192, 160, 128}
+I8_HALO_VARIANTS = (140, 141, 142, 143, 144)  # 3x3 conv, activation halo staged once per 64-code chunk (BN 160 / 128; 142-144 deeper weight rings)
 
 
 def quant_rows_i8(x2d, out=None, scales=None):
@@ -602,7 +603,8 @@ def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, 
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        c = _choose(key, list(I8_VARIANTS), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+        cands = list(I8_VARIANTS) + (list(I8_HALO_VARIANTS) if (kh, kw, stride, pad) == (3, 3, 1, 1) else [])
+        c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
     launch(c if c is not None else -1, out, amax, epi, False)

@@ -27,8 +27,15 @@ x = torch.randn(8, 64, 64, 320, device=dev).half()
 wt = (torch.randn(320, 3, 3, 320, device=dev) * 0.02).half()
 bias = torch.zeros(320, device=dev).half()
 am = torch.empty(8 * 320, device=dev)
-K.force_gemm(int(os.environ.get("QD_HALO_VAR", "200")))
-fn = lambda: K.conv2d_nhwc(x, wt, 320, 1, 1, bias=bias, amax=am)  # noqa: E731
+var = int(os.environ.get("QD_HALO_VAR", "200"))
+K.force_gemm(var)
+if var >= 140:  # the int8 halo conv (int8-MFMA mode) on the same shape
+    xq, sa = K.quant_samples_i8(x)
+    wq, sw16, _ = K.weight_quant(wt.view(320, -1).contiguous(), 9 * 320, 8, want_dq=False)
+    wq, sw = wq.view(320, 3, 3, 320), sw16.float().view(-1).contiguous()
+    fn = lambda: K.conv2d_i8(xq, sa, wq, sw, 320, 1, 1, bias=bias)  # noqa: E731
+else:
+    fn = lambda: K.conv2d_nhwc(x, wt, 320, 1, 1, bias=bias, amax=am)  # noqa: E731
 for _ in range(5):
     fn()
 ts = []
@@ -40,4 +47,4 @@ for _ in range(3):
     e1.record()
     e1.synchronize()
     ts.append(e0.elapsed_time(e1) / 20 * 1e3)
-print(f"abl {b:>2}: {min(ts):7.1f} us", flush=True)
+print(f"var {var} abl {b:>2}: {min(ts):7.1f} us", flush=True)

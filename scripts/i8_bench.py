@@ -27,6 +27,7 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true", help="also time every forced int8 conv variant")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -48,6 +49,20 @@ def main():
         flops = 2.0 * n * h * w * co * k * k * ci / (s * s)
         ch = [v for kk, v in K.gemm_choices().items() if kk[0] == "conv_i8" and kk[1:6] == (n, h, w, ci, co)]
         print(f"({n},{h},{w},{ci},{co},{k}) x{cnt}: {tf:8.1f} | {ti:8.1f} | {tf / ti:5.2f} | {flops / ti / 1e6:7.1f} | {ch}")
+        if a.sweep:
+            ref = K.conv2d_i8(xq, sa, wq, sw, ci, s, k // 2, bias=b)
+            row = []
+            for v in K.I8_VARIANTS + K.I8_HALO_VARIANTS:
+                K.force_gemm(v)
+                try:
+                    tv = timeit(lambda: K.conv2d_i8(xq, sa, wq, sw, ci, s, k // 2, bias=b), a.iters)
+                    same = torch.equal(K.conv2d_i8(xq, sa, wq, sw, ci, s, k // 2, bias=b), ref)
+                    row.append(f"{v}:{tv:.1f}{'' if same else '(DIFF)'}")
+                except RuntimeError as e:
+                    row.append(f"{v}:err")
+                finally:
+                    K.force_gemm(None)
+            print("    sweep us:", " ".join(row), flush=True)
     lins = [(32768, 320, 320), (32768, 2560, 320), (32768, 320, 1280), (8192, 640, 640), (8192, 5120, 640),
             (2048, 1280, 1280), (2048, 10240, 1280), (8192, 640, 2560), (616, 320, 768)]
     print("linear (M,N,K): f16 us | i8 us | speedup | i8 TOPS")

@@ -104,8 +104,10 @@ def _geglu_amax(k, dev):
 @pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups", [(64, 64, 3, 1, 16, False), (64, 128, 3, 2, 16, False),
                                                         (128, 64, 1, 1, 8, False), (64, 64, 3, 1, 8, True),
                                                         (320, 320, 3, 1, 32, False), (640, 640, 3, 1, 16, False),
-                                                        (1280, 1280, 3, 1, 8, False), (960, 320, 3, 1, 16, False)])
-@pytest.mark.parametrize("variant", I8_FORCE)
+                                                        (1280, 1280, 3, 1, 8, False), (960, 320, 3, 1, 16, False),
+                                                        (320, 320, 3, 1, 64, False), (640, 640, 3, 1, 32, False),
+                                                        (1280, 1280, 3, 1, 16, False), (640, 320, 3, 1, 32, True)])
+@pytest.mark.parametrize("variant", I8_FORCE + [140, 141, 142, 143, 144])
 def test_conv2d_i8_bit_exact(cin, cout, ksz, stride, hw, ups, variant, dev):
     k = K()
     rng = np.random.default_rng(cin * 7 + cout + ksz)
