@@ -456,11 +456,14 @@ def mmdit_dominant_roofline(model, dev, s, iters=10):
     tflops = 2.0 * m * n * k / (ms * 1e-3) / 1e12
     f8 = getattr(layer, "fp8_act", False)
     peak = PEAK_F8_TFLOPS if f8 else PEAK_F16_TFLOPS
+    from qdiff import kernels as K
+    ran = sorted({key[-1][ch[0]] for key, ch in K.gemm_choices().items()
+                  if ch is not None and key[0] == "linear" and key[1:4] == (m, n, k)})
     return {"bound": "mfma", "achieved": round(tflops, 1), "peak": peak, "unit": "TFLOP/s",
             "frac": round(tflops / peak, 4), "traffic": None,
             "kernel": f"ff.net.0.proj GEMM M={m} N={n} K={k} "
                       + ("(e4m3 x e4m3, v_mfma_scale_f32_16x16x128_f8f6f4, per-token quant included)" if f8 else
-                         f"({getattr(layer, 'qfmt', 'f16')} weights)"),
+                         f"({getattr(layer, 'qfmt', 'f16')} weights, {'/'.join(ran) or '?'} operand ran)"),
             "avg_us": round(ms * 1e3, 2)}
 
 

@@ -127,6 +127,11 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
  * weights only; quantized formats keep the planner's register-staged choice). */
 int qd_gemm_force(int variant);
 
+/* Measurement knob (process-global): rows per thread of the streaming GroupNorm statistics /
+ * apply passes (qd_groupnorm*, 0 = the built-in rule).  Changes the workspace size, so query
+ * qd_groupnorm_workspace after setting it. */
+int qd_gn_geom_force(int stats_rows_per_thread, int apply_rows_per_thread);
+
 /* fp32 elements of split-K workspace the GEMM plans for this shape (0: runs unsplit).  Pass
  * at least that much as (ws, ws_elems) to qd_linear_fwd / qd_conv2d_fwd (conv: M = N*Ho*Wo,
  * K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo); with less (or NULL) the call runs unsplit. */

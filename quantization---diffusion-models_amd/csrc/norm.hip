@@ -138,6 +138,15 @@ struct GnGeom {
   int bx, by, gx, z, rpb;  // apply pass
   int bys, zs, rpbs;       // stats pass: 256-thread blocks, up to 16 rows per thread
 };
+// measurement knob (qd_gn_geom_force): rows per thread of the statistics / apply passes, 0 = the
+// rule below
+static int g_gn_srpt = 0, g_gn_arpt = 0;
+extern "C" int qd_gn_geom_force(int stats_rows_per_thread, int apply_rows_per_thread) {
+  g_gn_srpt = stats_rows_per_thread > 0 ? stats_rows_per_thread : 0;
+  g_gn_arpt = apply_rows_per_thread > 0 ? apply_rows_per_thread : 0;
+  return 0;
+}
+
 static GnGeom gn_geom(int n, int hw, int c) {
   GnGeom g;
   const int chunks = c / 8;
@@ -147,11 +156,13 @@ static GnGeom gn_geom(int n, int hw, int c) {
   g.rpb = g.by * 4;  // >= 4 rows per thread, more blocks while the grid is small
   while (g.rpb > g.by && (long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) < 2048) g.rpb /= 2;
   while ((long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) > 8192) g.rpb *= 2;
+  if (g_gn_arpt) g.rpb = g.by * g_gn_arpt;
   g.z = (hw + g.rpb - 1) / g.rpb;
   // stats: 8 loads in flight per thread, 16 rows per thread while the grid keeps >= 512 blocks
   g.bys = g.by;
   g.rpbs = g.bys * 16;
   while (g.rpbs > g.bys * 8 && (long)g.gx * n * ((hw + g.rpbs - 1) / g.rpbs) < 256) g.rpbs /= 2;
+  if (g_gn_srpt) g.rpbs = g.bys * g_gn_srpt;
   g.zs = (hw + g.rpbs - 1) / g.rpbs;
   return g;
 }

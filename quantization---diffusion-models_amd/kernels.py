@@ -33,6 +33,20 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _cadd_ld(t, n, c, name="cadd"):
+    """Leading dim of a per-(sample, channel) fp16 add; t may be a row-strided [N, C] view (e.g. a
+    column slice of a stacked projection) - the kernels read C values of each of its N rows."""
+    if t is None:
+        return 0
+    if t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.float16:
+        raise ValueError(f"{name} must be an fp16 [N, C] tensor with unit column stride")
+    if tuple(t.shape) != (n, c):
+        raise ValueError(f"{name} must be [N, C] = {[n, c]}, got {list(t.shape)}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP (cuda) tensor, got {t.device}")
+    return t.stride(0)
+
+
 def _chk(t, name, dtype=torch.float16):
     if not t.is_cuda:
         raise ValueError(f"{name} must be a HIP (cuda) tensor, got {t.device}")
@@ -194,7 +208,7 @@ def import_table(entries, overwrite=True):
     for k, c in entries:
         key = _tuplify(k)
         if overwrite or key not in _TUNE:
-            _TUNE[key] = tuple(c) if c is not None else None
+            _TUNE[key] = tuple(c) if isinstance(c, (list, tuple)) else c  # (op, variant) | int | None
             n += 1
     return n
 
@@ -212,9 +226,10 @@ def load_table(path, overwrite=True):
     return import_table(d["entries"], overwrite)
 
 
-# A committed table (tuned on an MI355X by scripts/tune_table.py) makes kernel choices - and
-# therefore results - reproducible across processes; shapes it does not cover are tuned at
-# their first eager call.  QD_GEMM_TABLE=<path> selects another file, QD_GEMM_TABLE=none none.
+# The committed table (tuned on an MI355X by scripts/tune_table.py over every GEMM / conv shape of
+# the bench configurations) makes kernel choices - and therefore results - reproducible across
+# processes (tests/test_gpu_determinism.py); shapes it does not cover are tuned at their first
+# eager call.  QD_GEMM_TABLE=<path> selects another file, QD_GEMM_TABLE=none none.
 _TABLE_PATH = os.environ.get("QD_GEMM_TABLE", os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                              "gemm_table.json"))
 if _TABLE_PATH.lower() != "none" and os.path.exists(_TABLE_PATH):
@@ -505,10 +520,7 @@ def groupnorm_nhwc_i8(x, groups, eps, gamma, beta, silu=False, x2=None, fq_in=No
     amax, bits, cadd, ld = None, 0, None, 0
     if fq_in is not None:
         amax, bits, cadd = fq_in
-        if cadd is not None:
-            if cadd.dim() != 2 or cadd.stride(1) != 1 or cadd.dtype != torch.float16:
-                raise ValueError("cadd must be an fp16 [N, C] tensor with unit column stride")
-            ld = cadd.stride(0)
+        ld = _cadd_ld(cadd, n, c)
     if x2 is not None:
         _chk(x2, "x2")
     _lib.call("qd_groupnorm_i8", _p(x), _p(x2), c1 if x2 is not None else c, _p(amax), bits, _p(cadd), ld, n, hw, c,
@@ -618,11 +630,7 @@ def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
     n, c = y.shape[0], y.shape[-1]
     hw = y.numel() // (n * c)
     o = out if out is not None else _empty(y.shape, y.dtype, y.device)
-    ld = 0
-    if chan_add is not None:
-        if chan_add.dim() != 2 or chan_add.stride(1) != 1 or chan_add.dtype != torch.float16:
-            raise ValueError("chan_add must be an fp16 [N, C] tensor with unit column stride")
-        ld = chan_add.stride(0)
+    ld = _cadd_ld(chan_add, n, c, "chan_add")
     _lib.call("qd_fq_finalize", _p(y), _p(amax), n, hw, c, n_bits, _p(residual), _p(chan_add), ld, _p(o),
               _stream())
     return o
@@ -647,11 +655,7 @@ def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, o
         if x2 is not None:
             raise ValueError("fq_in GroupNorm takes a single source")
         amax, bits, cadd = fq_in
-        ld = 0
-        if cadd is not None:
-            if cadd.dim() != 2 or cadd.stride(1) != 1 or cadd.dtype != torch.float16:
-                raise ValueError("cadd must be an fp16 [N, C] tensor with unit column stride")
-            ld = cadd.stride(0)
+        ld = _cadd_ld(cadd, n, c)
         _lib.call("qd_groupnorm_fq_in", _p(x), _p(amax), bits, _p(cadd), ld, n, hw, c, groups, float(eps),
                   _p(gamma), _p(beta), 1 if silu else 0, q_bits, _p(out), _p(ws), _stream())
         return out
@@ -667,12 +671,8 @@ def groupnorm_fin(y, amax, bits, residual, groups, eps, gamma, beta, silu=False,
     _chk(y, "y")
     if residual is not None:
         _chk(residual, "residual")
-    ld = 0
-    if cadd is not None:
-        if cadd.dim() != 2 or cadd.stride(1) != 1 or cadd.dtype != torch.float16:
-            raise ValueError("cadd must be an fp16 [N, C] tensor with unit column stride")
-        ld = cadd.stride(0)
     n, c = y.shape[0], y.shape[-1]
+    ld = _cadd_ld(cadd, n, c)
     hw = y.numel() // (n * c)
     x = _empty(y.shape, torch.float16, y.device)
     h = _empty(y.shape, torch.float16, y.device)

@@ -274,3 +274,18 @@ def test_awq_clip_avoids_diffusers_qk_names():
         assert clip_avoided(n), n
     for n in ("attn1.to_v", "attn1.to_out.0", "ff.net.0.proj", "ff.net.2", "attn.add_v_proj"):
         assert not clip_avoided(n), n
+
+
+def test_committed_gemm_table_loads():
+    """The MI355X-tuned GEMM table (scripts/tune_table.py) is committed, well-formed and loaded at
+    import, so every process runs the same kernel variant per shape (VERDICT r2 #7)."""
+    import json
+    import os
+    from qdiff import kernels as K
+    path = os.path.join(os.path.dirname(K.__file__), "gemm_table.json")
+    d = json.load(open(path))
+    assert d["device_arch"].startswith("gfx950") and len(d["entries"]) > 500
+    kinds = {e[0][0] for e in d["entries"]}
+    assert {"conv", "linear", "conv_i8", "linear_i8", "linear_fp8"} <= kinds
+    if os.environ.get("QD_GEMM_TABLE", "").lower() != "none":
+        assert len(K.gemm_choices()) >= len(d["entries"])

@@ -605,7 +605,7 @@ def test_groupnorm_fq_in_matches_finalize_then_norm(bits, with_cadd, hw, dev):
     n, c = 2, 640
     y = (torch.randn(n, hw, c, generator=g) * 1.5).half().to(dev)
     amax = y.float().abs().amax(dim=1).reshape(-1).contiguous() if bits else None
-    big = (torch.randn(n, 2 * c, generator=g) * 0.3).half().to(dev)
+    big = (torch.randn(n, 3 * c, generator=g) * 0.3).half().to(dev)
     cadd = big[:, 100 * 8: 100 * 8 + c] if with_cadd else None  # row-strided view, like the stacked temb
     gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
     bet = (0.1 * torch.randn(c, generator=g)).half()
