@@ -234,7 +234,7 @@ def linear_families():
     dequantized copy through the LDS-DMA / ping-pong families; int8-MFMA linears separately."""
     from qdiff import kernels as K
     fam = {}
-    for key, ch in K.gemm_choices().items():
+    for key, ch in K.gemm_choices(used_only=True).items():
         if ch is None:
             continue
         if key[0] == "linear_i8":
@@ -247,6 +247,28 @@ def linear_families():
             continue
         fam[name] = fam.get(name, 0) + 1
     return fam
+
+
+def weight_footprint(model):
+    """HBM bytes of the denoiser's linear weights per operand form (MB): the packed-int4 codes +
+    group scales ([N][K/g] and the [K/g][N] copy the LDS-DMA stages read) vs the module's fp16
+    dequantized buffer (the reference's `weight`, which the tuner may also stream), and which
+    operand the linears' chosen kernels actually read; conv weights are fp16 [Co][kh][kw][Ci]."""
+    from qdiff import kernels as K
+    from qdiff.fake_quant import WxAxLinear
+    codes = f16 = 0
+    for m in model.pipeline.unet.modules() if hasattr(model.pipeline, "unet") else model.pipeline.transformer.modules():
+        if isinstance(m, WxAxLinear) and m.qcodes is not None and m.qfmt == "i4":
+            codes += m.qcodes.numel() + 2 * m.qscales.numel() * 2
+            f16 += m.weight.numel() * 2
+    ran = {"codes": 0, "f16 buffer": 0}
+    for key, ch in K.gemm_choices(used_only=True).items():
+        if key[0] == "linear" and key[-1][0] == "i4" and ch is not None:
+            ran["codes" if key[-1][ch[0]] == "i4" else "f16 buffer"] += 1
+    return {"int4_codes_and_scales_MB": round(codes / 2**20, 1), "fp16_buffer_MB": round(f16 / 2**20, 1),
+            "linear_shapes_by_operand": ran,
+            "operand_policy": "int4 codes only (default)" if K.W4_CODES_ONLY else
+            "tuned per shape: int4 codes vs the fp16 dequantized buffer (QD_W4_OPERAND=tuned)"}
 
 
 def pmc_traffic(variant=None):
@@ -421,6 +443,8 @@ def main():
                                                "per 512^2 image (SURVEY 8d)"},
             "linear_kernel_choice": linear_families(),
         }
+        if args.mode == "w4a16":
+            line["weight_stream"] = weight_footprint(model)
         if not args.no_e2e:
             log("end to end (text encoder + VAE decode) ...")
             line["end_to_end"] = end_to_end(model, out[:B], prompts[:B], dt / args.steps)
@@ -576,7 +600,10 @@ def main_sd35(args, model, rank, world, dev, log):
             "path_roofline": {"achieved": round(path_tflops / world, 1), "peak": PEAK_F16_TFLOPS,
                               "unit": "TFLOP/s per GPU", "frac": round(path_tflops / world / PEAK_F16_TFLOPS, 4),
                               "flop_per_image": round(2 * args.denoise_steps * gflop * 1e9)},
+            "linear_kernel_choice": linear_families(),
         }
+        if args.mode == "w4a16":
+            line["weight_stream"] = weight_footprint(model)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
             line["cpu_baseline"] = cpu_baseline_sd35(min(args.cpu_threads, len(os.sched_getaffinity(0))), cfg, s, sc,

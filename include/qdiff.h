@@ -44,7 +44,7 @@ extern "C" {
 /* weight storage formats of the GEMM B operand */
 #define QD_WFMT_F16 0   /* dequantized fp16 (the reference's own buffer format) */
 #define QD_WFMT_I8 1    /* int8 codes [N][K] + fp16 scales [N][K/group] */
-#define QD_WFMT_I4 2    /* int4 codes packed 2/byte along K (low nibble = even k) + scales */
+#define QD_WFMT_I4 2    /* int4 codes packed 8/dword along K (qd_pack_int4 layout) + scales */
 
 int qd_version(void);
 const char* qd_last_error(void);
@@ -87,7 +87,10 @@ int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, 
  * [2, 16] as the reference accepts any width; codes must be NULL above 8 bits. */
 int qd_weight_quant(const void* w, int rows, int cols, int group, int n_bits, int8_t* codes,
                     void* scales, void* w_dq, void* stream);
-/* pack int8 codes in [-8, 7] to int4, 2 per byte along cols (cols even). */
+/* pack int8 codes q in [-8, 7] to int4, 8 per little-endian dword along cols (cols % 8 == 0):
+ * in the dword of codes k = 8i .. 8i + 7, nibble j holds q(8i + 2j) + 8 and nibble j + 4 holds
+ * q(8i + 2j + 1) + 8, so (w >> 4j) & 0x000F000F | 0x64006400 is the fp16 pair (1024 + c, 1024 + c')
+ * of two consecutive k (the GEMM's packed dequant).  `packed` 4-B aligned. */
 int qd_pack_int4(const int8_t* codes, int rows, int cols, uint8_t* packed, void* stream);
 /* conv weight [Co][Ci][kh][kw] -> GEMM B layout [Co][kh][kw][Ci_pad] (zero-padded Ci). */
 int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pad, void* out,
@@ -112,19 +115,23 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
- * wfmt: QD_WFMT_*; wscale [N][K/group] fp16 for I8/I4.  lda/ldy in elements.
+ * wfmt: QD_WFMT_*; wscale [N][K/group] fp16 for I8/I4.  wscale_t (I4 only, optional, 16-B
+ * aligned): the same scales as [K/group][N]; with it the int4 codes also run in the LDS-DMA /
+ * ping-pong families (qd_gemm_force 110..115, 300..304), dequantized from LDS per fragment with the
+ * register tile's rounding (bit-identical results).  lda/ldy in elements.
  * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32).
  * M <= 4 without AMAX / GEGLU runs a weight-stream GEMV (same dequant and epilogue rounding;
  * environment QD_NO_GEMV, read at the first call, keeps the tile GEMM for every M). */
 int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
-                  const void* wscale, int group, const void* bias, const void* residual,
-                  void* y, int N, int ldy, int epi, float* amax, int rows_per_sample,
-                  float* ws, long ws_elems, void* stream);
+                  const void* wscale, const void* wscale_t, int group, const void* bias,
+                  const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                  int rows_per_sample, float* ws, long ws_elems, void* stream);
 
 /* Tuning / test knob (process-global, not thread-safe): force the GEMM kernel family of every
  * following qd_linear_fwd / qd_conv2d_fwd.  -1 = planner's choice (default); 0..3 = the
  * register-staged tiles 128x160, 128x128, 128x64, 64x64; 100 + i = LDS-DMA variant i (F16
- * weights only; quantized formats keep the planner's register-staged choice). */
+ * weights; packed int4 with wscale_t: the BK-32 variants 110..115 and ping-pong 300..304; other
+ * quantized formats keep the planner's register-staged choice). */
 int qd_gemm_force(int variant);
 
 /* Measurement knob (process-global): rows per thread of the streaming GroupNorm statistics /

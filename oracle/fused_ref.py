@@ -122,11 +122,14 @@ def dequant_weight(weight, wfmt, scales, group, weight_f16):
         return weight_f16.to(F16)
     if wfmt == "i8":
         q = weight.float()
-    else:  # packed int4, low nibble = even k
-        b = weight.to(torch.int16) & 0xFF
-        lo, hi = b & 0xF, (b >> 4) & 0xF
-        q = torch.stack([lo, hi], -1).reshape(weight.shape[0], -1).float()
-        q = torch.where(q >= 8, q - 16, q)
+    else:  # packed int4 (libqdiff qd_pack_int4): per dword of 8 codes, nibble j = q(2j) + 8,
+        # nibble j + 4 = q(2j + 1) + 8
+        b = weight.to(torch.int64) & 0xFF
+        n = b.shape[0]
+        b = b.reshape(n, -1, 4)
+        w = b[..., 0] | (b[..., 1] << 8) | (b[..., 2] << 16) | (b[..., 3] << 24)
+        sh = torch.tensor([0, 16, 4, 20, 8, 24, 12, 28], dtype=torch.int64)
+        q = (((w[..., None] >> sh) & 0xF) - 8).reshape(n, -1).float()
     n, k = q.shape
     s = scales.float().repeat_interleave(group, dim=1)[:, :k]
     return (q * s).half()

@@ -31,7 +31,7 @@ SIGNATURES = {
     "qd_weight_quant": [P, I, I, I, I, P, P, P, P],
     "qd_pack_int4": [P, I, I, P, P],
     "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
-    "qd_linear_fwd": [P, I, I, I, P, I, P, I, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
+    "qd_linear_fwd": [P, I, I, I, P, I, P, P, I, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
     "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, I, P, P],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],

@@ -84,7 +84,10 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   f16* ob = o + (long)b * sq * ldo + h * d;
   const int dchunks = d >> 3;
 
-  // B operand of S^T: Q[q = q0 + 16*(NQ*wid + g) + fr][dd = 32s + 8fq .. +8]
+  // B operand of S^T: Q[q = q0 + 16*(NQ*wid + g) + fr][dd = 32s + 8fq .. +8], pre-multiplied by
+  // scale * log2(e) (one fp16 rounding per element), so the MFMA chain - seeded with -m, the
+  // lane's running max - leaves the exponent s * scale * log2(e) - m ready for exp2: no per-score
+  // fma in the loop (the softmax VALU issue bounds this kernel at head_dim 40).
   f16x8 qf[NQ][DP / 32];
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
@@ -94,6 +97,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
       const int c = s * 4 + fq;
       f16x8 val = {};
       if (qrow < sq && c < dchunks) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) val[e] = (f16)((float)val[e] * scale_log2);
       qf[g][s] = val;
     }
   }
@@ -150,12 +155,15 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   };
 
   f32x4 oacc[NQ][TD];
-  float mrow[NQ];  // running max of this lane's queries (log2 domain)
+  float mrow[NQ];    // running max of this lane's queries (log2 domain); 0 until the first tile sets it
+  f32x4 mneg[NQ];    // -mrow broadcast: the seed accumulator of the S^T chain
+  bool first = true; // the first tile always moves the max (wave-uniform)
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
 #pragma unroll
     for (int j = 0; j < TD; ++j) oacc[g][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    mrow[g] = -INFINITY;
+    mrow[g] = 0.f;
+    mneg[g] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
 
   // per-lane LDS read offsets (elements, within a buffer)
@@ -172,11 +180,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   const int ntiles = (skv + KV_T - 1) / KV_T;
   auto tile = [&](const f16* ks, int kv0) {
     // ---- S^T[kv][q] = K Q^T: tile jt holds kv = 16jt + 4fq + r for query fr ----
+    // ---- S'^T = K (c Q)^T - m: tile jt holds kv = 16jt + 4fq + r for query fr, log2 domain ----
     f32x4 sacc[NQ][4];
-#pragma unroll
-    for (int g = 0; g < NQ; ++g)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) sacc[g][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DP / 32; ++s)
 #pragma unroll
@@ -184,7 +189,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
         const f16x8 kf = *reinterpret_cast<const f16x8*>(ks + kread[j][s]);
 #pragma unroll
         for (int g = 0; g < NQ; ++g)
-          sacc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[g][s], sacc[g][j], 0, 0, 0);
+          sacc[g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[g][s], s == 0 ? mneg[g] : sacc[g][j], 0, 0, 0);
       }
     if (kv0 + KV_T > skv) {
 #pragma unroll
@@ -221,23 +226,30 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(mrow[g], mx * scale_log2);
       // deferred rescale: the running max is only moved when some lane's max grew by more than
-      // 8 (log2 domain), so P stays <= 2^8 (exact in fp16's range, same relative rounding) and
-      // the O / denominator rescale is skipped on almost every tile after the first.  The
-      // decision precedes this tile's exponentials, so nothing at the old scale is pending.
-      if (__any(mnew > mrow[g] + 8.0f)) {  // wave-uniform; lanes that did not grow get alpha = 1
-        const float alpha = __builtin_amdgcn_exp2f(mrow[g] - mnew);
+      // 8 (log2 domain; mx is already relative to it), so P stays <= 2^8 (exact in fp16's range,
+      // same relative rounding) and the O / denominator rescale is skipped on almost every tile
+      // after the first.  The decision precedes this tile's exponentials, so nothing at the old
+      // scale is pending; a moved max shifts this tile's exponents by the growth d.
+      if (first || __any(mx > 8.0f)) {  // wave-uniform; lanes that did not grow get d = 0, alpha = 1
+        const float d = first ? mx : fmaxf(mx, 0.f);
+        if (!first) {  // (O is still zero on the first tile, where exp2(-d) may overflow)
+          const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-        for (int j = 0; j < TD; ++j) oacc[g][j] *= alpha;
-        mrow[g] = mnew;
+          for (int j = 0; j < TD; ++j) oacc[g][j] *= alpha;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sacc[g][j] -= d;
+        mrow[g] += d;
+        mneg[g] = (f32x4){-mrow[g], -mrow[g], -mrow[g], -mrow[g]};
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          pf[g][j >> 1][(j & 1) * 4 + r] = (f16)__builtin_amdgcn_exp2f(fmaf(sacc[g][j][r], scale_log2, -mrow[g]));
+          pf[g][j >> 1][(j & 1) * 4 + r] = (f16)__builtin_amdgcn_exp2f(sacc[g][j][r]);
     }
+    first = false;
     // ---- O^T[d][q] += V^T P^T ----
 #pragma unroll
     for (int s = 0; s < 2; ++s)

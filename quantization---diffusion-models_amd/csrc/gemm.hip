@@ -44,6 +44,7 @@ struct GemmArgs {
   int lda;
   const void* b;
   const f16* bscale;
+  const f16* bscale_t;  // the same group scales as [K / group][N] (int4 LDS-DMA families), or null
   int group;
   const f16* bias;
   const f16* res;
@@ -291,9 +292,8 @@ struct BLoader<BN, QD_WFMT_I4> {
       for (int cc = 0; cc < 4; ++cc) {
         f16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int nib = (w[cc] >> (4 * e)) & 0xf;
-          const int q = nib >= 8 ? nib - 16 : nib;
+        for (int e = 0; e < 8; ++e) {  // pair-interleaved offset-binary nibbles (qd_pack_int4)
+          const int q = (int)(((unsigned)w[cc] >> ((e & 1) * 16 + (e >> 1) * 4)) & 0xf) - 8;
           o[e] = (f16)((float)q * s[j]);
         }
         *reinterpret_cast<f16x8*>(lds + swz(row, 4 * hq + cc)) = o;
@@ -724,6 +724,87 @@ struct BDma {
   }
 };
 
+// ---- packed-int4 B operand in the LDS-DMA families ------------------------------------------
+// The codes go HBM -> LDS as they are stored (qd_pack_int4: BKT / 2 bytes per row and K step, so
+// one 1-KB DMA wave-instruction moves 2048 / BKT weight rows: a quarter of the fp16 operand's
+// bytes), followed in the stage by the step's group-scale row s[k0 / group][n0 .. n0 + BN) (fp16,
+// one piece, from the [K / group][N] copy; group % BKT == 0).  BKT 64 rows hold two 16-B chunks,
+// swapped on rows with bit 3 set (the DMA source is permuted, as the fp16 stages' XOR swizzle), so
+// the 16 rows x 4 dwords a fragment read touches are bank-conflict free.  A lane's B fragment
+// (row r, k = 32ks + 8fq .. + 7) is one ds_read_b32 of codes + its row's scale, dequantized in
+// registers (w4_frag); half(q * s) is the reference's dequantized weight, so every int4 variant
+// gives the fp16-buffer GEMM's bits.
+template <int BN, int NT, int BKT>
+struct BDma4 {
+  static constexpr int NW = NT / 64;
+  static constexpr int RB = BKT / 2;           // code bytes per row and stage
+  static constexpr int RPP = 1024 / RB;        // rows per 1-KB piece
+  static constexpr int G = (BN + RPP - 1) / RPP;
+  static constexpr int L = (G + NW - 1) / NW;
+  static constexpr int CODE_H = G * 512;       // halves of the code region (whole pieces)
+  static constexpr int SZ = CODE_H + 512;      // + the scale row piece
+  static constexpr int SW = NW - 1;            // the wave that DMAs the scale row
+  __amdgpu_buffer_rsrc_t rs, srs;
+  unsigned rowoff[L];
+  unsigned soff;
+  __device__ static int count(int wid) { return G / NW + (wid < G % NW ? 1 : 0) + (wid == SW ? 1 : 0); }
+  __device__ void init(const GemmArgs& p, int n0, int wid) {
+    rs = rsrc(p.b, p.b_bytes);
+    srs = rsrc(p.bscale_t, (unsigned)((p.K / p.group) * p.N * 2));
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int r = (j * NW + wid) * RPP + lane * 16 / RB;  // RB / 16 lanes per row
+      const int n = n0 + r;
+      // BKT 64: lane pair (2r', 2r' + 1) fills row r' chunks 0 / 1 with K halves (0, 1) ^ (r' >> 3 & 1)
+      const unsigned ch = BKT == 64 ? (unsigned)(((lane & 1) ^ ((r >> 3) & 1)) * 16) : 0u;
+      rowoff[j] = (r < BN && n < p.N) ? (unsigned)n * (unsigned)(p.K / 2) + ch : OOB;
+    }
+    soff = (lane * 8 < BN && n0 + lane * 8 < p.N) ? (unsigned)(n0 + lane * 8) * 2u : OOB;
+  }
+  __device__ void issue(const GemmArgs& p, int k0, f16* sb, int wid) {
+    const unsigned ko = (unsigned)(k0 / 2);
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (G % NW == 0 || j * NW + wid < G) glds16(rs, sb + (j * NW + wid) * 512, rowoff[j] + ko);
+    if (wid == SW) glds16(srs, sb + CODE_H, soff == OOB ? OOB : soff + (unsigned)(k0 / p.group) * (unsigned)p.N * 2u);
+  }
+};
+
+typedef f16 f16x2v __attribute__((ext_vector_type(2)));
+// B fragment of row `row`, k = 32ks + 8fq .. + 7 of the stage, from an int4 stage.  Per dword of
+// 8 offset-binary codes (pairs of consecutive k in nibbles j / j + 4): the pair in nibble 0 / 4
+// OR'd into fp16 0x6400 is (1024 + c, 1024 + c'); the pair in nibble 1 / 5 lands on mantissa bits
+// 4..7 and with 0x5400 is (64 + c, 64 + c') (ulp 1/16 there: c counts whole units); the same two
+// masks on w >> 8 give pairs 2 and 3.  Subtracting 1032 / 72 leaves (q, q') exactly, and one
+// v_pk_mul_f16 by (s, s) rounds q * s once: 1 shift + 4 and-or + 4 sub + 4 mul per 8 weights.
+__device__ __forceinline__ f16x8 w4_dq8(unsigned w, f16 s, unsigned m64, unsigned m54) {
+  const f16x2v s2 = {s, s};
+  const f16x2v o1032 = {(f16)1032.f, (f16)1032.f}, o72 = {(f16)72.f, (f16)72.f};
+  const unsigned w8 = w >> 8;
+  const f16x2v q0 = __builtin_bit_cast(f16x2v, (w & 0x000F000Fu) | m64) - o1032;
+  const f16x2v q1 = __builtin_bit_cast(f16x2v, (w & 0x00F000F0u) | m54) - o72;
+  const f16x2v q2 = __builtin_bit_cast(f16x2v, (w8 & 0x000F000Fu) | m64) - o1032;
+  const f16x2v q3 = __builtin_bit_cast(f16x2v, (w8 & 0x00F000F0u) | m54) - o72;
+  const f16x2v v0 = q0 * s2, v1 = q1 * s2, v2 = q2 * s2, v3 = q3 * s2;
+  return (f16x8){v0[0], v0[1], v1[0], v1[1], v2[0], v2[1], v3[0], v3[1]};
+}
+template <int BKT>
+__device__ __forceinline__ f16x8 w4_frag(const f16* sb, int row, int ks, int fq, int code_h, unsigned m64,
+                                         unsigned m54) {
+  constexpr int RB = BKT / 2;
+  const int ch = BKT == 64 ? ((ks ^ ((row >> 3) & 1)) << 4) : 0;
+  const unsigned w = *reinterpret_cast<const unsigned*>(reinterpret_cast<const char*>(sb) + row * RB + ch + fq * 4);
+  return w4_dq8(w, sb[code_h + row], m64, m54);
+}
+
+// the two magics in VGPRs (opaque to constant folding), so each mask-and-or is one v_and_or_b32
+// with the mask as its single literal
+__device__ __forceinline__ void w4_magics(unsigned& m64, unsigned& m54) {
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(m64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(m54));
+}
+
 // vmcnt of a value the caller's unrolling makes a compile-time constant (folds to one s_waitcnt)
 __device__ __forceinline__ void wait_vm_c(int n) {
   if (n <= 0) wait_vm<0>();
@@ -777,22 +858,39 @@ constexpr int dma_waves_per_eu(int bm, int bn, int st, int nt, int bkt = 64) {
              : 1;
 }
 
+// int4 B stages: A tile + the BDma4 code pieces and scale row
+constexpr int w4_stage_halves(int bm, int bn, int bkt) {
+  return bm * bkt + ((bn + 2048 / bkt - 1) / (2048 / bkt)) * 512 + 512;
+}
+constexpr int dma_lds_halves_w4(int bm, int bn, int st, int bkt) {
+  return st * w4_stage_halves(bm, bn, bkt) > epi_lds_halves(bm, bn) ? st * w4_stage_halves(bm, bn, bkt) : epi_lds_halves(bm, bn);
+}
+constexpr int dma_waves_per_eu_w4(int bm, int bn, int st, int nt, int bkt) {
+  return (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256 > 0
+             ? (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256
+             : 1;
+}
+
 template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false,
-          bool F8 = false>
-__global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
+          bool F8 = false, bool W4 = false>
+__global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, BN, ST, 64 * WGM * WGN, BKT)
+                                                     : dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
     k_gemm_dma(GemmArgs p) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ASZ = BM * BKT, SSZ = (BM + BN) * BKT + (F8 ? F8_SCL : 0);
-  constexpr int LDSZ = F8 ? dma_lds_halves_f8(BM, BN, ST) : dma_lds_halves(BM, BN, ST, BKT);
+  constexpr int ASZ = BM * BKT;
+  constexpr int SSZ = W4 ? ASZ + BDma4<BN, NT, BKT>::SZ : (BM + BN) * BKT + (F8 ? F8_SCL : 0);
+  constexpr int LDSZ = W4 ? dma_lds_halves_w4(BM, BN, ST, BKT) : F8 ? dma_lds_halves_f8(BM, BN, ST) : dma_lds_halves(BM, BN, ST, BKT);
   constexpr int KSUB = BKT / 32;  // 32-deep MFMA slices per stage
   static_assert(PIPE == 0 || (ST >= 3 && BKT == 64), "split-phase pipeline needs >= 3 stages of 64");
   static_assert(!I8 || (BKT == 32 && PIPE == 0), "int8: one 64-code MFMA k-slice per 64-B LDS row");
   static_assert(!F8 || (BKT == 64 && PIPE == 0 && !SPLIT && BN * 4 <= 1024),
                 "fp8: one 128-code group per 128-B LDS row, no split-K, the scale row in one DMA piece");
+  static_assert(!W4 || (!I8 && !F8 && PIPE == 0 && AMODE == AM_LINEAR && BN <= 512),
+                "int4: lock-step pipeline, linear A operand, one scale piece");
   using AL = ADma<BM, NT, AMODE, BKT>;
-  using BL = BDma<BN, NT, BKT>;
+  using BL = std::conditional_t<W4, BDma4<BN, NT, BKT>, BDma<BN, NT, BKT>>;
   __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
 
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
@@ -849,12 +947,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN, dma_waves_per_eu(BM, BN, ST, 6
       issue_scale(kbeg + s * BKT, smem + s * SSZ);
     }
   }
+  unsigned m64 = 0, m54 = 0;
+  if constexpr (W4) w4_magics(m64, m54);
   auto read_frags = [&](const f16* As, int ks, f16x8 (&af)[TM], f16x8 (&bf)[TN]) {
     const f16* Bs = As + ASZ;
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BKT>(wm0 + i * 16 + fr, ks * 4 + fq));
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BKT>(wn0 + j * 16 + fr, ks * 4 + fq));
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (W4) bf[j] = w4_frag<BKT>(Bs, wn0 + j * 16 + fr, ks, fq, BDma4<BN, NT, BKT>::CODE_H, m64, m54);
+      else bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BKT>(wn0 + j * 16 + fr, ks * 4 + fq));
+    }
   };
   auto mfmas = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
 #ifdef QD_ABLATE_NO_MFMA  // diagnostic build: staging + fragment reads only (values kept live)
@@ -990,17 +1093,19 @@ constexpr int pp_lds_halves(int bn) {
 // v_mfma_i32_16x16x64_i8 slice, the fragment reads unchanged); the int32 sums live in the fp32
 // accumulator registers (bit-cast) and are scaled by sa[m] * sw[n] before the epilogue, or go
 // to the split-K slab as int32 bits (k_splitk_reduce's i8 path) - the k_gemm_dma<I8> arithmetic.
-template <int BN, int WGM, int AMODE, bool SPLIT, bool I8 = false>
+// W4: packed-int4 B stages (BDma4: code pieces + the group-scale row), dequantized per fragment
+template <int BN, int WGM, int AMODE, bool SPLIT, bool I8 = false, bool W4 = false>
 __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   constexpr int BM = 256, BK = 32, NT = 512;
   constexpr int WGN = 8 / WGM;                      // wave grid WGM x WGN (2x4 or 4x2)
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16, TH = TM / 2;  // TH m-frags per phase
-  constexpr int ASZ = BM * BK, SSZ = (BM + BN) * BK;
+  constexpr int ASZ = BM * BK, SSZ = W4 ? ASZ + BDma4<BN, NT, BK>::SZ : (BM + BN) * BK;
   static_assert(WN % 16 == 0 && TM % 2 == 0 && (WGM == 2 || WGM == 4), "wave tile");
+  static_assert(!W4 || (!I8 && AMODE == AM_LINEAR), "int4 B: linear A operand");
   using AL = ADma<BM, NT, AMODE, BK>;
-  using BL = BDma<BN, NT, BK>;
-  __shared__ __attribute__((aligned(16))) f16 smem[pp_lds_halves(BN)];
+  using BL = std::conditional_t<W4, BDma4<BN, NT, BK>, BDma<BN, NT, BK>>;
+  __shared__ __attribute__((aligned(16))) f16 smem[4 * SSZ > 128 * (BN + 8) ? 4 * SSZ : 128 * (BN + 8)];
 
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
   const int ntile = nbm * nbn;
@@ -1051,6 +1156,8 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   asm volatile("" ::: "memory");
 
   f16x8 af[TH], bf[TN];
+  unsigned m64 = 0, m54 = 0;
+  if constexpr (W4) w4_magics(m64, m54);
   auto mfma_block = [&](int ih) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -1084,7 +1191,10 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < TH; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BK>(wm0 + i * 16 + fr, fq));
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BK>(wn0 + j * 16 + fr, fq));
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (W4) bf[j] = w4_frag<BK>(Bs, wn0 + j * 16 + fr, 0, fq, BDma4<BN, NT, BK>::CODE_H, m64, m54);
+      else bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BK>(wn0 + j * 16 + fr, fq));
+    }
     if (pre) al.issue(p, kbeg + (kt + 2) * BK, nxt, wid);
     bar();
     mfma_block(0);
@@ -1951,8 +2061,11 @@ extern "C" int qd_gemm_force(int variant) {
 // Cost model (seconds): a CU runs ~4 TFLOP/s of this kernel with 2 resident blocks, ~3 with
 // one; tile efficiency eff; a launch takes ceil(blocks / 512) rounds of 2 blocks per CU.
 // Splits add the fp32 slab round trip (~5 TB/s) and one reduction launch.
+// w4: packed-int4 weights with transposed scales - the ping-pong and BK-32 LDS-DMA variants run
+// them through BDma4 (quant_w alone admits only the register-staged tiles)
 static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bool amax, bool geglu = false,
-                      bool post = false) {
+                      bool post = false, int w4g = 0) {
+  const bool w4 = w4g > 0;  // int4 group size when the codes can take the DMA / ping-pong families
   struct T {
     int bm, bn;
     double eff;
@@ -1994,7 +2107,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         best.kps = nc / sp;
       }
     }
-  } else if (g_force >= 300 && g_force <= 304 && !quant_w && !post) {  // (own epilogue: no post-residual amax)
+  } else if (g_force >= 300 && g_force <= 304 && (!quant_w || w4) && !post) {  // (own epilogue: no post-residual amax)
     // ping-pong 256 x {256, 320, 192} tiles (2x4 waves, wave rows 128) and 256 x {160, 128}
     // (4x2 waves, wave rows 64); amax needs whole-sample wave tiles
     static const int kBn[] = {256, 320, 192, 160, 128};
@@ -2009,7 +2122,8 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         best.kps = K / sp;
       }
     }
-  } else if (g_force >= 100 && g_force < 200 && !quant_w) {
+  } else if (g_force >= 100 && g_force < 200 &&
+             (!quant_w || (w4 && w4g % kDmaC[g_force - 100].bkt == 0 && kDmaC[g_force - 100].pipe == 0))) {
     const DmaVar& d = kDmaC[g_force - 100];
     const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
     if (ok) {
@@ -2046,8 +2160,36 @@ static void launch_dma_v(const GemmArgs& p, hipStream_t st) {
   k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
 }
 
+template <int V, bool SPLIT>
+static void launch_dma_w4_v(const GemmArgs& p, hipStream_t st) {
+  constexpr DmaVar d = kDmaC[V];
+  const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
+  k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AM_LINEAR, SPLIT, false, false, true>
+      <<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+}
+
 template <int AMODE, bool SPLIT>
-static void launch_dma(const GemmArgs& p, int var, hipStream_t st) {
+static void launch_dma(const GemmArgs& p, int var, hipStream_t st, int fmt = QD_WFMT_F16) {
+  if constexpr (AMODE == AM_LINEAR) {
+    if (fmt == QD_WFMT_I4) {
+      switch (var) {
+        case 0: launch_dma_w4_v<0, SPLIT>(p, st); break;
+        case 1: launch_dma_w4_v<1, SPLIT>(p, st); break;
+        case 2: launch_dma_w4_v<2, SPLIT>(p, st); break;
+        case 3: launch_dma_w4_v<3, SPLIT>(p, st); break;
+        case 4: launch_dma_w4_v<4, SPLIT>(p, st); break;
+        case 5: launch_dma_w4_v<5, SPLIT>(p, st); break;
+        case 9: launch_dma_w4_v<9, SPLIT>(p, st); break;
+        case 10: launch_dma_w4_v<10, SPLIT>(p, st); break;
+        case 11: launch_dma_w4_v<11, SPLIT>(p, st); break;
+        case 12: launch_dma_w4_v<12, SPLIT>(p, st); break;
+        case 13: launch_dma_w4_v<13, SPLIT>(p, st); break;
+        case 14: launch_dma_w4_v<14, SPLIT>(p, st); break;
+        default: launch_dma_w4_v<15, SPLIT>(p, st); break;
+      }
+      return;
+    }
+  }
   switch (var) {
     case 0: launch_dma_v<0, AMODE, SPLIT>(p, st); break;
     case 1: launch_dma_v<1, AMODE, SPLIT>(p, st); break;
@@ -2072,6 +2214,16 @@ template <int AMODE, bool SPLIT>
 static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t st) {
   if (pl.kind == 3) {
     const int nwg = ((p.M + 255) / 256) * ((p.N + pl.bn - 1) / pl.bn) * p.splits;
+    if constexpr (AMODE == AM_LINEAR) {
+      if (fmt == QD_WFMT_I4) {
+        if (pl.bn == 256) k_gemm_pp<256, 2, AMODE, SPLIT, false, true><<<nwg, 512, 0, st>>>(p);
+        else if (pl.bn == 320) k_gemm_pp<320, 2, AMODE, SPLIT, false, true><<<nwg, 512, 0, st>>>(p);
+        else if (pl.bn == 192) k_gemm_pp<192, 2, AMODE, SPLIT, false, true><<<nwg, 512, 0, st>>>(p);
+        else if (pl.bn == 160) k_gemm_pp<160, 4, AMODE, SPLIT, false, true><<<nwg, 512, 0, st>>>(p);
+        else k_gemm_pp<128, 4, AMODE, SPLIT, false, true><<<nwg, 512, 0, st>>>(p);
+        return;
+      }
+    }
     if (pl.bn == 256) k_gemm_pp<256, 2, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
     else if (pl.bn == 320) k_gemm_pp<320, 2, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
     else if (pl.bn == 192) k_gemm_pp<192, 2, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
@@ -2086,7 +2238,7 @@ static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t 
       if (pl.bn == 160) k_conv_halo<160><<<nwg, 512, 0, st>>>(p);
       else k_conv_halo<128><<<nwg, 512, 0, st>>>(p);
     }
-  } else if (pl.kind == 1) launch_dma<AMODE, SPLIT>(p, pl.var, st);
+  } else if (pl.kind == 1) launch_dma<AMODE, SPLIT>(p, pl.var, st, fmt);
   else if (pl.bm == 128 && pl.bn == 160) launch_fmt<128, 160, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128 && pl.bn == 128) launch_fmt<128, 128, AMODE, SPLIT>(p, fmt, st);
   else if (pl.bm == 128) launch_fmt<128, 64, AMODE, SPLIT>(p, fmt, st);
@@ -2137,8 +2289,8 @@ struct GemvChunk {
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const int nib = (wd[d] >> (4 * e)) & 0xf;
-            w[d * 8 + e] = (f16)((float)(nib >= 8 ? nib - 16 : nib) * s);
+            const int q = (int)(((unsigned)wd[d] >> ((e & 1) * 16 + (e >> 1) * 4)) & 0xf) - 8;
+            w[d * 8 + e] = (f16)((float)q * s);
           }
         }
       }
@@ -2151,15 +2303,15 @@ template <int BFMT, int MM, int CPL>
 __device__ __forceinline__ void gemv_dot(const GemvChunk<BFMT>& ch, const f16x8 (&a)[MM][CPL][4], int j,
                                          float (&out)[MM]) {
     if constexpr (BFMT == QD_WFMT_I4) {
-      // packed decode: (nib ^ 8) | 0x6400 is the fp16 1024 + q + 8, minus 1032 = q exactly;
+      // packed decode: c | 0x6400 is the fp16 1024 + c = 1024 + q + 8, minus 1032 = q exactly;
       // v_pk_mul_f16 by s rounds q * s (exact in fp32) once, as the tile loader's
-      // half((float)q * s).  Lanes of a pair are k = 8d + t and 8d + t + 4.
+      // half((float)q * s).  Lanes of a pair are k = 8d + 2t and 8d + 2t + 1 (qd_pack_int4).
       const f16 sh = (f16)ch.s;
       const f16x2 s2 = {sh, sh};
       const f16x2 off = {(f16)1032.f, (f16)1032.f};
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const unsigned u = (unsigned)ch.v[0][d] ^ 0x88888888u;
+        const unsigned u = (unsigned)ch.v[0][d];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const f16x2 q2 = __builtin_bit_cast(f16x2, ((u >> (4 * t)) & 0x000F000Fu) | 0x64006400u) - off;
@@ -2191,8 +2343,6 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
   constexpr int R = 4;
   const int lane = threadIdx.x & 63;
   const int nch = p.K / 32;
-  // int4: the activations are kept as (k, k + 4) pairs, the order the packed nibble decode
-  // below produces weights in; other formats keep k order
   f16x8 a[MM][CPL][4];
 #pragma unroll
   for (int m = 0; m < MM; ++m)
@@ -2201,10 +2351,8 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
       const int c = lane + 64 * j;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f16x8 v = (m < p.M && c < nch) ? *reinterpret_cast<const f16x8*>(p.a + (long)m * p.lda + c * 32 + q * 8)
-                                             : f16x8{};
-        if constexpr (BFMT == QD_WFMT_I4) a[m][j][q] = __builtin_shufflevector(v, v, 0, 4, 1, 5, 2, 6, 3, 7);
-        else a[m][j][q] = v;
+        a[m][j][q] = (m < p.M && c < nch) ? *reinterpret_cast<const f16x8*>(p.a + (long)m * p.lda + c * 32 + q * 8)
+                                           : f16x8{};
       }
     }
   const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
@@ -2284,8 +2432,9 @@ static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 
 template <int AMODE>
 static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t st) {
   const bool post = (p.epi & QD_EPI_AMAX_POST) != 0;
+  const int w4g = fmt == QD_WFMT_I4 && p.bscale_t != nullptr && AMODE == AM_LINEAR ? p.group : 0;
   Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
-                      (p.epi & QD_EPI_GEGLU) != 0, post);
+                      (p.epi & QD_EPI_GEGLU) != 0, post, w4g);
   if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn))) {  // halo conv not applicable
     const int f = g_force;
     g_force = -1;
@@ -2351,19 +2500,22 @@ static int check_common(const GemmArgs& p, int fmt) {
 
 extern "C" long qd_gemm_workspace(int M, int N, int K, int wfmt, int rows_per_sample, int epi) {
   const Plan pl = plan_gemm(M, N, K, wfmt != QD_WFMT_F16, rows_per_sample, (epi & QD_EPI_AMAX) != 0,
-                            (epi & QD_EPI_GEGLU) != 0, (epi & QD_EPI_AMAX_POST) != 0);
+                            (epi & QD_EPI_GEGLU) != 0, (epi & QD_EPI_AMAX_POST) != 0,
+                            wfmt == QD_WFMT_I4 ? 64 : 0);  // (group unknown here: size for every int4 variant)
   return split_ws_elems(pl, M, N);
 }
 
 extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
-                             const void* wscale, int group, const void* bias, const void* residual,
-                             void* y, int N, int ldy, int epi, float* amax, int rows_per_sample,
-                             float* ws, long ws_elems, void* stream) {
+                             const void* wscale, const void* wscale_t, int group, const void* bias,
+                             const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                             int rows_per_sample, float* ws, long ws_elems, void* stream) {
   GemmArgs p{};
   p.a = (const f16*)x;
   p.lda = lda;
   p.b = w;
   p.bscale = (const f16*)wscale;
+  p.bscale_t = wfmt == QD_WFMT_I4 ? (const f16*)wscale_t : nullptr;
+  QD_REQUIRE(!p.bscale_t || (reinterpret_cast<uintptr_t>(wscale_t) & 15) == 0, "wscale_t must be 16-B aligned");
   p.group = group;
   p.bias = (const f16*)bias;
   p.res = (const f16*)residual;

@@ -445,20 +445,30 @@ extern "C" int qd_weight_quant(const void* w, int rows, int cols, int group, int
   return 0;
 }
 
-__global__ void k_pack_int4(const int8_t* __restrict__ codes, long pairs, uint8_t* __restrict__ out) {
+// Packed int4 GEMM operand: per 8-code word (k = 8i .. 8i + 7, one little-endian dword) nibble j
+// holds c(8i + 2j) and nibble j + 4 holds c(8i + 2j + 1), j = 0..3, with c = q + 8 (offset binary).
+// Then ((w >> 4j) & 0x000F000F) | 0x64006400 is the fp16 pair (1024 + c(2j), 1024 + c(2j + 1)):
+// two codes in k order per 2 VALU, the MFMA fragment's own element order.
+__global__ void k_pack_int4(const int8_t* __restrict__ codes, long words, uint32_t* __restrict__ out) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= pairs) return;
-  const uint8_t lo = (uint8_t)codes[2 * i] & 0xF;
-  const uint8_t hi = (uint8_t)codes[2 * i + 1] & 0xF;
-  out[i] = lo | (hi << 4);
+  if (i >= words) return;
+  const int8_t* c = codes + 8 * i;
+  uint32_t w = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w |= (uint32_t)((c[2 * j] + 8) & 0xF) << (4 * j);
+    w |= (uint32_t)((c[2 * j + 1] + 8) & 0xF) << (4 * j + 16);
+  }
+  out[i] = w;
 }
 
 extern "C" int qd_pack_int4(const int8_t* codes, int rows, int cols, uint8_t* packed, void* stream) {
   QD_REQUIRE(codes && packed, "null pointer");
-  QD_REQUIRE(cols % 2 == 0, "int4 packing needs even cols");
-  const long pairs = (long)rows * cols / 2;
-  if (pairs == 0) return 0;
-  k_pack_int4<<<grid1(pairs), 256, 0, S(stream)>>>(codes, pairs, packed);
+  QD_REQUIRE(cols % 8 == 0, "int4 packing needs cols % 8 == 0");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(packed) & 3) == 0, "packed int4 buffer must be 4-B aligned");
+  const long words = (long)rows * cols / 8;
+  if (words == 0) return 0;
+  k_pack_int4<<<grid1(words), 256, 0, S(stream)>>>(codes, words, reinterpret_cast<uint32_t*>(packed));
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -62,12 +62,14 @@ def awq_unpack_linear(qweight, qzeros, scales, group):
 
 
 def packed_nibbles_to_codes(packed, k):
-    """This build's GEMM layout (2 codes per byte along K, low nibble = even k) -> int8 [N, K]."""
-    lo = (packed & 0xF).to(torch.int8)
-    hi = ((packed >> 4) & 0xF).to(torch.int8)
-    lo = torch.where(lo >= 8, lo - 16, lo)
-    hi = torch.where(hi >= 8, hi - 16, hi)
-    return torch.stack([lo, hi], -1).reshape(packed.shape[0], k)
+    """This build's GEMM layout -> int8 [N, K]: per 8-code word (one little-endian dword, k = 8i ..
+    8i + 7) nibble j holds q(8i + 2j) + 8 and nibble j + 4 holds q(8i + 2j + 1) + 8 (qd_pack_int4)."""
+    n = packed.shape[0]
+    w = packed.contiguous().view(torch.uint8).reshape(n, -1, 4).to(torch.int32)
+    w = w[..., 0] | (w[..., 1] << 8) | (w[..., 2] << 16) | (w[..., 3] << 24)
+    shifts = torch.tensor([0, 16, 4, 20, 8, 24, 12, 28], dtype=torch.int32, device=packed.device)
+    c = (w[..., None] >> shifts) & 0xF
+    return (c - 8).to(torch.int8).reshape(n, k)
 
 
 @torch.no_grad()

@@ -7,6 +7,7 @@ argument errors; kernel failures surface as ``RuntimeError`` from ``_lib.call``.
 """
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -182,8 +183,17 @@ REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the re
 DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 114, 115,   # LDS-DMA variants (fp16 weights)
                 300, 301, 302, 303, 304)                        # ping-pong 256-row
 HALO_VARIANTS = (200, 201, 202, 203)  # 3x3 conv with the activation halo staged once per channel chunk
+# packed int4 through the lock-step LDS-DMA stages and the ping-pong tiles (BDma4 code stages,
+# dequantized per fragment)
+W4_VARIANTS = (100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115, 300, 301, 302, 303, 304)
 _TUNE = {}
+_USED = set()  # GEMM keys this process has launched (bench reporting: gemm_choices(used_only=True))
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
+# W4A16 operand policy: the packed-int4 codes (+ group scales) are the only candidate operand of an
+# int4 linear - the weight stream is 4x smaller than the module's fp16 dequantized buffer and the
+# LDS-DMA / ping-pong int4 stages run within noise of it end to end (profiles/r03g_c3_*);
+# QD_W4_OPERAND=tuned lets the tuner also time the fp16 buffer (the reference's own weight) per shape
+W4_CODES_ONLY = os.environ.get("QD_W4_OPERAND", "codes") != "tuned"
 _OVERRIDE = None  # benchmarking: force every GEMM onto one qd_gemm_force id (see force_gemm)
 
 
@@ -242,9 +252,10 @@ def force_gemm(variant=None):
     _OVERRIDE = variant
 
 
-def gemm_choices():
-    """{shape key: (weight format, qd_gemm_force id)} chosen so far."""
-    return dict(_TUNE)
+def gemm_choices(used_only=False):
+    """{shape key: (op index, qd_gemm_force id)} chosen so far (used_only: only the keys this
+    process launched, not every entry of the loaded table)."""
+    return {k: v for k, v in _TUNE.items() if not used_only or k in _USED}
 
 
 def _force(v):
@@ -289,13 +300,35 @@ def _choose(key, cands, run):
 
 
 def _cands(ops):
-    """(op index, variant) candidates: register tiles for every format, DMA for fp16."""
+    """(op index, variant) candidates: register tiles for every format, the LDS-DMA / ping-pong
+    families for fp16 and packed-int4 operands."""
     out = []
     for i, op in enumerate(ops):
         out += [(i, v) for v in REG_VARIANTS]
         if op[1] == "f16":
             out += [(i, v) for v in DMA_VARIANTS]
+        elif op[1] == "i4" and op[3] % 32 == 0:
+            # BK-64 stages take one group-scale row per 64-deep step: group % 64 == 0
+            out += [(i, v) for v in W4_VARIANTS if op[3] % 64 == 0 or not 100 <= v <= 109]
     return out
+
+
+# [K / group][N] copies of int4 group scales (the LDS-DMA int4 stages DMA one scale row per K
+# step), made once per scales tensor: keyed by the tensor's id while it lives, re-made when it is
+# edited in place (version counter)
+_SCALES_T = {}
+
+
+def scales_t(sc):
+    key = id(sc)
+    e = _SCALES_T.get(key)
+    if e is not None and e[0] == sc._version and e[1].device == sc.device:
+        return e[1]
+    t = sc.t().contiguous()
+    if e is None:
+        weakref.finalize(sc, _SCALES_T.pop, key, None)
+    _SCALES_T[key] = (sc._version, t)
+    return t
 
 
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
@@ -324,7 +357,7 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     if residual is not None:
         _chk(residual, "residual")
     ops = [(weight, wfmt, scales, group)]
-    if weight_f16 is not None and wfmt != "f16":
+    if weight_f16 is not None and wfmt != "f16" and not (wfmt == "i4" and W4_CODES_ONLY):
         ops.append((weight_f16, "f16", None, 0))
 
     def launch(c, y, am, ep, scratch):
@@ -336,13 +369,15 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
                 ws, wsn = (torch.empty(n, dtype=torch.float32, device=x2d.device), n) if n > 0 else (None, 0)
             else:
                 ws, wsn = _gemm_ws(M, N, K, WFMT[fmt], rows_per_sample, ep, x2d.device)
-            _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(w), WFMT[fmt], _p(sc), gr,
+            sct = scales_t(sc) if fmt == "i4" else None
+            _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(w), WFMT[fmt], _p(sc), _p(sct), gr,
                       _p(bias), _p(residual), _p(y), N, y.stride(0), ep, _p(am), rows_per_sample,
                       _p(ws), wsn, _stream())
         finally:
             _force(-1)
 
     key = ("linear", M, N, K, x2d.stride(0), epi & ~EPI_AMAX_ZEROED, rows_per_sample, tuple(o[1] for o in ops))
+    _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
@@ -404,6 +439,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
             _force(-1)
 
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
+    _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
@@ -484,6 +520,7 @@ def linear_fp8(xq, sa, w8, gs, bias=None, residual=None, out=None, gelu_tanh=Fal
             _force(-1)
 
     key = ("linear_fp8", M, N, Kd, xq.stride(0), epi)
+    _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         c = _choose(key, list(F8_VARIANTS), lambda c: launch(c, ty))
@@ -574,6 +611,7 @@ def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, row
             _force(-1)
 
     key = ("linear_i8", M, N, Kd, xq.stride(0), epi & ~EPI_AMAX_ZEROED, rows_per_sample)
+    _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
@@ -612,6 +650,7 @@ def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, 
             _force(-1)
 
     key = ("conv_i8", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
+    _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None

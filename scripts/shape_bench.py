@@ -1,7 +1,10 @@
 """Per-variant GPU time of the SD1.5 CFG-batch-8 GEMM / conv shapes, launch overhead excluded:
 each (shape, variant) is captured as a HIP graph of `iters` back-to-back calls and replayed.
-usage: python scripts/shape_bench.py [--int8] [--iters 20] [--only conv|linear] [--amax]
-(--amax: the fp16 convs with the per-(sample, channel) output-amax epilogue of the W8A8 path)"""
+usage: python scripts/shape_bench.py [--int8] [--iters 20] [--only conv|linear] [--amax] [--w4 [--mscale 2]]
+(--amax: the fp16 convs with the per-(sample, channel) output-amax epilogue of the W8A8 path;
+ --w4: the linears as W4A16 group-128 codes - packed int4 through the register tile and the LDS-DMA /
+ ping-pong int4 stages vs the fp16 dequantized buffer through every fp16 family; --mscale 2 = C3's
+ CFG batch 16)"""
 import argparse
 import os
 import sys
@@ -74,7 +77,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None, choices=["conv", "linear"])
     ap.add_argument("--amax", action="store_true")
+    ap.add_argument("--w4", action="store_true")
+    ap.add_argument("--mscale", type=int, default=1)
     a = ap.parse_args()
+    if a.w4:
+        return w4_linears(a)
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
     if a.int8:
@@ -112,6 +119,34 @@ def main():
             else:
                 res = run_variants(lambda: K.linear(x, wt, bias=b, geglu=geglu), variants, a.iters)
             print(f"linear ({m},{nn},{kk}{',geglu' if geglu else ''}) x{cnt}: " + fmt(res, flops), flush=True)
+
+
+def w4_linears(a):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    f16v = list(K.REG_VARIANTS) + list(K.DMA_VARIANTS)
+    i4v = list(K.REG_VARIANTS) + list(K.W4_VARIANTS)
+    tot16 = tot4 = 0.0
+    for (m, nn, kk, geglu, cnt) in LINS:
+        m *= a.mscale
+        x = torch.randn(m, kk, generator=g).half().to(dev)
+        wt = (torch.randn(nn, kk, generator=g) / kk ** 0.5).half().to(dev)
+        b = torch.zeros(nn, dtype=torch.float16, device=dev)
+        gs = 128
+        while kk % gs:
+            gs -= 32
+        codes, sc, wdq = K.weight_quant(wt, gs, 4)
+        packed = K.pack_int4(codes)
+        flops = 2.0 * m * nn * kk
+        r16 = run_variants(lambda: K.linear(x, wdq, "f16", bias=b, geglu=geglu), f16v, a.iters)
+        r4 = run_variants(lambda: K.linear(x, packed, "i4", sc, gs, bias=b, geglu=geglu), i4v, a.iters)
+        b16 = min(t for t in r16.values() if t)
+        b4 = min(t for t in r4.values() if t)
+        tot16 += cnt * b16
+        tot4 += cnt * b4
+        print(f"linear ({m},{nn},{kk}{',geglu' if geglu else ''}) x{cnt} g{gs}: fp16 buffer {fmt(r16, flops)}", flush=True)
+        print(f"    int4 codes {fmt(r4, flops)}  -> i4/f16 {b4 / b16:.3f}", flush=True)
+    print(f"sum over one eval's linears: fp16 buffer {tot16:.0f} us, int4 codes {tot4:.0f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -87,14 +87,46 @@ def run_sd35(dev):
         torch.cuda.empty_cache()
 
 
+def run_w4(dev):
+    """Only the packed-int4 (W4A16) GEMM shapes: SD1.5 at CFG batch 2 / 16, SD3.5-L."""
+    from qdiff.models import StableDiffusion1_x, StableDiffusion3_5
+    g = torch.Generator().manual_seed(0)
+    m = StableDiffusion1_x.from_pretrained("synthetic:sd15", device=dev, seed=0)
+    m.quantize(quant_config=dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False), quantUnet=True)
+    for b in (1, 8):
+        lat = torch.randn(b, 4, 64, 64, generator=g).half()
+        m.generate(prompt=[f"p{i}" for i in range(b)], lat=lat, num_inference_steps=2, use_graph=False,
+                   output_type="latent")
+    log("sd15 w4a16")
+    del m
+    torch.cuda.empty_cache()
+    m = StableDiffusion3_5.from_pretrained("synthetic:sd35", device=dev, seed=0)
+    m.quantize(quant_config=dict(w_bit=4, a_bit=16, q_group_size=128, quantize_act=False), quantTransformer=True)
+    lat = torch.randn(1, 16, 128, 128, generator=g).half()
+    m.generate(prompt=["a"], lat=lat, height=1024, width=1024, num_inference_steps=2, use_graph=False,
+               output_type="latent")
+    log("sd35 w4a16")
+    del m
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="sd15,sdxl,sd35")
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--retune-i4", action="store_true",
+                    help="keep the committed table, re-tune only the linears whose operands include packed int4")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    for name in a.models.split(","):
-        {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
+    if a.retune_i4:
+        K.load_table(OUT)
+        for key in [k for k in K.gemm_choices() if k[0] == "linear" and "i4" in k[-1]]:
+            del K._TUNE[key]
+        log("committed table without its int4 linears")
+        run_w4(dev)
+    else:
+        for name in a.models.split(","):
+            {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
     K.save_table(a.out)
     log(f"wrote {a.out}")
 

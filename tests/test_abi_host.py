@@ -41,8 +41,8 @@ def test_bad_arguments_fail_before_launch():
         _lib.call("qd_act_fakequant", ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 1, 8, 1, 1, 1, 0, 1,
                   ctypes.c_void_p(16), None)
     with pytest.raises(RuntimeError, match="K must be"):
-        _lib.call("qd_linear_fwd", ctypes.c_void_p(16), 4, 12, 12, ctypes.c_void_p(16), 0, None, 0, None, None,
-                  ctypes.c_void_p(16), 4, 4, 0, None, 0, None, 0, None)
+        _lib.call("qd_linear_fwd", ctypes.c_void_p(16), 4, 12, 12, ctypes.c_void_p(16), 0, None, None, 0, None,
+                  None, ctypes.c_void_p(16), 4, 4, 0, None, 0, None, 0, None)
 
 
 def test_sd15_tree_matches_reference_counts():

@@ -49,8 +49,13 @@ def test_geglu_deinterleave_and_linear_amax():
 def test_dequant_weight_codes():
     q = torch.randint(-8, 8, (4, 64), dtype=torch.int8)
     s = _r(4, 2, seed=8).abs()
-    lo, hi = q[:, 0::2].to(torch.int16) & 0xF, q[:, 1::2].to(torch.int16) & 0xF
-    packed = (lo | (hi << 4)).to(torch.uint8)
+    # qd_pack_int4 layout: per dword of 8 codes, nibble j = q(2j) + 8, nibble j + 4 = q(2j + 1) + 8
+    c = (q.to(torch.int64) + 8).view(4, -1, 8)
+    w = torch.zeros(c.shape[:2], dtype=torch.int64)
+    for j in range(4):
+        w |= c[..., 2 * j] << (4 * j)
+        w |= c[..., 2 * j + 1] << (4 * j + 16)
+    packed = torch.stack([(w >> (8 * i)) & 0xFF for i in range(4)], -1).reshape(4, -1).to(torch.uint8)
     w4 = FR.dequant_weight(packed, "i4", s, 32, None)
     w8 = FR.dequant_weight(q, "i8", s, 32, None)
     ref = (q.float() * s.float().repeat_interleave(32, 1)).half()

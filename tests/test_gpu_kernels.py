@@ -88,12 +88,14 @@ def test_weight_codes(golden, dev):
         assert same_bits(scales.cpu().numpy(), s_ref)
         assert same_bits(wdq.cpu().numpy(), g[f"wgroup_b{bits}_k2560_out"])
         if bits == 4:
+            # qd_pack_int4: per little-endian dword of 8 codes, nibble j = q(2j) + 8 and
+            # nibble j + 4 = q(2j + 1) + 8 (offset binary, k pairs in MFMA fragment order)
             packed = k.pack_int4(codes).cpu().numpy()
-            lo = (packed & 0xF).astype(np.int8)
-            hi = (packed >> 4).astype(np.int8)
-            lo[lo >= 8] -= 16
-            hi[hi >= 8] -= 16
-            assert np.array_equal(np.stack([lo, hi], -1).reshape(c_ref.shape), c_ref)
+            w = packed.reshape(packed.shape[0], -1, 4).astype(np.uint32)
+            w = w[..., 0] | (w[..., 1] << 8) | (w[..., 2] << 16) | (w[..., 3] << 24)
+            sh = np.array([0, 16, 4, 20, 8, 24, 12, 28], dtype=np.uint32)
+            q = ((w[..., None] >> sh) & 0xF).astype(np.int8) - 8
+            assert np.array_equal(q.reshape(c_ref.shape), c_ref)
 
 
 def test_fq_finalize_bit_exact(dev):
@@ -592,6 +594,45 @@ def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     ref = (h * F.gelu(gt).half().float()).half().float()
     tol = 2 * ulp16(ref) + 2 * ulp16(h) * gt.abs() + 2.5 * h.abs() * ulp16(gt) + 1e-3
     assert ((fused - ref).abs() <= tol).all(), (variant, (fused - ref).abs().max().item())
+
+
+@pytest.mark.parametrize("variant", [100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115,
+                                     300, 301, 302, 303, 304])
+def test_int4_lds_dma_variants_bit_identical(variant, forced_gemm, dev):
+    """Packed-int4 codes through the LDS-DMA / ping-pong families (BDma4: codes + the K step's
+    group-scale row DMA'd into the stage, dequantized per fragment) give the SAME bits as the
+    same tile variant on the fp16 dequantized buffer: half(q * s) from LDS equals the buffer, and
+    the K order (and split-K plan) is the variant's.  Ragged M / N tails, groups 32 / 64 / 128,
+    split-K shapes, bias / residual / amax / GEGLU epilogues."""
+    k = K()
+    forced_gemm(variant)
+    g = torch.Generator().manual_seed(variant)
+    for M, N, Kd, gs in ((200, 320, 320, 64), (616, 640, 768, 128), (4096, 1280, 5120, 128), (77, 200, 1280, 128),
+                         (1000, 2560, 320, 32), (4096, 320, 1280, 128), (128, 128, 64, 64), (300, 64, 128, 64)):
+        x = torch.randn(M, Kd, generator=g).half().to(dev)
+        w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+        b = torch.randn(N, generator=g).half().to(dev)
+        res = torch.randn(M, N, generator=g).half().to(dev)
+        codes, scales, wdq = k.weight_quant(w, gs, 4)
+        packed = k.pack_int4(codes)
+        y4 = k.linear(x, packed, "i4", scales, gs, bias=b, residual=res)
+        y16 = k.linear(x, wdq, "f16", bias=b, residual=res)
+        assert torch.equal(y4, y16), (variant, M, N, Kd, (y4.float() - y16.float()).abs().max().item())
+        if M % 256 == 0:
+            a4 = torch.empty(M // 256 * N, dtype=torch.float32, device=dev)
+            a16 = torch.empty_like(a4)
+            z4 = k.linear(x, packed, "i4", scales, gs, bias=b, amax=a4, rows_per_sample=256)
+            z16 = k.linear(x, wdq, "f16", bias=b, amax=a16, rows_per_sample=256)
+            assert torch.equal(z4, z16) and torch.equal(a4, a16), (variant, M, N, Kd)
+    M, I, Kd, gs = 1000, 640, 320, 64
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(2 * I, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+    b = torch.randn(2 * I, generator=g).half().to(dev)
+    perm = k.geglu_interleave_rows(2 * I, dev)
+    codes, scales, wdq = k.weight_quant(w[perm].contiguous(), gs, 4)
+    f4 = k.linear(x, k.pack_int4(codes), "i4", scales, gs, bias=b[perm].contiguous(), geglu=True)
+    f16 = k.linear(x, wdq, "f16", bias=b[perm].contiguous(), geglu=True)
+    assert torch.equal(f4, f16), variant
 
 
 @pytest.mark.parametrize("bits,with_cadd,hw", [(8, True, 256), (0, True, 256), (8, False, 256), (4, True, 256),
