@@ -257,7 +257,8 @@ def weight_footprint(model):
     from qdiff import kernels as K
     from qdiff.fake_quant import WxAxLinear
     codes = f16 = 0
-    for m in model.pipeline.unet.modules() if hasattr(model.pipeline, "unet") else model.pipeline.transformer.modules():
+    net = getattr(model.pipeline, "unet", None) or model.pipeline.transformer
+    for m in net.modules():
         if isinstance(m, WxAxLinear) and m.qcodes is not None and m.qfmt == "i4":
             codes += m.qcodes.numel() + 2 * m.qscales.numel() * 2
             f16 += m.weight.numel() * 2
@@ -267,8 +268,8 @@ def weight_footprint(model):
             ran["codes" if key[-1][ch[0]] == "i4" else "f16 buffer"] += 1
     return {"int4_codes_and_scales_MB": round(codes / 2**20, 1), "fp16_buffer_MB": round(f16 / 2**20, 1),
             "linear_shapes_by_operand": ran,
-            "operand_policy": "int4 codes only (default)" if K.W4_CODES_ONLY else
-            "tuned per shape: int4 codes vs the fp16 dequantized buffer (QD_W4_OPERAND=tuned)"}
+            "operand_policy": "int4 codes only (QD_W4_OPERAND=codes)" if K.W4_CODES_ONLY else
+            "tuned per shape: int4 codes vs the fp16 dequantized buffer (default)"}
 
 
 def pmc_traffic(variant=None):

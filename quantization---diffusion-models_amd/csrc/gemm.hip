@@ -404,6 +404,24 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     static_assert(WGM <= 8, "column-max slots");
     float* const cmx = reinterpret_cast<float*>(ct + BM * LP);
     const bool blk_amax = do_amax && !geglu && WGM > 1 && p.rows_per_sample % BM == 0;
+    const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
+    const __amdgpu_buffer_rsrc_t yrs = rsrc(p.y, ybytes);
+    const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res && !post ? p.res : p.y, has_res && !post ? ybytes : 0u);
+    // the residual tile of the coalesced pass is loaded first, all NR chunks per thread in flight
+    // while the fragments go to LDS (a 2-deep load / add / store loop left the epilogue waiting on
+    // HBM latency NR / 2 times)
+    constexpr int CPR16 = BN / 8, NR = (BM * CPR16 + NT - 1) / NT;
+    const bool pre_res = has_res && !post && !geglu;
+    f16x8 rq[NR];
+    if (pre_res) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int e = (int)threadIdx.x + i * NT;
+        const int row = e / CPR16, n = n0 + (e - row * CPR16) * 8;
+        const bool ok = (BM * CPR16 % NT == 0 || e < BM * CPR16) && m0 + row < p.M && n < p.N;
+        rq[i] = bload(rrs, ok ? ((unsigned)(m0 + row) * (unsigned)p.ldy + (unsigned)n) * 2u : OOB);
+      }
+    }
     {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -468,9 +486,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // division); stores / residual loads are 32-bit-offset buffer ops (rows past M fall off the
     // end of the buffer range and are dropped / read 0).
     static_assert(BN % 32 == 0 || BN % 16 == 0, "tile width");
-    const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
-    const __amdgpu_buffer_rsrc_t yrs = rsrc(p.y, ybytes);
-    const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res && !post ? p.res : p.y, has_res && !post ? ybytes : 0u);
+    if (pre_res) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int e = (int)threadIdx.x + i * NT;
+        const int row = e / CPR16, c = e - row * CPR16;
+        const int n = n0 + c * 8;
+        if ((BM * CPR16 % NT == 0 || e < BM * CPR16) && n < p.N) {
+          const unsigned off = ((unsigned)(m0 + row) * (unsigned)p.ldy + (unsigned)n) * 2u;
+          f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i][r]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
+        }
+      }
+      return;
+    }
     auto pass2 = [&](auto cpr_c, auto geglu_c) {
       constexpr int CPR = decltype(cpr_c)::value;
       constexpr bool GG = decltype(geglu_c)::value;
@@ -865,10 +896,14 @@ constexpr int w4_stage_halves(int bm, int bn, int bkt) {
 constexpr int dma_lds_halves_w4(int bm, int bn, int st, int bkt) {
   return st * w4_stage_halves(bm, bn, bkt) > epi_lds_halves(bm, bn) ? st * w4_stage_halves(bm, bn, bkt) : epi_lds_halves(bm, bn);
 }
+// (at most 2 waves per SIMD: the smaller int4 stages would admit 3 blocks, whose 170-register cap
+// spills the 128 x 160 tile's accumulators + prefetched residual)
 constexpr int dma_waves_per_eu_w4(int bm, int bn, int st, int nt, int bkt) {
-  return (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256 > 0
-             ? (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256
-             : 1;
+  return (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256 > 2
+             ? 2
+             : (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256 > 0
+                   ? (163840 / (2 * dma_lds_halves_w4(bm, bn, st, bkt))) * nt / 256
+                   : 1;
 }
 
 template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false,

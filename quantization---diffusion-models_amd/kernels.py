@@ -189,11 +189,12 @@ W4_VARIANTS = (100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115, 
 _TUNE = {}
 _USED = set()  # GEMM keys this process has launched (bench reporting: gemm_choices(used_only=True))
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
-# W4A16 operand policy: the packed-int4 codes (+ group scales) are the only candidate operand of an
-# int4 linear - the weight stream is 4x smaller than the module's fp16 dequantized buffer and the
-# LDS-DMA / ping-pong int4 stages run within noise of it end to end (profiles/r03g_c3_*);
-# QD_W4_OPERAND=tuned lets the tuner also time the fp16 buffer (the reference's own weight) per shape
-W4_CODES_ONLY = os.environ.get("QD_W4_OPERAND", "codes") != "tuned"
+# W4A16 operand policy: by default the tuner times, per shape, the packed-int4 codes (LDS-DMA /
+# ping-pong int4 stages, a 4x smaller weight stream) against the module's fp16 dequantized buffer
+# (the reference's own `weight`) and keeps the faster - bit-identical results either way.
+# QD_W4_OPERAND=codes makes the codes the only operand: SD1.5 C3 runs within noise of the tuned mix
+# (8.71 vs 8.74 img/s, profiles/r03g_c3_*), SD3.5-L 6 % slower (profiles/r03h_sd35_*)
+W4_CODES_ONLY = os.environ.get("QD_W4_OPERAND", "tuned") == "codes"
 _OVERRIDE = None  # benchmarking: force every GEMM onto one qd_gemm_force id (see force_gemm)
 
 

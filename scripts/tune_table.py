@@ -123,7 +123,9 @@ def main():
         for key in [k for k in K.gemm_choices() if k[0] == "linear" and "i4" in k[-1]]:
             del K._TUNE[key]
         log("committed table without its int4 linears")
-        run_w4(dev)
+        for codes_only in (False, True):  # both W4 operand policies (their keys differ)
+            K.W4_CODES_ONLY = codes_only
+            run_w4(dev)
     else:
         for name in a.models.split(","):
             {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
