@@ -2082,14 +2082,30 @@ static constexpr DmaVar kDmaC[] = {
     {64, 64, 2, 2, 4, 0, 1.00, 32},    // 15: BK 32, 4 stages, small-M / short-K shapes
 };
 static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
+static int g_split = 0;   // with a forced DMA / ping-pong / halo variant: exact split-K count (0 = the fit rule)
+
+// split s (1 = unsplit) of a forced variant's plan when it is valid for the shape (else the rule's)
+static bool forced_split(int nsteps, int s_min_steps, int& sp) {
+  if (g_split <= 0) return false;
+  if (g_split == 1) {
+    sp = 1;
+    return true;
+  }
+  if (nsteps % g_split != 0 || nsteps / g_split < s_min_steps) return false;
+  sp = g_split;
+  return true;
+}
 
 extern "C" int qd_gemm_force(int variant) {
-  QD_REQUIRE(variant == -1 || (variant >= 0 && variant < 4) ||
-                 (variant >= 100 && variant < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (variant >= 200 && variant <= 203) || (variant >= 300 && variant <= 304) || (variant >= 120 && variant <= 123) ||
-                 (variant >= 130 && variant <= 134) || (variant >= 140 && variant <= 144),
+  const int v = variant >= 1000 ? variant % 1000 : variant, sp = variant >= 1000 ? variant / 1000 : 0;
+  QD_REQUIRE(v == -1 || (v >= 0 && v < 4) ||
+                 (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 203) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
+                 (v >= 130 && v <= 134) || (v >= 140 && v <= 144),
              "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200-203 halo conv, "
-             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-144)");
-  g_force = variant;
+             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-144); + 1000 * s: split-K count s (1 = unsplit)");
+  QD_REQUIRE(sp <= 32, "qd_gemm_force: split count above 32");
+  g_force = v;
+  g_split = sp;
   return 0;
 }
 
@@ -2135,11 +2151,17 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       const long tiles_mn = (long)(M / 256) * (N / bn);
       const int nc = K / 576;
       best = {2, 256, bn, g_force >= 202 ? 1 : 0, 1, nc};
-      for (int sp = 2; sp <= nc; ++sp) {
-        if (nc % sp != 0) continue;
-        if (tiles_mn * sp > 256) break;
-        best.splits = sp;
-        best.kps = nc / sp;
+      int fsp;
+      if (forced_split(nc, 1, fsp)) {
+        best.splits = fsp;
+        best.kps = nc / fsp;
+      } else {
+        for (int sp = 2; sp <= nc; ++sp) {
+          if (nc % sp != 0) continue;
+          if (tiles_mn * sp > 256) break;
+          best.splits = sp;
+          best.kps = nc / sp;
+        }
       }
     }
   } else if (g_force >= 300 && g_force <= 304 && (!quant_w || w4) && !post) {  // (own epilogue: no post-residual amax)
@@ -2150,11 +2172,17 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
     if (!amax || rows_per_sample % (bnp >= 192 ? 128 : 64) == 0) {
       best = {3, 256, bnp, 0, 1, K};
       const long tiles_mn = (long)((M + 255) / 256) * ((N + bnp - 1) / bnp);
-      for (int sp = 2; sp <= 32 && !geglu && K % 32 == 0; ++sp) {
-        if ((K / 32) % sp != 0 || K / sp < 512) continue;
-        if (tiles_mn * sp > 256L) break;
-        best.splits = sp;
-        best.kps = K / sp;
+      int fsp;
+      if (!geglu && K % 32 == 0 && forced_split(K / 32, 8, fsp)) {
+        best.splits = fsp;
+        best.kps = K / fsp;
+      } else {
+        for (int sp = 2; sp <= 32 && !geglu && K % 32 == 0; ++sp) {
+          if ((K / 32) % sp != 0 || K / sp < 512) continue;
+          if (tiles_mn * sp > 256L) break;
+          best.splits = sp;
+          best.kps = K / sp;
+        }
       }
     }
   } else if (g_force >= 100 && g_force < 200 &&
@@ -2167,11 +2195,17 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
       const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
       const int per_cu = std::max(1, std::min(by_lds, by_waves));
-      for (int sp = 2; sp <= 32 && !geglu && !post && K % 64 == 0; ++sp) {
-        if ((K / 64) % sp != 0 || K / sp < 512) continue;
-        if (tiles_mn * sp > 256L * per_cu) break;
-        best.splits = sp;
-        best.kps = K / sp;
+      int fsp;
+      if (!geglu && !post && K % 64 == 0 && forced_split(K / 64, 4, fsp)) {
+        best.splits = fsp;
+        best.kps = K / fsp;
+      } else {
+        for (int sp = 2; sp <= 32 && !geglu && !post && K % 64 == 0; ++sp) {
+          if ((K / 64) % sp != 0 || K / sp < 512) continue;
+          if (tiles_mn * sp > 256L * per_cu) break;
+          best.splits = sp;
+          best.kps = K / sp;
+        }
       }
     }
   }

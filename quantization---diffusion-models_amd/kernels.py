@@ -314,6 +314,28 @@ def _cands(ops):
     return out
 
 
+# explicit split-K counts for the shapes whose output tiles cannot fill the GPU (the 16x16 / 8x8
+# levels: M 512-2048 rows against K up to 23040): the library's rule takes the largest split that
+# fits one resident round, whose fp32 slabs (S x M x N) can cost more than the parallelism buys.
+# Candidate id = variant + 1000 * s (qd_gemm_force), s = 1 forcing an unsplit run.
+SPLIT_COUNTS = (1, 2, 3, 4, 6, 8)
+SPLIT_DMA_VARIANTS = (100, 103, 104, 105, 109, 114, 115, 301)
+
+
+def _split_cands(M, N, K, ops, halo=False):
+    if K < 2048 or ((M + 127) // 128) * ((N + 127) // 128) >= 256:
+        return []
+    out = []
+    for i, op in enumerate(ops):
+        if op[1] != "f16":
+            continue
+        for v in SPLIT_DMA_VARIANTS:
+            out += [(i, v + 1000 * s) for s in SPLIT_COUNTS]
+        if halo:
+            out += [(i, v + 1000 * s) for v in (202, 203) for s in (1, 2, 3, 4, 5, 6)]
+    return out
+
+
 # [K / group][N] copies of int4 group scales (the LDS-DMA int4 stages DMA one scale row per K
 # step), made once per scales tensor: keyed by the tensor's id while it lives, re-made when it is
 # edited in place (version counter)
@@ -382,7 +404,8 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        c = _choose(key, _cands(ops), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+        c = _choose(key, _cands(ops) + _split_cands(M, N, K, ops),
+                    lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
     launch(c if c is not None else (0, -1), out, amax, epi, False)
@@ -445,8 +468,11 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
         cands = _cands([(w_khwc, "f16", None, 0)])
-        if kh == 3 and kw == 3 and stride == 1 and pad == 1 and cip % 64 == 0:
+        halo = kh == 3 and kw == 3 and stride == 1 and pad == 1 and cip % 64 == 0
+        if halo:
             cands += [(0, v) for v in HALO_VARIANTS]
+        if cip % 64 == 0:
+            cands += _split_cands(M, co, Kd, [(w_khwc, "f16", None, 0)], halo=halo)
         c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)

@@ -129,6 +129,8 @@ def main():
     else:
         for name in a.models.split(","):
             {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
+        K.W4_CODES_ONLY = True  # the QD_W4_OPERAND=codes policy's int4 linears (their own keys)
+        run_w4(dev)
     K.save_table(a.out)
     log(f"wrote {a.out}")
 
