@@ -29,6 +29,27 @@ __device__ __forceinline__ f16x4 tr_read(const f16* p) {
   return __builtin_bit_cast(f16x4, r);
 }
 
+// raw v_max3 / v_max (no canonicalising v_max x, x in front, which fmaxf brings)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float maxf_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// max with the value of lane l ^ 32 / l ^ 16 (v_permlane32_swap / v_permlane16_swap)
+__device__ __forceinline__ float xmax32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return maxf_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return maxf_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 // LDS row stride (elements) of the row-major V tile: an odd multiple of 8 dwords, so the
 // 8 consecutive rows one 32-lane half reads with ds_read_b64_tr_b16 hit 8 disjoint bank octets.
 constexpr int v_stride(int dv) { return ((dv / 2 / 8) & 1) ? dv : dv + 16; }
@@ -217,15 +238,19 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
     f16x8 pf[NQ][2];
 #pragma unroll
     for (int g = 0; g < NQ; ++g) {
-      // 16 scores -> one max: 8 three-input maxes (hipcc does not form v_max3_f32 from the chain)
-      float mx = sacc[g][0][0];
-#pragma unroll
-      for (int e = 1; e < 16; e += 2) {
-        const float a = sacc[g][e >> 2][e & 3], b = e + 1 < 16 ? sacc[g][(e + 1) >> 2][(e + 1) & 3] : a;
-        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mx) : "v"(mx), "v"(a), "v"(b));
+      // 16 scores -> one max as a depth-3 tree of three-input maxes (a serial chain stalls on each
+      // dependency), then across the 4 lane groups holding the query's other keys with the
+      // gfx950 permlane swaps (VALU, no LDS round trip as a ds_bpermute shuffle would take)
+      float mx;
+      {
+        const f32x4* a = sacc[g];
+        const float m0 = max3f(a[0][0], a[0][1], a[0][2]), m1 = max3f(a[0][3], a[1][0], a[1][1]);
+        const float m2 = max3f(a[1][2], a[1][3], a[2][0]), m3 = max3f(a[2][1], a[2][2], a[2][3]);
+        const float m4 = max3f(a[3][0], a[3][1], a[3][2]);
+        mx = maxf_raw(max3f(m0, m1, m2), max3f(m3, m4, a[3][3]));
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xmax32(mx);
+      mx = xmax16(mx);
       // deferred rescale: the running max is only moved when some lane's max grew by more than
       // 8 (log2 domain; mx is already relative to it), so P stays <= 2^8 (exact in fp16's range,
       // same relative rounding) and the O / denominator rescale is skipped on almost every tile
