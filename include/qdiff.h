@@ -181,6 +181,11 @@ int qd_quant_rows_i8(const void* x, long rows, int c, int ldx, int8_t* y, int ld
  * call unless amax_zeroed (a pooled buffer zeroed once per step). */
 int qd_quant_samples_i8(const void* x, int n, long per_sample, int8_t* y, float* scales, float* amax_ws,
                         int amax_zeroed, void* stream);
+/* qd_quant_samples_i8 with the per-(sample, channel) amax of x [n][rows][c] already reduced by its
+ * producer (a GEMM's QD_EPI_AMAX | QD_EPI_AMAX_POST epilogue): the sample's scale is the max over
+ * amax_nc[n][0..c) - the same value, codes and scales as qd_quant_samples_i8. */
+int qd_quant_samples_i8_amax(const void* x, int n, long per_sample, const float* amax_nc, int c, int8_t* y,
+                             float* scales, void* stream);
 /* y[M, N] = (x_i8[M, K] . w_i8[N, K]^T) * sa[m] * sw[n] (+ epilogue), K % 64 == 0, lda % 16 == 0;
  * sa fp32 [M], sw fp32 [N] (16-B aligned).  Epilogue flags / rows_per_sample / workspace as
  * qd_linear_fwd (workspace size: qd_gemm_i8_workspace).  qd_gemm_force 110..113 picks the tile. */

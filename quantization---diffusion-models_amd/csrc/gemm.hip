@@ -2715,7 +2715,9 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 
 // variant: qd_gemm_force 110..115 (DMA variants 10-15, the 64-B-row family), else a default by
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
-static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu) {
+// post: post-residual amax epilogue - the lock-step DMA tiles only (the ping-pong epilogue
+// reduces before its residual add; split-K slabs would run it in the reduce kernel)
+static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu, bool post = false) {
   if (g_force >= 140 && g_force <= 144 && !geglu && Kh % 288 == 0) {
     // int8 halo conv (applicability checked at launch): 140 BN 160 / 141 BN 128 (3-slot weight
     // ring), 142 / 143 / 144 BN 160 with 4 / 5 / 6 slots; K splits over whole 64-code chunks
@@ -2734,7 +2736,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
       return pl;
     }
   }
-  if (g_force >= 130 && g_force <= 134) {
+  if (g_force >= 130 && g_force <= 134 && !post) {
     // ping-pong: wave rows 128 (BN >= 192) or 64 must lie in one sample for the amax epilogue
     const int bnp = kPpBn[g_force - 130];
     if (!amax || rows_per_sample % (bnp >= 192 ? 128 : 64) == 0) {
@@ -2758,7 +2760,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
   const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
   const int per_cu = std::max(1, std::min(by_lds, by_waves));
-  for (int sp = 2; sp <= 32 && !geglu && Kh % 32 == 0; ++sp) {
+  for (int sp = 2; sp <= 32 && !geglu && !post && Kh % 32 == 0; ++sp) {
     if ((Kh / 32) % sp != 0 || Kh / sp < 256) continue;
     if (tiles_mn * sp > 256L * per_cu) break;
     pl.splits = sp;
@@ -2769,11 +2771,12 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
 
 template <int AMODE>
 static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
-  Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0);
+  const bool post = (p.epi & QD_EPI_AMAX_POST) != 0;
+  Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post);
   if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 32))) {  // int8 halo conv not applicable
     const int f = g_force;
     g_force = -1;
-    pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0);
+    pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post);
     g_force = f;
   }
   if (pl.splits > 1 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N))) {
@@ -2828,7 +2831,8 @@ static int check_i8(const GemmArgs& p) {
 }
 
 extern "C" long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, int epi) {
-  const Plan pl = plan_i8(M, N, K / 2, rows_per_sample, (epi & QD_EPI_AMAX) != 0, (epi & QD_EPI_GEGLU) != 0);
+  const Plan pl = plan_i8(M, N, K / 2, rows_per_sample, (epi & QD_EPI_AMAX) != 0, (epi & QD_EPI_GEGLU) != 0,
+                          (epi & QD_EPI_AMAX_POST) != 0);
   return split_ws_elems(pl, M, N);
 }
 

@@ -843,11 +843,26 @@ __global__ void __launch_bounds__(256) k_sample_absmax(const f16* __restrict__ x
   if (threadIdx.x == 0) atomic_max_pos(amax + n, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
+// c > 0: amax holds the per-(sample, channel) maxima of x [n][rows][c] (reduced by its producer's
+// GEMM epilogue); every block takes the sample's max over them (exact: the same scale as the
+// per-sample reduction)
 __global__ void __launch_bounds__(256) k_sample_apply_i8(const f16* __restrict__ x, long per_sample,
                                                          const float* __restrict__ amax, int8_t* __restrict__ y,
-                                                         float* __restrict__ sa) {
+                                                         float* __restrict__ sa, int c = 0) {
   const long n = blockIdx.y;
-  const float s = fq_scale(amax[n], 127);
+  float an;
+  if (c > 0) {
+    __shared__ float red[4];
+    float m = 0.f;
+    for (int j = threadIdx.x; j < c; j += 256) m = fmaxf(m, amax[n * c + j]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    an = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  } else {
+    an = amax[n];
+  }
+  const float s = fq_scale(an, 127);
   const double rs = rcp_exact(s);
   if (blockIdx.x == 0 && threadIdx.x == 0) sa[n] = s;
   const f16* p = x + n * per_sample;
@@ -862,6 +877,19 @@ __global__ void __launch_bounds__(256) k_sample_apply_i8(const f16* __restrict__
     }
     *reinterpret_cast<uint2*>(q + i) = make_uint2(lo, hi);
   }
+}
+
+extern "C" int qd_quant_samples_i8_amax(const void* x, int n, long per_sample, const float* amax_nc, int c,
+                                        int8_t* y, float* scales, void* stream) {
+  QD_REQUIRE(x && amax_nc && y && scales, "null pointer");
+  QD_REQUIRE(c > 0 && per_sample % c == 0 && per_sample % 8 == 0, "per_sample must be rows * c, a multiple of 8");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 7) == 0, "alignment");
+  if ((long)n * per_sample == 0) return 0;
+  const long ch = (per_sample / 8 + 255) / 256;  // 2048-element blocks per sample
+  const int gx = (int)std::min<long>(std::max<long>(1, 1024 / n), ch);
+  k_sample_apply_i8<<<dim3(gx, n), 256, 0, S(stream)>>>((const f16*)x, per_sample, amax_nc, y, scales, c);
+  QD_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int qd_quant_samples_i8(const void* x, int n, long per_sample, int8_t* y, float* scales, float* amax_ws,

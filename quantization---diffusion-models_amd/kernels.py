@@ -557,13 +557,18 @@ def linear_fp8(xq, sa, w8, gs, bias=None, residual=None, out=None, gelu_tanh=Fal
     return out
 
 
-def quant_samples_i8(x, out=None, scales=None):
+def quant_samples_i8(x, out=None, scales=None, amax_nc=None):
     """int8 codes of x [N, ...] with one scale per sample (the conv-input granularity of the
-    int8 mode): (codes int8 of x's shape, scales [N] fp32)."""
+    int8 mode): (codes int8 of x's shape, scales [N] fp32).  amax_nc: x's per-(sample, channel)
+    amax [N * C] from its producer's epilogue (the sample max is taken over it: same result)."""
     _chk(x, "x")
     n = x.shape[0]
     q = out if out is not None else _empty(x.shape, torch.int8, x.device)
     sa = scales if scales is not None else _empty((n,), torch.float32, x.device)
+    if amax_nc is not None:
+        _lib.call("qd_quant_samples_i8_amax", _p(x), n, x.numel() // max(n, 1), _p(amax_nc), x.shape[-1], _p(q),
+                  _p(sa), _stream())
+        return q, sa
     ws, zeroed = A.zeroed_f32(n, x.device)
     _lib.call("qd_quant_samples_i8", _p(x), n, x.numel() // max(n, 1), _p(q), _p(sa), _p(ws), 1 if zeroed else 0,
               _stream())
@@ -611,7 +616,7 @@ def _i8_ws(M, N, K, rows_per_sample, epi, device, scratch=False):
 
 
 def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, rows_per_sample=0, amax_zeroed=False,
-              geglu=False, gelu_tanh=False):
+              geglu=False, gelu_tanh=False, amax_post=False):
     """y = half((xq . wq^T) * sa[m] * sw[n] (+ bias)) (+ residual / GEGLU / GELU-tanh / amax as
     linear()); xq [M, K] int8 codes (row stride % 16 == 0), sa [M] fp32, wq [N, K] int8, sw [N] fp32."""
     if xq.dtype != torch.int8 or wq.dtype != torch.int8 or not xq.is_cuda:
@@ -626,7 +631,8 @@ def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, row
         out = _empty((M, N // 2 if geglu else N), torch.float16, xq.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
-          (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0)
+          (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0) | \
+          (EPI_AMAX_POST if amax_post and amax is not None and residual is not None else 0)
 
     def launch(c, y, am, ep, scratch):
         _force(c if _OVERRIDE is None else _OVERRIDE)

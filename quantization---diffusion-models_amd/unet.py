@@ -466,7 +466,8 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         if isinstance(x, tuple):  # (int8 codes, per-sample scales) from a fused producer
             return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer)
         if i8 is not None and co_pad in (None, layer.out_channels) and x.shape[-1] == layer.ci_pad:
-            return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer)
+            return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer,
+                                in_amax if x.shape[-1] == layer.in_channels else None)
     wk, bias = _conv_weight(layer, co_pad)
     stride, pad = layer.stride[0], layer.padding[0]
     ci = layer.weight.shape[1]
@@ -513,12 +514,13 @@ def lin_i8(layer):
         getattr(layer, "_qd_hook", None) is None
 
 
-def _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer):
+def _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer, in_amax=None):
     """int8-MFMA mode conv: per-sample int8 codes of the fp16 NHWC input (or the producer's fused
     (codes, scales)), int8 implicit GEMM with the output (+ bias, + residual) in fp16; the
     time-embedding add is deferred to the consumer like the fake-quant path's (no output
-    fake-quant in this mode)."""
-    xq, sa = x if isinstance(x, tuple) else K.quant_samples_i8(x)
+    fake-quant in this mode).  in_amax: x's per-(n, c) amax from its producer's epilogue (the
+    per-sample scale is taken over it instead of a separate reduction pass)."""
+    xq, sa = x if isinstance(x, tuple) else K.quant_samples_i8(x, amax_nc=in_amax)
     y = K.conv2d_i8(xq, sa, i8[0], i8[1], layer.in_channels, layer.stride[0], layer.padding[0], upsample,
                     bias=layer.bias, residual=residual)
     if chan_add is None:
@@ -731,7 +733,9 @@ def transformer_fwd(tm, x, ctx_kv, pend=False):
     # the last block's feed-forward output GEMM reduces proj_out's per-(n, c) input amax in its
     # epilogue (post-residual) when proj_out quantizes per channel through the fp16 path
     q_out = 0 if tm.linear_proj or conv_i8(tm.proj_out) else conv_qbits(tm.proj_out)
-    want = AMAX_POST and q_out > 0 and n * hh * ww >= AMAX_POST_MIN_ROWS and (hh * ww) % 64 == 0
+    # int8-MFMA mode: the same epilogue amax gives proj_out's per-sample int8 scale
+    i8_out = I8_AMAX_FUSE and not tm.linear_proj and conv_i8(tm.proj_out) and lin_i8(tm.transformer_blocks[-1].ff.net[2])
+    want = AMAX_POST and (q_out > 0 or i8_out) and n * hh * ww >= AMAX_POST_MIN_ROWS and (hh * ww) % 64 == 0
     in_amax = None
     for bi, blk in enumerate(tm.transformer_blocks):
         last = bi == len(tm.transformer_blocks) - 1
@@ -848,6 +852,15 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
     h = ln(blk.norm3, lin_i8(blk.ff.net[0].proj) and blk.ff.net[0].proj.output_quant_name == "None")
     g = ff_geglu(blk.ff.net[0].proj, h)
     fo = blk.ff.net[2]
+    if want_amax and lin_i8(fo) and fo.output_quant_name == "None" and g.shape[0] >= I8_MIN_ROWS:
+        # int8-MFMA mode: per-token codes of the GEGLU output, the block output's per-(n, c) amax
+        # after the residual add reduced in the GEMM epilogue (proj_out's per-sample scale)
+        i8 = fo.i8_operand()
+        xq, sa = K.quant_rows_i8(g)
+        amax, zeroed = A.zeroed_f32(n * c, t.device)
+        out = K.linear_i8(xq, sa, i8[0], i8[1], bias=fo.bias, residual=t, amax=amax, rows_per_sample=s,
+                          amax_zeroed=zeroed, amax_post=True)
+        return out, amax
     op = _fake_quant_gemm_operand(fo) if want_amax and not isinstance(g, tuple) and g.shape[0] >= I8_MIN_ROWS else None
     if op is not None:
         w, fmt, sc, gr, wf = op
@@ -863,6 +876,7 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
 AMAX_POST_MIN_ROWS = 8192
 AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
 LN_FQ = not os.environ.get("QD_NO_LN_FQ")  # A/B switch: proj_in finalize as its own pass before norm1
+I8_AMAX_FUSE = not os.environ.get("QD_NO_I8_AMAX_FUSE")  # A/B switch: proj_out's int8 scale by its own pass
 
 
 def _fake_quant_gemm_operand(layer):
