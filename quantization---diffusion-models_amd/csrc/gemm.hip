@@ -412,6 +412,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // HBM latency NR / 2 times)
     constexpr int CPR16 = BN / 8, NR = (BM * CPR16 + NT - 1) / NT;
     const bool pre_res = has_res && !post && !geglu;
+    // post-residual amax: the residual in the fragments' layout (4 consecutive columns of one row
+    // per lane and fragment), all TM x TN 8-B loads issued before any is used
+    constexpr bool PF_POST = TM * TN <= 20;  // (register budget: the 4 x 5 fragment tiles and smaller)
+    f16x4 rf[PF_POST ? TM : 1][PF_POST ? TN : 1];
+    if (PF_POST && post) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 16 + fq * 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wm0 + i * 16 + fr;
+          if constexpr (PF_POST)
+            rf[i][j] = (m < p.M && n < p.N) ? *reinterpret_cast<const f16x4*>(p.res + (long)m * p.ldy + n) : f16x4{};
+        }
+      }
+    }
     f16x8 rq[NR];
     if (pre_res) {
 #pragma unroll
@@ -440,9 +456,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           if (post) {
             const bool ok = m0 + ml < p.M && col_ok;
             if (ok) {
-              const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)(m0 + ml) * p.ldy + n);
+              f16x4 rv;
+              if constexpr (PF_POST) rv = rf[i][j];
+              else rv = *reinterpret_cast<const f16x4*>(p.res + (long)(m0 + ml) * p.ldy + n);
 #pragma unroll
-              for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
+              for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rv[r]);
             }
           }
           if (do_amax) {  // (uniform) the column maxes only when an amax is reduced
