@@ -874,6 +874,170 @@ static void launch_ln(const f16* x, long rows, int c, float eps, const f16* g, c
   else k_layernorm<PER, 1, I8><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, eps, g, b, y, y8, sa8);
 }
 
+// ---------------------------------------------------------------------------------------
+// Grouped-row LayerNorm (every C = 8 * LPR * P with LPR in {8..64} lanes per row, P <= 5 16-B
+// chunks per lane: SD's 320 / 640 / 1280 / 2560, CLIP's 768 / 1280): a wave holds 64 / LPR rows at
+// once, lane l of a row owning chunks l, l + LPR, ... (coalesced), so all 64 lanes carry data
+// (the one-row-per-wave kernel above leaves 24 of 64 lanes idle at C 320) and 64 / LPR rows' loads
+// are in flight per wave.  Sums: each lane's P x 8 values in order, then a butterfly over the row's
+// LPR lanes.  MODE 0: fp16 out; 1: int8 codes + one scale per row (the int8-MFMA mode's linear
+// input); 2: the input is a conv output with its per-(sample, channel) output fake-quant pending -
+// t = fq(y) is written (the residual stream) and LayerNorm(t) (qd_layernorm_fq).  The three modes
+// share the arithmetic, so LN-fq == finalize + LN and LN-int8 == LN + per-row quant bit for bit.
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int LPR>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int LPR, int P, int MODE>
+__global__ void __launch_bounds__(256) k_ln_rows(const f16* __restrict__ x, long rows, int c, float eps,
+                                                 const f16* __restrict__ gamma, const f16* __restrict__ beta,
+                                                 f16* __restrict__ y, int8_t* __restrict__ y8, float* __restrict__ sa8,
+                                                 int iters, int rps, const float* __restrict__ amax, int qmax,
+                                                 f16* __restrict__ t_out) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, lr = lane % LPR, rw = lane / LPR;
+  const long wrow0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW * iters;
+  // MODE 2: the sample's C scales s and 1/s, computed once per block into LDS (a block's rows lie in
+  // one sample: host check rps % (4 * RPW * iters) == 0); held in registers they would cost 120 VGPRs
+  extern __shared__ double lds_fq[];
+  if constexpr (MODE == 2) {
+    const long n = (long)blockIdx.x * 4 * RPW * iters / rps;
+    float* ssc = reinterpret_cast<float*>(lds_fq + c);
+    for (int j = threadIdx.x; j < c / 8; j += 256) {
+      float s8[8];
+      double r8[8];
+      fq_scales8(amax + n * c + j * 8, qmax, s8, r8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        lds_fq[j * 8 + e] = r8[e];
+        ssc[j * 8 + e] = s8[e];
+      }
+    }
+    __syncthreads();
+  }
+  if (wrow0 >= rows) return;
+  f16x8 g[P], b[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    g[i] = *reinterpret_cast<const f16x8*>(gamma + (lr + i * LPR) * 8);
+    b[i] = *reinterpret_cast<const f16x8*>(beta + (lr + i * LPR) * 8);
+  }
+  for (int it = 0; it < iters; ++it) {
+    const long row = wrow0 + (long)it * RPW + rw;
+    const bool ok = row < rows;
+    f16x8 v[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+      v[i] = ok ? *reinterpret_cast<const f16x8*>(x + row * c + (lr + i * LPR) * 8) : (f16x8){};
+    if constexpr (MODE == 2) {
+      const float* ssc = reinterpret_cast<const float*>(lds_fq + c);
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int ch = (lr + i * LPR) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = fq_apply_r((float)v[i][e], ssc[ch + e], lds_fq[ch + e]);
+        if (ok) *reinterpret_cast<f16x8*>(t_out + row * c + (lr + i * LPR) * 8) = v[i];
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)v[i][e];
+    const float mean = group_sum<LPR>(s) / (float)c;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = (float)v[i][e] - mean;
+        q = fmaf(a, a, q);
+      }
+    const float rstd = 1.0f / sqrtf(group_sum<LPR>(q) / (float)c + eps);
+    f16x8 o[P];
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[i][e] = to_f16(fmaf(((float)v[i][e] - mean) * rstd, (float)g[i][e], (float)b[i][e]));
+        if (MODE == 1) m = fmaxf(m, fabsf((float)o[i][e]));
+      }
+    if constexpr (MODE == 1) {
+      const float s8 = fq_scale(group_max<LPR>(m), 127);
+      const double r8 = rcp_exact(s8);
+      if (ok && lr == 0) sa8[row] = s8;
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        unsigned lo = 0, hi = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const f16 tq = (f16)(float)((double)(float)o[i][e] * r8);
+          const unsigned qv = (unsigned)(uint8_t)(int8_t)__builtin_rintf((float)tq);
+          if (e < 4) lo |= qv << (8 * e);
+          else hi |= qv << (8 * (e - 4));
+        }
+        if (ok) *reinterpret_cast<uint2*>(y8 + row * c + (lr + i * LPR) * 8) = make_uint2(lo, hi);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < P; ++i)
+        if (ok) *reinterpret_cast<f16x8*>(y + row * c + (lr + i * LPR) * 8) = o[i];
+    }
+  }
+}
+
+// (LPR, P) of the grouped-row kernel for C, or LPR = 0 (the one-row-per-wave kernels)
+static void ln_rows_geom(int c, int& lpr, int& per) {
+  lpr = per = 0;
+  if (c % 8) return;
+  const int ch = c / 8;
+  for (int l = 8; l <= 64; l *= 2)
+    if (ch % l == 0 && ch / l <= 5) {
+      lpr = l;
+      per = ch / l;
+      return;
+    }
+}
+static bool ln_rows_env() {
+  static const bool off = getenv("QD_LN_ROWS_OFF") != nullptr;  // A/B switch: the one-row-per-wave kernels
+  return !off;
+}
+
+template <int MODE>
+static bool launch_ln_rows(const f16* x, long rows, int c, float eps, const f16* g, const f16* b, f16* y, int8_t* y8,
+                           float* sa8, int rps, const float* amax, int qmax, f16* t_out, hipStream_t st) {
+  int lpr, per;
+  ln_rows_geom(c, lpr, per);
+  if (!lpr || !ln_rows_env()) return false;
+  const int rpw = 64 / lpr;
+  int iters = 1;  // more rows per wave while the grid keeps >= 1024 blocks
+  while (iters < 4 && (rows + 4L * rpw * iters * 2 - 1) / (4L * rpw * iters * 2) >= 1024) iters *= 2;
+  if (MODE == 2) {
+    while (iters > 1 && rps % (4 * rpw * iters)) iters >>= 1;
+    if (rps % (4 * rpw)) return false;
+  }
+  const int grid = (int)((rows + 4L * rpw * iters - 1) / (4L * rpw * iters));
+  const size_t lds = MODE == 2 ? (size_t)c * 12 : 0;
+#define QD_LNR(L, PP)                                                                                          \
+  if (lpr == L && per == PP) {                                                                                 \
+    k_ln_rows<L, PP, MODE><<<grid, 256, lds, st>>>(x, rows, c, eps, g, b, y, y8, sa8, iters, rps, amax, qmax, t_out); \
+    return true;                                                                                               \
+  }
+  QD_LNR(8, 5) QD_LNR(16, 5) QD_LNR(32, 3) QD_LNR(32, 4) QD_LNR(32, 5) QD_LNR(64, 2) QD_LNR(64, 4) QD_LNR(64, 5)
+#undef QD_LNR
+  return false;
+}
+
 // LayerNorm of a conv output whose per-(sample, channel) output fake-quant is still pending
 // (Transformer2DModel proj_in -> BasicTransformerBlock norm1): t = fq(y; amax[n][c]) is written
 // (the block's residual stream, k_finalize's arithmetic) and LayerNorm(t) (k_layernorm's) in the
@@ -975,6 +1139,10 @@ extern "C" int qd_layernorm_fq(const void* x, const float* amax, int n_bits, int
   const int qm = (1 << (n_bits - 1)) - 1;
   hipStream_t st = S(stream);
   const f16 *xp = (const f16*)x, *g = (const f16*)gamma, *b = (const f16*)beta;
+  if (launch_ln_rows<2>(xp, rows, c, eps, g, b, (f16*)y, nullptr, nullptr, rows_per_sample, amax, qm, (f16*)t_out, st)) {
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
 #define QD_LNFQ(P, RR) \
   k_fq_layernorm<P, RR><<<grid, 256, 0, st>>>(xp, rows, c, rows_per_sample, amax, qm, eps, g, b, (f16*)t_out, (f16*)y)
   if (per <= 1) QD_LNFQ(1, 4);
@@ -995,6 +1163,10 @@ extern "C" int qd_layernorm_i8(const void* x, int rows, int c, float eps, const 
   const int per = (c / 8 + 63) / 64;
   hipStream_t st = S(stream);
   const f16 *xp = (const f16*)x, *g = (const f16*)gamma, *b = (const f16*)beta;
+  if (launch_ln_rows<1>(xp, rows, c, eps, g, b, nullptr, y8, scales, 0, nullptr, 0, nullptr, st)) {
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
   if (per <= 1) launch_ln<1, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
   else if (per <= 2) launch_ln<2, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
   else if (per <= 3) launch_ln<3, true>(xp, rows, c, eps, g, b, nullptr, st, y8, scales);
@@ -1015,6 +1187,10 @@ extern "C" int qd_layernorm(const void* x, int rows, int c, float eps, const voi
   hipStream_t st = S(stream);
   const f16 *xp = (const f16*)x, *g = (const f16*)gamma, *b = (const f16*)beta;
   f16* yp = (f16*)y;
+  if (launch_ln_rows<0>(xp, rows, c, eps, g, b, yp, nullptr, nullptr, 0, nullptr, 0, nullptr, st)) {
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
   if (per <= 1) launch_ln<1>(xp, rows, c, eps, g, b, yp, st);
   else if (per <= 2) launch_ln<2>(xp, rows, c, eps, g, b, yp, st);
   else if (per <= 3) launch_ln<3>(xp, rows, c, eps, g, b, yp, st);
