@@ -117,7 +117,7 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
  * wfmt: QD_WFMT_*; wscale [N][K/group] fp16 for I8/I4.  wscale_t (I4 only, optional, 16-B
  * aligned): the same scales as [K/group][N]; with it the int4 codes also run in the LDS-DMA /
- * ping-pong families (qd_gemm_force 110..115, 300..304), dequantized from LDS per fragment with the
+ * ping-pong families (qd_gemm_force 110..117, 300..304), dequantized from LDS per fragment with the
  * register tile's rounding (bit-identical results).  lda/ldy in elements.
  * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32).
  * M <= 4 without AMAX / GEGLU runs a weight-stream GEMV (same dequant and epilogue rounding;
@@ -130,7 +130,7 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
 /* Tuning / test knob (process-global, not thread-safe): force the GEMM kernel family of every
  * following qd_linear_fwd / qd_conv2d_fwd.  -1 = planner's choice (default); 0..3 = the
  * register-staged tiles 128x160, 128x128, 128x64, 64x64; 100 + i = LDS-DMA variant i (F16
- * weights; packed int4 with wscale_t: the BK-32 variants 110..115 and ping-pong 300..304; other
+ * weights; packed int4 with wscale_t: the BK-32 variants 110..117 and ping-pong 300..304; other
  * quantized formats keep the planner's register-staged choice). */
 int qd_gemm_force(int variant);
 

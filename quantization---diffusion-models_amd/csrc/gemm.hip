@@ -2098,6 +2098,10 @@ static constexpr DmaVar kDmaC[] = {
     {256, 256, 2, 4, 4, 0, 1.00, 32},  // 13: BK 32, 4 stages, 1 block / CU
     {128, 64, 2, 2, 4, 0, 1.00, 32},   // 14: BK 32, 4 stages, small-M / short-K shapes
     {64, 64, 2, 2, 4, 0, 1.00, 32},    // 15: BK 32, 4 stages, small-M / short-K shapes
+    // short-K, large-N tiles with 2 blocks / CU (4 waves, 64 x 128 / 128 x 64 wave tiles): one block's
+    // epilogue (GELU VALU, output stores) can run beside the other block's MFMAs
+    {128, 256, 2, 2, 3, 0, 1.00, 32},  // 16
+    {256, 128, 2, 2, 3, 0, 1.00, 32},  // 17
 };
 static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
 static int g_split = 0;   // with a forced DMA / ping-pong / halo variant: exact split-K count (0 = the fit rule)
@@ -2119,7 +2123,7 @@ extern "C" int qd_gemm_force(int variant) {
   QD_REQUIRE(v == -1 || (v >= 0 && v < 4) ||
                  (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 203) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
                  (v >= 130 && v <= 134) || (v >= 140 && v <= 144),
-             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..113, fp8: 120..123), 200-203 halo conv, "
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..117, fp8: 120..123), 200-203 halo conv, "
              "300-304 ping-pong (int8: 130-134, int8 halo conv 140-144); + 1000 * s: split-K count s (1 = unsplit)");
   QD_REQUIRE(sp <= 32, "qd_gemm_force: split count above 32");
   g_force = v;
@@ -2203,7 +2207,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         }
       }
     }
-  } else if (g_force >= 100 && g_force < 200 &&
+  } else if (g_force >= 100 && g_force < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0])) &&
              (!quant_w || (w4 && w4g % kDmaC[g_force - 100].bkt == 0 && kDmaC[g_force - 100].pipe == 0))) {
     const DmaVar& d = kDmaC[g_force - 100];
     const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
@@ -2272,6 +2276,8 @@ static void launch_dma(const GemmArgs& p, int var, hipStream_t st, int fmt = QD_
         case 12: launch_dma_w4_v<12, SPLIT>(p, st); break;
         case 13: launch_dma_w4_v<13, SPLIT>(p, st); break;
         case 14: launch_dma_w4_v<14, SPLIT>(p, st); break;
+        case 16: launch_dma_w4_v<16, SPLIT>(p, st); break;
+        case 17: launch_dma_w4_v<17, SPLIT>(p, st); break;
         default: launch_dma_w4_v<15, SPLIT>(p, st); break;
       }
       return;
@@ -2293,6 +2299,8 @@ static void launch_dma(const GemmArgs& p, int var, hipStream_t st, int fmt = QD_
     case 12: launch_dma_v<12, AMODE, SPLIT>(p, st); break;
     case 13: launch_dma_v<13, AMODE, SPLIT>(p, st); break;
     case 14: launch_dma_v<14, AMODE, SPLIT>(p, st); break;
+    case 16: launch_dma_v<16, AMODE, SPLIT>(p, st); break;
+    case 17: launch_dma_v<17, AMODE, SPLIT>(p, st); break;
     default: launch_dma_v<15, AMODE, SPLIT>(p, st); break;
   }
 }
@@ -2727,11 +2735,13 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
     case 13: launch_i8_v<13, AMODE, SPLIT>(p, st); break;
     case 14: launch_i8_v<14, AMODE, SPLIT>(p, st); break;
     case 15: launch_i8_v<15, AMODE, SPLIT>(p, st); break;
+    case 16: launch_i8_v<16, AMODE, SPLIT>(p, st); break;
+    case 17: launch_i8_v<17, AMODE, SPLIT>(p, st); break;
     default: launch_i8_v<11, AMODE, SPLIT>(p, st); break;
   }
 }
 
-// variant: qd_gemm_force 110..115 (DMA variants 10-15, the 64-B-row family), else a default by
+// variant: qd_gemm_force 110..117 (DMA variants 10-17, the 64-B-row family), else a default by
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 // post: post-residual amax epilogue - the lock-step DMA tiles only (the ping-pong epilogue
 // reduces before its residual add; split-K slabs would run it in the reduce kernel)
@@ -2770,7 +2780,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
     }
   }
   int var = N % 160 == 0 ? 10 : 11;
-  if (g_force >= 110 && g_force <= 115) var = g_force - 100;
+  if (g_force >= 110 && g_force <= 117) var = g_force - 100;
   if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];

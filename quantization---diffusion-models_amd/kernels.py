@@ -180,12 +180,12 @@ def conv_weight_khwc(w, ci_pad):
 # candidates reduce fixed-order fp32 slabs (deterministic for a given choice).
 # QD_GEMM_TUNE=0 disables the search (library planner only).
 REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
-DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 114, 115,   # LDS-DMA variants (fp16 weights)
+DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 114, 115, 116, 117,   # LDS-DMA variants (fp16 weights)
                 300, 301, 302, 303, 304)                        # ping-pong 256-row
 HALO_VARIANTS = (200, 201, 202, 203)  # 3x3 conv with the activation halo staged once per channel chunk
 # packed int4 through the lock-step LDS-DMA stages and the ping-pong tiles (BDma4 code stages,
 # dequantized per fragment)
-W4_VARIANTS = (100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115, 300, 301, 302, 303, 304)
+W4_VARIANTS = (100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115, 116, 117, 300, 301, 302, 303, 304)
 _TUNE = {}
 _USED = set()  # GEMM keys this process has launched (bench reporting: gemm_choices(used_only=True))
 _TUNE_ON = os.environ.get("QD_GEMM_TUNE", "1") != "0"
@@ -483,7 +483,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 # ---------------------------------------------------------------- int8-MFMA W8A8 mode
 # int8 x int8 GEMMs (qd_linear_i8 / qd_conv2d_i8): exact int32 sums, so every tile variant and
 # split gives identical bits - the tuner below only picks the fastest.
-I8_VARIANTS = (110, 111, 112, 113, 114, 115,   # qd_gemm_force ids: LDS-DMA variants 10-15 (64-B rows)
+I8_VARIANTS = (110, 111, 112, 113, 114, 115, 116, 117,  # qd_gemm_force ids: LDS-DMA variants 10-17 (64-B rows)
                130, 131, 132, 133, 134)  # ping-pong 256 x {256, 320, 192, 160, 128}
 I8_HALO_VARIANTS = (140, 141, 142, 143, 144)  # 3x3 conv, activation halo staged once per 64-code chunk (BN 160 / 128; 142-144 deeper weight rings)
 

@@ -17,7 +17,7 @@ def K():
 
 
 # tuned choice, the LDS-DMA variants and the 256-row ping-pong variants (kernels.I8_VARIANTS)
-I8_FORCE = [None, 110, 111, 112, 113, 114, 115, 130, 131, 132, 133, 134]
+I8_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 130, 131, 132, 133, 134]
 
 
 def _bits(a):

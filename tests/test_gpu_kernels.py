@@ -517,7 +517,7 @@ def forced_gemm():
     kernels.force_gemm(None)
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 3] + list(range(100, 116)) + [300, 301])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 3] + list(range(100, 118)) + [300, 301])
 @pytest.mark.parametrize("fmt", ["f16", "i8"])
 def test_linear_post_residual_amax(variant, fmt, forced_gemm, dev):
     """QD_EPI_AMAX_POST: the epilogue adds the residual to the fragments and reduces the
@@ -598,7 +598,7 @@ def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     assert ((fused - ref).abs() <= tol).all(), (variant, (fused - ref).abs().max().item())
 
 
-@pytest.mark.parametrize("variant", [100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115,
+@pytest.mark.parametrize("variant", [100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115, 116, 117,
                                      300, 301, 302, 303, 304])
 def test_int4_lds_dma_variants_bit_identical(variant, forced_gemm, dev):
     """Packed-int4 codes through the LDS-DMA / ping-pong families (BDma4: codes + the K step's
