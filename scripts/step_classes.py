@@ -5,7 +5,7 @@ import csv
 import sys
 
 CLASSES = [("GEMM/conv", ("k_gemm", "k_conv_halo", "k_gemv")), ("split-K reduce", ("k_splitk",)),
-           ("attention", ("k_attn",)), ("GroupNorm", ("k_gn_",)), ("LayerNorm", ("k_layernorm",)),
+           ("attention", ("k_attn",)), ("GroupNorm", ("k_gn_",)), ("LayerNorm", ("k_layernorm", "k_ln_rows", "k_fq_layernorm")),
            ("finalize", ("k_finalize",)), ("colmax + apply", ("k_colmax", "k_apply", "k_act_")),
            ("int8 act quant", ("k_quant_rows_i8", "k_sample_")), ("scheduler / embed", ("k_cfg", "k_timestep")),
            ("elementwise", ("k_silu", "k_add", "k_concat", "k_geglu", "k_zero", "k_nchw", "k_nhwc"))]
