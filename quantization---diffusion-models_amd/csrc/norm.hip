@@ -153,8 +153,10 @@ static GnGeom gn_geom(int n, int hw, int c) {
   g.bx = std::min(chunks, 256);
   g.by = 256 / g.bx;
   g.gx = (chunks + g.bx - 1) / g.bx;
-  g.rpb = g.by * 4;  // >= 4 rows per thread, more blocks while the grid is small
-  while (g.rpb > g.by && (long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) < 2048) g.rpb /= 2;
+  // >= 4 rows per thread: the per-thread setup (coefficients, fake-quant scales) is amortised over
+  // 4 rows (2 rows per thread, the earlier rule's choice for grids under 2048 blocks, measured 5-9 %
+  // slower on every SD1.5 streaming shape: profiles/r03w_gn_geom_sweep.log)
+  g.rpb = g.by * 4;
   while ((long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) > 8192) g.rpb *= 2;
   if (g_gn_arpt) g.rpb = g.by * g_gn_arpt;
   g.z = (hw + g.rpb - 1) / g.rpb;
