@@ -195,8 +195,9 @@ static CrGeom cr_geom(int n, long hw, int c) {
   g.bx = chunks < 256 ? chunks : 256;
   g.by = 256 / g.bx;
   g.gx = (chunks + g.bx - 1) / g.bx;
+  // >= 4 rows per thread: the per-thread fake-quant scale setup (two amax loads, 8 f64
+  // reciprocals) is amortised over 4 rows, as in the GroupNorm apply (profiles/r03z_*)
   g.rpb = g.by * 4;
-  while (g.rpb > g.by && (long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) < 2048) g.rpb /= 2;
   while ((long)g.gx * n * ((hw + g.rpb - 1) / g.rpb) > 8192) g.rpb *= 2;
   g.z = (int)((hw + g.rpb - 1) / g.rpb);
   return g;
