@@ -2755,6 +2755,12 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
       const long tiles_mn = (long)(M / 256) * (N / bn);
       const int nc = Kh / 288;
       Plan pl{2, 256, bn, g_force - 140, 1, nc};
+      int fsp;
+      if (forced_split(nc, 1, fsp)) {  // explicit split count (tuner candidate)
+        pl.splits = fsp;
+        pl.kps = nc / fsp;
+        return pl;
+      }
       for (int sp = 2; sp <= nc; ++sp) {
         if (nc % sp != 0) continue;
         if (tiles_mn * sp > 256) break;
@@ -2770,6 +2776,12 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
     if (!amax || rows_per_sample % (bnp >= 192 ? 128 : 64) == 0) {
       Plan pl{3, 256, bnp, 0, 1, Kh};
       const long tiles_mn = (long)((M + 255) / 256) * ((N + bnp - 1) / bnp);
+      int fsp;
+      if (!geglu && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp)) {
+        pl.splits = fsp;
+        pl.kps = Kh / fsp;
+        return pl;
+      }
       for (int sp = 2; sp <= 32 && !geglu && Kh % 32 == 0; ++sp) {
         if ((Kh / 32) % sp != 0 || Kh / sp < 256) continue;
         if (tiles_mn * sp > 256L) break;
@@ -2788,6 +2800,12 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
   const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
   const int per_cu = std::max(1, std::min(by_lds, by_waves));
+  int fsp;
+  if (g_force >= 110 && !geglu && !post && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp)) {
+    pl.splits = fsp;
+    pl.kps = Kh / fsp;
+    return pl;
+  }
   for (int sp = 2; sp <= 32 && !geglu && !post && Kh % 32 == 0; ++sp) {
     if ((Kh / 32) % sp != 0 || Kh / sp < 256) continue;
     if (tiles_mn * sp > 256L * per_cu) break;

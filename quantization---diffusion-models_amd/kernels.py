@@ -336,6 +336,20 @@ def _split_cands(M, N, K, ops, halo=False):
     return out
 
 
+# int8 (int32 partial slabs: every split count gives the same bits) - explicit split counts for
+# the int8 GEMMs whose tiles cannot fill the GPU; K in int8 codes
+I8_SPLIT_VARIANTS = (110, 111, 115, 133)
+
+
+def _i8_split_cands(M, N, K, halo=False):
+    if K < 2048 or ((M + 127) // 128) * ((N + 127) // 128) >= 256:
+        return []
+    out = [v + 1000 * s for v in I8_SPLIT_VARIANTS for s in SPLIT_COUNTS]
+    if halo:
+        out += [v + 1000 * s for v in (142, 143) for s in (1, 2, 3, 4, 5, 6)]
+    return out
+
+
 # [K / group][N] copies of int4 group scales (the LDS-DMA int4 stages DMA one scale row per K
 # step), made once per scales tensor: keyed by the tensor's id while it lives, re-made when it is
 # edited in place (version counter)
@@ -648,7 +662,8 @@ def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, row
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        c = _choose(key, list(I8_VARIANTS), lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+        c = _choose(key, list(I8_VARIANTS) + ([] if epi & (EPI_GEGLU | EPI_AMAX_POST) else _i8_split_cands(M, N, Kd)),
+                    lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
     launch(c if c is not None else -1, out, amax, epi, False)
@@ -687,7 +702,9 @@ def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, 
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        cands = list(I8_VARIANTS) + (list(I8_HALO_VARIANTS) if (kh, kw, stride, pad) == (3, 3, 1, 1) else [])
+        halo = (kh, kw, stride, pad) == (3, 3, 1, 1)
+        cands = list(I8_VARIANTS) + (list(I8_HALO_VARIANTS) if halo else []) + \
+            _i8_split_cands(M, co, Kd, halo)
         c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)

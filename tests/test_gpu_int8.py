@@ -18,6 +18,8 @@ def K():
 
 # tuned choice, the LDS-DMA variants and the 256-row ping-pong variants (kernels.I8_VARIANTS)
 I8_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 130, 131, 132, 133, 134]
+# explicit split-K counts (variant + 1000 * s; the int32 slabs make every split bit-identical)
+I8_SPLIT_FORCE = [1110, 3110, 4111, 2115, 6133, 8111]
 
 
 def _bits(a):
@@ -51,7 +53,7 @@ def test_sample_codes(dev):
 
 @pytest.mark.parametrize("M,N,Kd", [(64, 64, 64), (200, 320, 320), (616, 640, 768), (4096, 2560, 320),
                                     (8, 1280, 1280), (1000, 64, 128), (256, 1280, 5120), (77, 320, 2560)])
-@pytest.mark.parametrize("variant", I8_FORCE)
+@pytest.mark.parametrize("variant", I8_FORCE + I8_SPLIT_FORCE)
 def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
     k = K()
     rng = np.random.default_rng(M + N + Kd)
@@ -107,7 +109,7 @@ def _geglu_amax(k, dev):
                                                         (1280, 1280, 3, 1, 8, False), (960, 320, 3, 1, 16, False),
                                                         (320, 320, 3, 1, 64, False), (640, 640, 3, 1, 32, False),
                                                         (1280, 1280, 3, 1, 16, False), (640, 320, 3, 1, 32, True)])
-@pytest.mark.parametrize("variant", I8_FORCE + [140, 141, 142, 143, 144])
+@pytest.mark.parametrize("variant", I8_FORCE + [140, 141, 142, 143, 144] + I8_SPLIT_FORCE + [1142, 2142, 3143, 5142])
 def test_conv2d_i8_bit_exact(cin, cout, ksz, stride, hw, ups, variant, dev):
     k = K()
     rng = np.random.default_rng(cin * 7 + cout + ksz)
