@@ -164,7 +164,7 @@ def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320, int8=False):
     tflops = flops / (ms * 1e-3) / 1e12
     peak = PEAK_I8_TOPS if int8 else PEAK_F16_TFLOPS
     choice = _conv_choice((n, h, w, c), "conv_i8" if int8 else "conv")
-    tr = pmc_traffic(choice["variant"] if choice else None) if (n, h, w, c) == (8, 64, 64, 320) and not int8 else None
+    tr = pmc_traffic(choice["variant"] if choice else None, int8) if (n, h, w, c) == (8, 64, 64, 320) else None
     return {"bound": "mfma", "achieved": round(tflops, 1), "peak": peak, "unit": "TOP/s" if int8 else "TFLOP/s",
             "frac": round(tflops / peak, 4), "traffic": (tr or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "bytes per launch (rocprofv3 PMC)", "traffic_detail": tr,
@@ -181,7 +181,12 @@ def _conv_choice(shape=(8, 64, 64, 320), kind="conv"):
     for key, ch in K.gemm_choices().items():
         if kind == "conv_i8":
             if key[:8] == ("conv_i8", n, h, w, c, c, 3, 3):
-                return {"variant": ch, "family": "k_gemm_dma<I8>"} if ch else None
+                if not ch:
+                    return None
+                v = ch % 1000  # (+ 1000 * s: an explicit split-K count)
+                fam = ("k_conv_halo_i8" if 140 <= v <= 144 else "k_gemm_pp<I8>" if 130 <= v <= 134 else
+                       "k_gemm_dma<I8>")
+                return {"variant": ch, "family": fam}
             continue
         if key[:8] == ("conv", n, h, w, c, c, 3, 3):
             fam = ("k_gemm_pp" if ch and ch[1] >= 300 else "k_conv_halo" if ch and ch[1] >= 200 else
@@ -272,7 +277,7 @@ def weight_footprint(model):
             "tuned per shape: int4 codes vs the fp16 dequantized buffer (default)"}
 
 
-def pmc_traffic(variant=None):
+def pmc_traffic(variant=None, int8=False):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 --pmc
     measurement (profiles/*pmc_dominant.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes over
     scripts/roof_kernel.py - the same kernel and shape as dominant_kernel_roofline(), per GEMM
@@ -284,12 +289,16 @@ def pmc_traffic(variant=None):
     with open(files[-1]) as f:
         d = json.load(f)
     if "by_variant" in d:
-        rec = d["by_variant"].get(str(variant))
+        rec = d["by_variant"].get(f"i8:{variant}" if int8 else str(variant))
         if rec is None:
             return None
+        alg = d["algorithmic_bytes_per_launch_i8" if int8 else "algorithmic_bytes_per_launch"]
         return {"hbm_bytes_per_launch": rec["hbm_bytes_per_launch"], "kernel": rec["kernel_name"][:80],
-                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
-                "source": os.path.relpath(files[-1], ROOT)}
+                "read_bytes_per_launch": rec.get("read_bytes_per_launch"),
+                "write_bytes_per_launch": rec.get("write_bytes_per_launch"),
+                "algorithmic_bytes_per_launch": alg, "source": os.path.relpath(files[-1], ROOT)}
+    if int8:
+        return None
     return {"hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
             "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
             "source": os.path.relpath(files[-1], ROOT)}
@@ -424,7 +433,7 @@ def main():
         t_min = SD15_I8_FLOP_PER_IMAGE / (PEAK_I8_TOPS * 1e12) + SD15_F16_FLOP_PER_IMAGE / (PEAK_F16_TFLOPS * 1e12)
         wq = "W8A8" if args.mode.startswith("w8a8") else args.mode.upper()
         line = {
-            "metric": f"images/sec SD1.5 {wq} {args.res}x{args.res} 50-step",
+            "metric": f"images/sec SD1.5 {wq} {args.res}x{args.res} 50-step" + (" int8-MFMA" if int8 else ""),
             "value": round(value, 4), "unit": "images/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "i8 (int32 accumulate) + f16" if int8 else "f16",
@@ -503,15 +512,21 @@ def cpu_baseline_sd35(threads, cfg, s, sc, steps):
     c = cfg.inner_dim
     x = torch.randn(256, c, generator=g).half()
     w = (torch.randn(4 * c, c, generator=g) * 0.02).half()
-    t0 = time.time()
-    F.linear(x, w)
-    t_lin = time.time() - t0
-    lin_rate = 2 * 256 * 4 * c * c / t_lin
     L = s + sc
     q = torch.randn(1, 2, L, cfg.attention_head_dim, generator=g).half()
-    t0 = time.time()
-    F.scaled_dot_product_attention(q, q, q)
-    t_att = time.time() - t0
+
+    def med3(fn):  # the SD1.5 baseline's protocol (oracle/cpu_baseline.py): 1 warm-up + median of 3
+        fn()
+        ts = []
+        for _ in range(3):
+            t0 = time.time()
+            fn()
+            ts.append(time.time() - t0)
+        return sorted(ts)[1]
+
+    t_lin = med3(lambda: F.linear(x, w))
+    lin_rate = 2 * 256 * 4 * c * c / t_lin
+    t_att = med3(lambda: F.scaled_dot_product_attention(q, q, q))
     att_rate = 4 * 2 * L * L * cfg.attention_head_dim / t_att
     att_gflop = cfg.num_layers * 4 * L * L * c / 1e9
     gemm_gflop = mmdit_gflop_per_sample(cfg, s, sc) - att_gflop
@@ -519,7 +534,7 @@ def cpu_baseline_sd35(threads, cfg, s, sc, steps):
     return {"value": round(1.0 / per_image, 10), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": (f"fp16 linear {c}->{4 * c} x256 tokens {t_lin:.2f}s ({lin_rate / 1e9:.2f} GFLOP/s), SDPA "
                        f"2 heads x {L}^2 d{cfg.attention_head_dim} {t_att:.2f}s ({att_rate / 1e9:.2f} GFLOP/s); "
-                       f"image = {steps} steps x CFG 2 x class FLOPs / class rates"),
+                       f"each 1 warm-up + median of 3; image = {steps} steps x CFG 2 x class FLOPs / class rates"),
             "seconds_per_image": round(per_image, 1)}
 
 

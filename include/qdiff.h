@@ -141,8 +141,10 @@ int qd_gn_geom_force(int stats_rows_per_thread, int apply_rows_per_thread);
 
 /* fp32 elements of split-K workspace the GEMM plans for this shape (0: runs unsplit).  Pass
  * at least that much as (ws, ws_elems) to qd_linear_fwd / qd_conv2d_fwd (conv: M = N*Ho*Wo,
- * K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo); with less (or NULL) the call runs unsplit. */
-long qd_gemm_workspace(int M, int N, int K, int wfmt, int rows_per_sample, int epi);
+ * K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo); with less (or NULL) the call runs unsplit.
+ * group: the int4 group size the qd_linear_fwd call passes (QD_WFMT_I4 with wscale_t; else 0),
+ * so the queried plan is the launch's plan. */
+long qd_gemm_workspace(int M, int N, int K, int wfmt, int group, int rows_per_sample, int epi);
 
 /* NHWC implicit-GEMM Conv2d: y[N, Ho, Wo, Co] = conv(x[N, H, W, Ci], W[Co][kh][kw][Ci_pad]).
  * WxAxConv2d.forward's F.conv2d (fake_quant.py:339); groups = dilation = 1.

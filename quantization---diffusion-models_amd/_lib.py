@@ -84,7 +84,7 @@ SIGNATURES = {
 
 # size queries (no status code)
 QUERIES = {
-    "qd_gemm_workspace": ([I, I, I, I, I, I], ctypes.c_long),
+    "qd_gemm_workspace": ([I, I, I, I, I, I, I], ctypes.c_long),
     "qd_groupnorm_workspace": ([I, I, I, I], I),
     "qd_gemm_i8_workspace": ([I, I, I, I, I], ctypes.c_long),
 }

@@ -19,25 +19,62 @@ from torch import nn
 from . import kernels as K
 
 
+# torch's CPU sum over the stacked calls (mean_of_dict -> torch.mean of fp16 = fp32 sum / count ->
+# fp16) accumulates rows in the multi-level cascade of aten/src/ATen/native/cpu/SumKernel.cpp
+# (multi_row_sum): 16 rows into level 0, then level j += level j-1 whenever the row count is a
+# multiple of 16^j, the levels added 0 += 1 += 2 += 3 at the end (level width 16 while the call
+# count is <= 2^16).  The hook keeps the same four fp32 accumulators on device, so mean() has the
+# reference's bits, not just its value to within fp32 rounding (tests/test_calib_mean.py).
+_LEVEL_BITS, _LEVELS, _MAX_CALLS = 4, 4, 1 << 16
+
+
 class MeanMaxActivationHook:
     def __init__(self, channels, device):
-        self.sum = torch.zeros(channels, dtype=torch.float32, device=device)
+        # acc[0] (= self.sum) receives each call's per-channel max; acc[1..3] the cascade levels
+        self.acc = [torch.zeros(channels, dtype=torch.float32, device=device) for _ in range(_LEVELS)]
         self.ws = torch.empty(channels, dtype=torch.float32, device=device)
         self.count = 0
         self.hook_handle = None
 
+    @property
+    def sum(self):
+        return self.acc[0]
+
     def __call__(self, x2d):
-        K.channel_absmax_accum(x2d, self.ws, self.sum)
+        K.channel_absmax_accum(x2d, self.ws, self.acc[0])
+        self._advance()
+
+    def record_max(self, amax):
+        """One call's per-channel max |x| (fp16 or fp32 values), accumulated like __call__."""
+        self.acc[0] += amax.to(torch.float32)
+        self._advance()
+
+    def _advance(self):
         self.count += 1
+        i = self.count
+        if i % (1 << _LEVEL_BITS):
+            return
+        for j in range(1, _LEVELS):  # a full 16-row chunk: carry level j-1 into level j
+            self.acc[j] += self.acc[j - 1]
+            self.acc[j - 1].zero_()
+            if i & (((1 << _LEVEL_BITS) - 1) << (j * _LEVEL_BITS)):
+                break
 
     def mean(self):
-        """mean over recorded calls, rounded to fp16 like torch.mean of a stacked fp16 list."""
+        """mean over recorded calls with the reference's bits: fp32 cascade sum / count -> fp16
+        (StableDiffusion1_x.py:104-112 mean_of_dict = torch.mean of the stacked fp16 maxima)."""
         if self.count == 0:
             raise RuntimeError("calibration hook recorded no calls")
-        return (self.sum / self.count).to(torch.float16)
+        if self.count > _MAX_CALLS:
+            raise NotImplementedError(f"{self.count} calls: torch's cascade widens its levels past 2^16 rows")
+        tot = self.acc[0].clone()
+        for j in range(1, _LEVELS):
+            tot += self.acc[j]
+        return (tot / self.count).to(torch.float16)
 
     def clear(self):
-        self.sum.zero_()
+        for a in self.acc:
+            a.zero_()
         self.count = 0
 
 

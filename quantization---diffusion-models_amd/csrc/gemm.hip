@@ -2593,10 +2593,12 @@ static int check_common(const GemmArgs& p, int fmt) {
   return 0;
 }
 
-extern "C" long qd_gemm_workspace(int M, int N, int K, int wfmt, int rows_per_sample, int epi) {
+extern "C" long qd_gemm_workspace(int M, int N, int K, int wfmt, int group, int rows_per_sample, int epi) {
+  // the launch's own plan: an int4 weight plans its LDS-DMA stages with its group (qd_linear_fwd
+  // with wscale_t), so the slab size queried here is the one that launch uses
   const Plan pl = plan_gemm(M, N, K, wfmt != QD_WFMT_F16, rows_per_sample, (epi & QD_EPI_AMAX) != 0,
                             (epi & QD_EPI_GEGLU) != 0, (epi & QD_EPI_AMAX_POST) != 0,
-                            wfmt == QD_WFMT_I4 ? 64 : 0);  // (group unknown here: size for every int4 variant)
+                            wfmt == QD_WFMT_I4 ? group : 0);
   return split_ws_elems(pl, M, N);
 }
 

@@ -56,8 +56,10 @@ def gather_latents(lat, dst=0):
         return lat
     world = dist.get_world_size()
     if dist.get_backend() == "nccl":
-        out = [torch.empty_like(lat) for _ in range(world)]
-        dist.all_gather(out, lat)
+        # a true gather (ProcessGroupNCCL::gather: each rank sends its shard to dst only), not an
+        # all_gather that would ship every shard to every rank
+        out = [torch.empty_like(lat) for _ in range(world)] if dist.get_rank() == dst else None
+        dist.gather(lat.contiguous(), out, dst)
         return torch.cat(out) if dist.get_rank() == dst else None
     src = lat.cpu() if lat.is_cuda else lat
     out = [torch.empty_like(src) for _ in range(world)] if dist.get_rank() == dst else None

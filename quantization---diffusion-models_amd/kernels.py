@@ -402,10 +402,10 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
         _force(c[1] if _OVERRIDE is None else _OVERRIDE)
         try:
             if scratch:
-                n = _lib.load().qd_gemm_workspace(M, N, K, WFMT[fmt], rows_per_sample, ep)
+                n = _lib.load().qd_gemm_workspace(M, N, K, WFMT[fmt], gr, rows_per_sample, ep)
                 ws, wsn = (torch.empty(n, dtype=torch.float32, device=x2d.device), n) if n > 0 else (None, 0)
             else:
-                ws, wsn = _gemm_ws(M, N, K, WFMT[fmt], rows_per_sample, ep, x2d.device)
+                ws, wsn = _gemm_ws(M, N, K, WFMT[fmt], rows_per_sample, ep, x2d.device, gr)
             sct = scales_t(sc) if fmt == "i4" else None
             _lib.call("qd_linear_fwd", _p(x2d), M, K, x2d.stride(0), _p(w), WFMT[fmt], _p(sc), _p(sct), gr,
                       _p(bias), _p(residual), _p(y), N, y.stride(0), ep, _p(am), rows_per_sample,
@@ -435,9 +435,9 @@ def geglu_interleave_rows(n2, device):
     return torch.stack([idx, idx + half], 1).reshape(-1)
 
 
-def _gemm_ws(M, N, K, wfmt, rows_per_sample, epi, device):
+def _gemm_ws(M, N, K, wfmt, rows_per_sample, epi, device, group=0):
     """Split-K slab workspace the kernel plans for this shape (None if it runs unsplit)."""
-    n = _lib.load().qd_gemm_workspace(M, N, K, wfmt, rows_per_sample, epi)
+    n = _lib.load().qd_gemm_workspace(M, N, K, wfmt, group, rows_per_sample, epi)
     if n <= 0:
         return None, 0
     return _empty((n,), torch.float32, device), n
@@ -466,7 +466,7 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
             if cip % 64:
                 ws, wsn = None, 0
             elif scratch:
-                m_ = _lib.load().qd_gemm_workspace(M, co, Kd, 0, ho * wo, ep)
+                m_ = _lib.load().qd_gemm_workspace(M, co, Kd, 0, 0, ho * wo, ep)
                 ws, wsn = (torch.empty(m_, dtype=torch.float32, device=x.device), m_) if m_ > 0 else (None, 0)
             else:
                 ws, wsn = _gemm_ws(M, co, Kd, 0, ho * wo, ep, x.device)

@@ -94,6 +94,9 @@ def pndm_tables(num_inference_steps, cfg: PNDMConfig = PNDMConfig()):
     return torch.from_numpy(ts), torch.stack(a_t).float(), torch.stack(a_p).float()
 
 
+_SPACING_DEFAULT = {"EulerDiscreteScheduler": "linspace"}
+
+
 def config_from_diffusers(d):
     """A scheduler config object from a diffusers scheduler_config.json dict (the local
     checkpoint's own scheduler, as DiffusionPipeline.from_pretrained would build it)."""
@@ -113,8 +116,11 @@ def config_from_diffusers(d):
     # the device step kernels implement "leading" spacing without sample clipping / dynamic
     # thresholding: a config asking for anything else would silently run another schedule than
     # DiffusionPipeline.from_pretrained builds from the same file
-    if d.get("timestep_spacing", "leading") != "leading":
-        raise NotImplementedError(f"{name} timestep_spacing {d['timestep_spacing']!r} (only 'leading')")
+    # (a missing key means the class's own default: diffusers' EulerDiscreteScheduler defaults to
+    # "linspace", DDIM and PNDM to "leading")
+    spacing = d.get("timestep_spacing", _SPACING_DEFAULT.get(name, "leading"))
+    if spacing != "leading":
+        raise NotImplementedError(f"{name} timestep_spacing {spacing!r} (only 'leading')")
     if d.get("thresholding", False):
         raise NotImplementedError(f"{name} thresholding=True (dynamic thresholding) has no device kernel")
     if name == "DDIMScheduler" and d.get("clip_sample", True):  # diffusers' DDIM default is True

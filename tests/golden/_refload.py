@@ -80,3 +80,22 @@ def load_reference():
     qz = _load("awq.quantize.quantizer", f"{REF}/quantize/quantizer.py")
     sq = _load("awq.quantize.quantizer_SQ", f"{REF}/quantize/quantizer_SQ.py")
     return types.SimpleNamespace(fake_quant=fq, quantizer=qz, quantizer_SQ=sq, calib_data=cd)
+
+
+def load_sd15_adapter():
+    """models/StableDiffusion1_x.py (its mean_of_dict uses no instance state).  Its imports are
+    torch / BaseAWQForDiffusion / QUANTISABLE_COMPONENTS from .base (the base module needs the
+    absent diffusers and AutoAWQ runtime: import-only stand-ins here) and diffusers'
+    BasicTransformerBlock (absent: an import-only stand-in)."""
+    import torch
+    load_reference()
+    base = sys.modules["awq.models.base"]
+    base.torch = torch
+    base.BaseAWQForDiffusion = type("BaseAWQForDiffusion", (), {})
+    base.QUANTISABLE_COMPONENTS = {}
+    d = sys.modules["diffusers"]
+    _stub("diffusers.models")
+    _stub("diffusers.models.attention", BasicTransformerBlock=_Unreachable)
+    d.models = sys.modules["diffusers.models"]
+    d.models.attention = sys.modules["diffusers.models.attention"]
+    return _load("awq.models.StableDiffusion1_x", f"{REF}/models/StableDiffusion1_x.py")

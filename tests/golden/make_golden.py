@@ -166,6 +166,19 @@ def gen_smooth(ref, out):
     hook(None, (t16(x),), None)
     out["hook_x"] = x
     out["hook_amax"] = hook.max_scales[0].numpy()
+    # the mean over calls (StableDiffusion1_x.py:104-112 mean_of_dict: torch.mean of the stacked
+    # per-call fp16 maxima) for 3, 24 and 600 calls (600 = the reference's calibration: 12 pipeline
+    # calls x 50 steps); magnitudes spread over ~2^14 so the fp32 sums round
+    sd15 = _refload.load_sd15_adapter()
+    for calls in (3, 24, 600):
+        hook = ref.calib_data.Mean_Max_Activation_Hook()
+        xs = []
+        for i in range(calls):
+            xi = (rng.standard_normal((1, 4, 320)) * np.exp(rng.standard_normal(320) * 2.5)).astype(F16)
+            hook(None, (t16(xi),), None)
+            xs.append(xi)
+        out[f"mean{calls}_x"] = np.stack(xs)
+        out[f"mean{calls}_mean"] = sd15.StableDiffusion1_x.mean_of_dict(None, hook.max_scales).numpy()
 
 
 class _Tiny(torch.nn.Module):

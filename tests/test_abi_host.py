@@ -259,10 +259,15 @@ def test_scheduler_configs_rejected_when_unsupported():
     for bad in ({"_class_name": "DDIMScheduler", **base},                      # diffusers default clip_sample=True
                 {"_class_name": "DDIMScheduler", "clip_sample": False, "timestep_spacing": "trailing", **base},
                 {"_class_name": "PNDMScheduler", "timestep_spacing": "linspace", **base},
+                # no timestep_spacing key: EulerDiscreteScheduler's diffusers default is "linspace"
+                {"_class_name": "EulerDiscreteScheduler", **base},
                 {"_class_name": "DDIMScheduler", "clip_sample": False, "thresholding": True, **base}):
         with pytest.raises(NotImplementedError):
             config_from_diffusers(bad)
-    for cfg in (DDIMConfig(), PNDMConfig()):  # what save_pretrained writes reloads
+    from qdiff.scheduler import EulerDiscreteConfig
+    assert isinstance(config_from_diffusers({"_class_name": "EulerDiscreteScheduler", "timestep_spacing": "leading",
+                                             **base}), EulerDiscreteConfig)
+    for cfg in (DDIMConfig(), PNDMConfig(), EulerDiscreteConfig()):  # what save_pretrained writes reloads
         assert type(config_from_diffusers(config_to_diffusers(cfg))) is type(cfg)
 
 

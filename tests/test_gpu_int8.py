@@ -103,6 +103,47 @@ def _geglu_amax(k, dev):
     assert torch.equal(amax.cpu(), y.float().abs().view(2, 256, -1).amax(1).reshape(-1).cpu())
 
 
+@pytest.mark.parametrize("variant", I8_FORCE + I8_SPLIT_FORCE)
+def test_linear_i8_post_residual_amax_and_fused_scale(variant, dev):
+    """the int8 proj_out scale fusion (unet.block_fwd: the last ff.net.2 GEMM reduces the
+    block output's per-(n, c) amax after its residual add, qd_linear_i8 post-residual amax) and
+    quant_samples_i8(x, amax_nc=...) (qd_quant_samples_i8_amax).  At the SD1.5 64x64 shape (two
+    samples of 4096 tokens, K 1280 -> N 320): the output equals the plain residual call bit for bit,
+    the amax equals the exact per-(sample, channel) max |output|, and the per-sample codes / scales
+    taken over that amax equal quant_samples_i8 of the output, for every tile variant (split-K ids
+    fall back to the unsplit plan this epilogue needs)."""
+    k = K()
+    rng = np.random.default_rng(31)
+    n, s, Kd, N = 2, 4096, 1280, 320
+    x = rng.standard_normal((n * s, Kd)).astype(np.float16)
+    w = (rng.standard_normal((N, Kd)) / Kd ** 0.5).astype(np.float16)
+    b = rng.standard_normal(N).astype(np.float16)
+    res = (rng.standard_normal((n * s, N)) * 3).astype(np.float16)
+    res[s:] *= 5  # the two samples get different scales
+    xq, sa = R.quant_rows_i8(x)
+    wq, sw = R.weight_rows_i8(w)
+    ref = R.linear_i8(xq, sa, wq, sw, b, res)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    amax = torch.empty(n * N, dtype=torch.float32, device=dev)
+    k.force_gemm(variant)
+    try:
+        y = k.linear_i8(t(xq), t(sa), t(wq), t(sw), bias=t(b), residual=t(res), amax=amax, rows_per_sample=s,
+                        amax_post=True)
+        plain = k.linear_i8(t(xq), t(sa), t(wq), t(sw), bias=t(b), residual=t(res))
+    finally:
+        k.force_gemm(None)
+    assert np.array_equal(_bits(y.cpu().numpy()), _bits(ref))
+    assert torch.equal(y, plain)
+    exact = np.abs(ref.astype(np.float32)).reshape(n, s, N).max(1).reshape(-1)
+    assert np.array_equal(amax.cpu().numpy(), exact)
+    y4 = y.view(n, 64, 64, N)
+    q0, s0 = k.quant_samples_i8(y4)
+    q1, s1 = k.quant_samples_i8(y4, amax_nc=amax)
+    qr, sr = R.quant_samples_i8(ref.reshape(n, 64, 64, N))
+    assert torch.equal(s0, s1) and torch.equal(q0, q1)
+    assert np.array_equal(s1.cpu().numpy(), sr) and np.array_equal(q1.cpu().numpy(), qr)
+
+
 @pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups", [(64, 64, 3, 1, 16, False), (64, 128, 3, 2, 16, False),
                                                         (128, 64, 1, 1, 8, False), (64, 64, 3, 1, 8, True),
                                                         (320, 320, 3, 1, 32, False), (640, 640, 3, 1, 16, False),

@@ -293,10 +293,10 @@ def test_gemm_plans_split_k_for_small_m():
     from qdiff import _lib
     lib = _lib.load()
     # SD1.5 8x8 level: M = 8 * 64, N = 1280, K = 9 * 1280 -> too few 128-row tiles, K is split
-    assert lib.qd_gemm_workspace(512, 1280, 11520, 0, 64, 4) > 0
-    assert lib.qd_gemm_workspace(128, 1280, 11520, 0, 64, 4) > 0
+    assert lib.qd_gemm_workspace(512, 1280, 11520, 0, 0, 64, 4) > 0
+    assert lib.qd_gemm_workspace(128, 1280, 11520, 0, 0, 64, 4) > 0
     # the big-M levels run unsplit
-    assert lib.qd_gemm_workspace(32768, 320, 2880, 0, 4096, 4) == 0
+    assert lib.qd_gemm_workspace(32768, 320, 2880, 0, 0, 4096, 4) == 0
 
 
 # ------------------------------------------------------------------ attention
@@ -318,6 +318,35 @@ def test_attention(b, heads, sq, skv, d, dev):
     ref = (p @ vh).transpose(1, 2).reshape(b, sq, c)
     # P is rounded to fp16 before P.V (flash-style); error ~ 1e-3 relative to |V|
     assert (o - ref).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("d,gain", [(40, 3.0), (80, 2.5), (64, 3.0), (160, 2.0)])
+def test_attention_sharp_softmax(d, gain, dev):
+    """large-norm Q / K (logits of magnitude 30-60, a near one-hot softmax).  The kernel
+    multiplies Q by scale * log2(e) and rounds it to fp16 before the QK^T MFMA, so each logit carries
+    an extra relative error <= 2^-11 of sum_i |q_i k_i| * scale; a softmax with logit errors <= e moves
+    its output by <= 2 e max|v| (to first order).  The bound below is that term + the 1e-2 of the
+    fp16 P rounding (test_attention), against an fp32 reference of the same fp16 inputs."""
+    k = K()
+    g = torch.Generator().manual_seed(d)
+    b, heads, sq, skv = 2, 4, 512, 640
+    c = heads * d
+    q = (torch.randn(b, sq, c, generator=g) * gain).half()
+    kk = (torch.randn(b, skv, c, generator=g) * gain).half()
+    v = torch.randn(b, skv, c, generator=g).half()
+    o = k.attention(q.to(dev), kk.to(dev), v.to(dev), heads).cpu().float()
+    qh = q.float().view(b, sq, heads, d).transpose(1, 2)
+    kh = kk.float().view(b, skv, heads, d).transpose(1, 2)
+    vh = v.float().view(b, skv, heads, d).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) / math.sqrt(d)
+    assert s.abs().max().item() > 25  # sharp
+    ref = (torch.softmax(s, -1) @ vh).transpose(1, 2).reshape(b, sq, c)
+    e_logit = 2.0 ** -11 * (qh.abs() @ kh.abs().transpose(-1, -2)).amax(-1) / math.sqrt(d)  # [b, h, sq]
+    bound = 1e-2 + 2 * e_logit * vh.abs().amax(dim=(-1, -2), keepdim=True)[..., 0]
+    err = (o - ref).abs().view(b, sq, heads, d).amax(-1).transpose(1, 2)  # [b, h, sq]
+    print(f"d={d}: max err {err.max().item():.3g}, max bound {bound.max().item():.3g}, "
+          f"max err/bound {(err / bound).max().item():.3f}")
+    assert (err <= bound).all()
 
 
 # ------------------------------------------------------------------ norms / elementwise
