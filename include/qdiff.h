@@ -112,6 +112,14 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
                                 half(half(y + bias) + residual) - the per-(sample, channel) input amax
                                 of the quantized conv that consumes it (fake_quant.py:125 reduction),
                                 so no separate column-max pass; never split-K or ping-pong tiles */
+#define QD_EPI_CADD 128      /* int8 conv (qd_conv2d_i8): out = half(out + cadd[n * cadd_ld + col]), one
+                                fp16 vector per (sample, column) after the residual - the diffusers
+                                ResnetBlock2D time-embedding add of conv1's output */
+#define QD_EPI_GNSTATS 256   /* int8 conv (qd_conv2d_i8): GroupNorm statistics of the FINAL output over
+                                64-row slots of each sample into gn_part[M / 64][N] float4 = (slot mean,
+                                sum of squared deviations from it, min, max), fp32 - the consuming
+                                GroupNorm (qd_groupnorm_part) needs no statistics pass over the
+                                tensor; rows_per_sample % 64 == 0, never ping-pong tiles */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
@@ -195,10 +203,14 @@ int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const vo
                  const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
                  int rows_per_sample, float* ws, long ws_elems, void* stream);
 /* NHWC implicit-GEMM conv on int8 codes: x_i8 [N, H, W, Ci_pad] (Ci_pad % 64 == 0), one scale
- * per sample sa[N]; w_i8 [Co][kh][kw][Ci_pad], sw[Co]; geometry / epilogue as qd_conv2d_fwd. */
+ * per sample sa[N]; w_i8 [Co][kh][kw][Ci_pad], sw[Co]; geometry / epilogue as qd_conv2d_fwd.
+ * QD_EPI_CADD: + cadd[n * cadd_ld + co] after the residual (cadd_ld <= 0: Co).  QD_EPI_GNSTATS:
+ * the consumer GroupNorm's slot statistics of the final output into gn_part [N*Ho*Wo / 64][Co]
+ * float4 (Ho*Wo % 64 == 0; for qd_groupnorm_part). */
 int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w, int ci, int ci_pad, const void* wt,
                  const float* sw, int co, int kh, int kw, int stride, int pad, int upsample2x, const void* bias,
-                 const void* residual, void* y, int epi, float* amax, float* ws, long ws_elems, void* stream);
+                 const void* residual, void* y, int epi, float* amax, const void* cadd, int cadd_ld,
+                 float* gn_part, float* ws, long ws_elems, void* stream);
 /* fp32 elements of split-K workspace qd_linear_i8 / qd_conv2d_i8 plan for this shape (K = codes
  * per row; conv: M = N*Ho*Wo, K = kh*kw*Ci_pad, rows_per_sample = Ho*Wo). */
 long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, int epi);
@@ -210,6 +222,13 @@ long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, int epi);
 int qd_groupnorm_i8(const void* x, const void* x2, int c1, const float* in_amax, int in_bits, const void* cadd,
                     int cadd_ld, int n, int hw, int c, int groups, float eps, const void* gamma, const void* beta,
                     int silu, int8_t* y8, float* scales, float* ws, void* stream);
+/* GroupNorm(+SiLU) of x [N, hw, C] (fp16 NHWC) from the slot statistics its producer wrote
+ * (qd_conv2d_i8 with QD_EPI_GNSTATS: part [N * hw / 64][C] float4, hw % 64 == 0): no statistics
+ * pass.  y8 + scales: int8 codes, one scale per sample (as qd_groupnorm_i8); else fp16 y.
+ * ws: qd_groupnorm_workspace(). */
+int qd_groupnorm_part(const float* part, const void* x, int n, int hw, int c, int groups, float eps,
+                      const void* gamma, const void* beta, int silu, void* y, int8_t* y8, float* scales, float* ws,
+                      void* stream);
 /* qd_layernorm with per-row int8 output (= qd_quant_rows_i8 of the fp16 LayerNorm output). */
 int qd_layernorm_i8(const void* x, int rows, int c, float eps, const void* gamma, const void* beta, int8_t* y8,
                     float* scales, void* stream);

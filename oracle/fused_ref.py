@@ -17,7 +17,7 @@ value of every output of that launch, composed from the reference's own operatio
 Each output comes with the tolerance the tests apply to it (``Out``): bit-exact for pure
 fake-quant / copy ops, 2 fp16 ulp + the fp32 summation-order bound for reductions, and one
 quantization step where a fake-quant follows a reduction (a rounding boundary the two summation
-orders straddle moves the code by one).
+orders straddle moves the code by one, the scale itself possibly one ulp apart: + 2 ulp).
 """
 import math
 from dataclasses import dataclass
@@ -64,7 +64,11 @@ def compare(got, o: Out):
     if o.ulp_of is not None:
         bound = bound + 2 * ulp(o.ulp_of)
     if o.step is not None:
-        bound = torch.maximum(bound, o.step * 1.0001 + u + atol)
+        # a flipped code (one step) in an element whose fake-quant SCALE also differs by one fp16
+        # ulp (the per-(n, c) amax is itself a maximum of values the two summation orders round
+        # differently): |q| ulp(s) <= |ref| 2^-10 <= 2 ulp(|ref|) on top of the step and the output
+        # rounding u (groupnorm_nhwc#36.h at 1.0099 x the one-step bound)
+        bound = torch.maximum(bound, o.step * 1.0001 + 3 * u + atol)
     beyond1 = (d > u * 1.0001 + atol).float().mean().item()
     bad = int((d > bound).sum()) + int((~nan_ok).sum())
     return (d / bound).max().item(), beyond1, bad

@@ -28,9 +28,11 @@ class Arena:
         self.zviews = None
         self.zpool = None
         self.zi = 0
+        self.stream = None
 
     def zeroed_f32(self, n, device):
         """A zero-filled fp32 buffer of n elements for this step -> (tensor, True)."""
+        self._check_stream(device)
         if self.zviews is not None:
             if self.zi >= len(self.zviews) or self.zviews[self.zi].numel() != n:
                 raise RuntimeError(f"arena: zeroed buffer #{self.zi} changed size; the step is not shape-static")
@@ -52,10 +54,24 @@ class Arena:
             self.zviews.append(self.zpool[off:off + n])
             off += (n + 63) // 64 * 64
 
+    def _check_stream(self, device):
+        """The plan is one stream's launch order: every buffer is handed out assuming the launches
+        that use it are ordered on that stream (the zero pool is cleared at the step start on it).
+        A launch on another stream would race with that order, so a second stream is refused."""
+        device = torch.device(device)
+        if device.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(device)
+        if self.stream is None:
+            self.stream = cur  # the step's stream (a graph capture runs on its own stream)
+        elif cur != self.stream:
+            raise RuntimeError("arena: buffers requested on a second stream; the step plan is single-stream")
+
     def begin_step(self):
         """Zero the pool (one launch, captured into the step's graph)."""
         self.i = 0
         self.zi = 0
+        self.stream = None
         if self.zpool is not None:
             from . import _lib
             _lib.call("qd_fill_zero", self.zpool.data_ptr(), self.zpool.numel(),
@@ -67,6 +83,7 @@ class Arena:
 
     def alloc(self, shape, dtype, device):
         shape = torch.Size(shape)
+        self._check_stream(device)
         if self.i < len(self.bufs):
             t = self.bufs[self.i]
             if t.shape != shape or t.dtype != dtype:

@@ -76,6 +76,12 @@ struct GemmArgs {
   // is added to the accumulator; the row's activation scale sa[m] multiplies the sum.
   const float* gs;
   int f8;
+  // GroupNorm-statistics epilogue (QD_EPI_GNSTATS) and the per-(sample, column) add (QD_EPI_CADD):
+  // the int8-MFMA mode's producing convs hand their consumer GroupNorm (norm.hip k_gn_coeff<1>) the
+  // moments of each 64-row slot of the final output, gnp[slot][col] = (mean, M2, min, max)
+  const f16* cadd;
+  int cadd_ld;
+  float* gnp;
 };
 
 constexpr int BK = 64;
@@ -358,6 +364,45 @@ __device__ __forceinline__ void i8_scale(const GemmArgs& p, const i32x4 (&acc)[T
   }
 }
 
+// 16-lane (one DPP row = the fr lanes of one fq group) reductions: xor 1, xor 2, half-row mirror,
+// row mirror - every lane ends with the same value (each step adds a commutative pair)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float row16_min(float v) {
+  v = fminf(v, dppf<0xB1>(v));
+  v = fminf(v, dppf<0x4E>(v));
+  v = fminf(v, dppf<0x141>(v));
+  return fminf(v, dppf<0x140>(v));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  return fmaxf(v, dppf<0x140>(v));
+}
+
+// GroupNorm slot moments of one column over 64 rows held as 4 values x 16 lanes (fragments
+// i = 4s .. 4s+3 of a wave, rows 16 i + fr): mean, then the sum of squared deviations from it (two
+// passes over registers: no cancellation), min, max.  All fp32, fixed order (deterministic).
+__device__ __forceinline__ float4 slot_moments(float v0, float v1, float v2, float v3) {
+  const float s = row16_sum(((v0 + v1) + v2) + v3);
+  const float mean = s * (1.0f / 64.0f);
+  const float d0 = v0 - mean, d1 = v1 - mean, d2 = v2 - mean, d3 = v3 - mean;
+  const float m2 = row16_sum(((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+  const float mn = row16_min(fminf(fminf(v0, v1), fminf(v2, v3)));
+  const float mx = row16_max(fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
+  return make_float4(mean, m2, mn, mx);
+}
+
 // ---- shared epilogue ----------------------------------------------------------------------
 // acc[i][j]: C^T fragment (rows n = n0 + wn0 + 16j + 4fq + r, column m = m0 + wm0 + 16i + fr).
 // LDS halves the epilogue needs: the [BM][BN + 8] fp16 C tile + the per-wave-row column-max
@@ -397,6 +442,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // post-residual amax: the residual is added to the fragments (8-B loads per lane) before the
     // column maxes, and the coalesced pass below stores the tile as it stands
     const bool post = has_res && do_amax && (p.epi & QD_EPI_AMAX_POST) && !geglu && !gtanh;
+    // GroupNorm slot statistics / per-(sample, column) add of the final output: the residual (and
+    // the add) go to the fragments like the post-residual amax (rows_per_sample % WM == 0, host)
+    const bool gn = (p.epi & QD_EPI_GNSTATS) && p.gnp && !geglu && !gtanh;
+    const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd && !geglu && !gtanh;
+    const bool fres = has_res && (post || gn || cadd);
     // amax: the WGM wave rows of the block combine their column maxes in LDS first when the
     // block's rows lie in one sample, so each (sample, column) address takes one atomic per
     // block instead of one per wave row (same-line atomic chains bound this epilogue)
@@ -406,17 +456,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool blk_amax = do_amax && !geglu && WGM > 1 && p.rows_per_sample % BM == 0;
     const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
     const __amdgpu_buffer_rsrc_t yrs = rsrc(p.y, ybytes);
-    const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res && !post ? p.res : p.y, has_res && !post ? ybytes : 0u);
+    const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res && !fres ? p.res : p.y, has_res && !fres ? ybytes : 0u);
     // the residual tile of the coalesced pass is loaded first, all NR chunks per thread in flight
     // while the fragments go to LDS (a 2-deep load / add / store loop left the epilogue waiting on
     // HBM latency NR / 2 times)
     constexpr int CPR16 = BN / 8, NR = (BM * CPR16 + NT - 1) / NT;
-    const bool pre_res = has_res && !post && !geglu;
+    const bool pre_res = has_res && !fres && !geglu;
     // post-residual amax: the residual in the fragments' layout (4 consecutive columns of one row
     // per lane and fragment), all TM x TN 8-B loads issued before any is used
     constexpr bool PF_POST = TM * TN <= 20;  // (register budget: the 4 x 5 fragment tiles and smaller)
     f16x4 rf[PF_POST ? TM : 1][PF_POST ? TN : 1];
-    if (PF_POST && post) {
+    if (PF_POST && fres) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn0 + j * 16 + fq * 4;
@@ -446,14 +496,18 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
         const bool col_ok = n < p.N;  // N % 8 == 0: a lane's 4 columns are all in or all out
         f16x4 bq = {};
         if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+        f16x4 cv = {};
+        if (cadd && col_ok)  // the wave's rows lie in one sample (host check)
+          cv = *reinterpret_cast<const f16x4*>(p.cadd + (long)(min(m0 + wm0, p.M - 1) / p.rows_per_sample) * p.cadd_ld + n);
         float cm[4] = {0.f, 0.f, 0.f, 0.f};
+        f16x4 hs[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int ml = wm0 + i * 16 + fr;
           f16x4 h;
 #pragma unroll
           for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[r]);
-          if (post) {
+          if (fres) {
             const bool ok = m0 + ml < p.M && col_ok;
             if (ok) {
               f16x4 rv;
@@ -463,6 +517,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
               for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rv[r]);
             }
           }
+          if (cadd) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)cv[r]);
+          }
+          hs[i] = h;
           if (do_amax) {  // (uniform) the column maxes only when an amax is reduced
             const bool ok = m0 + ml < p.M && col_ok;
 #pragma unroll
@@ -470,6 +529,25 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
               if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
           }
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
+        }
+        if constexpr (WM % 64 == 0) {
+          if (gn) {  // (uniform) 64-row slots: fragments 4s .. 4s+3 (rows per sample % 64 == 0: a slot
+                     // is all in or all past M)
+#pragma unroll
+            for (int s = 0; s < WM / 64; ++s) {
+              float4 mo[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                mo[r] = slot_moments((float)hs[4 * s][r], (float)hs[4 * s + 1][r], (float)hs[4 * s + 2][r],
+                                     (float)hs[4 * s + 3][r]);
+              const int srow = m0 + wm0 + 64 * s;
+              if (fr == 0 && col_ok && srow < p.M) {
+                float4* dst = reinterpret_cast<float4*>(p.gnp) + (long)(srow / 64) * p.N + n;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[r] = mo[r];
+              }
+            }
+          }
         }
         if (do_amax && !geglu) {
           // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
@@ -548,7 +626,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
               for (int r = 0; r < 8; ++r) v[r] = (f16)gelu_tanh_f((float)v[r]);
             }
           }
-          if (has_res && !post) {
+          if (has_res && !fres) {
             const f16x8 rq = bload(rrs, m0 + row < p.M ? off : OOB);
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
@@ -2069,6 +2147,110 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   }
 }
 
+// split-K reduction + epilogue with the GroupNorm slot statistics (QD_EPI_GNSTATS) and the
+// per-(sample, column) add (QD_EPI_CADD): block = one 64-row slot x 64 columns; thread (cq, rg)
+// owns 4 columns x rows 4 rg .. 4 rg + 3 (16 column quads x 16 row groups).  Slabs summed in split
+// order (int32 for the int8 path: exact); h = half(s + bias) [+ residual] [+ cadd]; the thread's
+// 4-row moments (two passes over registers) are merged over the 16 row groups in fixed order
+// (Chan: mean = sum of means / 16, M2 = sum M2 + 4 sum (mean_g - mean)^2).
+__global__ void __launch_bounds__(256) k_splitk_reduce_gn(GemmArgs p) {
+  __shared__ float4 red[16][64];  // [row group][column]
+  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int nl = cq * 4, n = blockIdx.x * 64 + nl;
+  const int mb = blockIdx.y * 64;
+  const bool col_ok = n < p.N;
+  const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
+  const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
+  const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd;
+  float v[4][4];  // [row][col]
+  if (col_ok) {
+    const long mn = (long)p.M * p.N;
+    f32x4 s[4];
+    long off[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      off[rr] = (long)(mb + rg * 4 + rr) * p.N + n;  // M % 64 == 0 (host check)
+      s[rr] = *reinterpret_cast<const f32x4*>(p.part + off[rr]);
+    }
+    if (p.i8) {
+      i32x4 si[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) si[rr] = __builtin_bit_cast(i32x4, s[rr]);
+      for (int k = 1; k < p.splits; ++k) {
+        i32x4 t[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) t[rr] = *reinterpret_cast<const i32x4*>(p.part + k * mn + off[rr]);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) si[rr] += t[rr];
+      }
+      const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = mb + rg * 4 + rr;
+        const float sa = p.sa[p.sa_rps ? m / p.sa_rps : m];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[rr][r] = ((float)si[rr][r] * sa) * sw[r];
+      }
+    } else {
+      for (int k = 1; k < p.splits; ++k) {
+        f32x4 t[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) t[rr] = *reinterpret_cast<const f32x4*>(p.part + k * mn + off[rr]);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) s[rr] += t[rr];
+      }
+    }
+    f16x4 bq = {}, cv = {};
+    if (has_bias) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+    if (cadd) cv = *reinterpret_cast<const f16x4*>(p.cadd + (long)(mb / p.rows_per_sample) * p.cadd_ld + n);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = mb + rg * 4 + rr;
+      f16x4 h;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[r] = (f16)(s[rr][r] + (float)bq[r]);
+      if (has_res) {
+        const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)m * p.ldy + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
+      }
+      if (cadd) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)cv[r]);
+      }
+      *reinterpret_cast<f16x4*>(p.y + (long)m * p.ldy + n) = h;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[rr][r] = (float)h[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // this thread's 4-row moments of column r
+      const float mean = (((v[0][r] + v[1][r]) + v[2][r]) + v[3][r]) * 0.25f;
+      const float d0 = v[0][r] - mean, d1 = v[1][r] - mean, d2 = v[2][r] - mean, d3 = v[3][r] - mean;
+      red[rg][nl + r] = make_float4(mean, ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3,
+                                    fminf(fminf(v[0][r], v[1][r]), fminf(v[2][r], v[3][r])),
+                                    fmaxf(fmaxf(v[0][r], v[1][r]), fmaxf(v[2][r], v[3][r])));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64 && blockIdx.x * 64 + (int)threadIdx.x < p.N) {
+    const int c = threadIdx.x;
+    float sm = 0.f, mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) sm += red[g][c].x;
+    const float mean = sm * (1.0f / 16.0f);
+    float m2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float4 e = red[g][c];
+      const float d = e.x - mean;
+      m2 += e.y + 4.0f * (d * d);
+      mn = fminf(mn, e.z);
+      mx = fmaxf(mx, e.w);
+    }
+    reinterpret_cast<float4*>(p.gnp)[(long)blockIdx.y * p.N + blockIdx.x * 64 + c] = make_float4(mean, m2, mn, mx);
+  }
+}
+
 // ---- tile / split selection (host) ----------------------------------------------------------
 // kind 0: register-staged k_gemm (any weight format); kind 1: LDS-DMA k_gemm_dma (F16 weights)
 struct Plan {
@@ -2747,7 +2929,11 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 // post: post-residual amax epilogue - the lock-step DMA tiles only (the ping-pong epilogue
 // reduces before its residual add; split-K slabs would run it in the reduce kernel)
-static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu, bool post = false) {
+// gn: GroupNorm-statistics / per-(sample, column) add epilogue - lock-step DMA tiles whose wave
+// rows are a multiple of the 64-row slot and lie in one sample, or the halo conv (64-row waves);
+// split-K plans reduce through k_splitk_reduce_gn
+static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu, bool post = false,
+                    bool gn = false) {
   if (g_force >= 140 && g_force <= 144 && !geglu && Kh % 288 == 0) {
     // int8 halo conv (applicability checked at launch): 140 BN 160 / 141 BN 128 (3-slot weight
     // ring), 142 / 143 / 144 BN 160 with 4 / 5 / 6 slots; K splits over whole 64-code chunks
@@ -2772,7 +2958,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
       return pl;
     }
   }
-  if (g_force >= 130 && g_force <= 134 && !post) {
+  if (g_force >= 130 && g_force <= 134 && !post && !gn) {
     // ping-pong: wave rows 128 (BN >= 192) or 64 must lie in one sample for the amax epilogue
     const int bnp = kPpBn[g_force - 130];
     if (!amax || rows_per_sample % (bnp >= 192 ? 128 : 64) == 0) {
@@ -2796,6 +2982,8 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   int var = N % 160 == 0 ? 10 : 11;
   if (g_force >= 110 && g_force <= 117) var = g_force - 100;
   if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
+  if (gn && (rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0 || (kDmaC[var].bm / kDmaC[var].wgm) % 64 != 0))
+    var = 11;
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];
   Plan pl{1, d.bm, d.bn, var, 1, Kh};
@@ -2817,14 +3005,17 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   return pl;
 }
 
+static bool epi_gn(int epi) { return (epi & (QD_EPI_GNSTATS | QD_EPI_CADD)) != 0; }
+
 template <int AMODE>
 static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
-  const bool post = (p.epi & QD_EPI_AMAX_POST) != 0;
-  Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post);
+  const bool post = (p.epi & QD_EPI_AMAX_POST) != 0, gn = epi_gn(p.epi);
+  Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post,
+                    gn);
   if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 32))) {  // int8 halo conv not applicable
     const int f = g_force;
     g_force = -1;
-    pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post);
+    pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post, gn);
     g_force = f;
   }
   if (pl.splits > 1 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N))) {
@@ -2850,7 +3041,8 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
     else if (pl.kind == 3) launch_pp_i8<AMODE, true>(p, pl.bn, st);
     else launch_i8<AMODE, true>(p, pl.var, st);
     const int gx = (p.N + 255) / 256;
-    if ((long)gx * ((p.M + 15) / 16) >= 512) k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
+    if (gn) k_splitk_reduce_gn<<<dim3((p.N + 63) / 64, p.M / 64), 256, 0, st>>>(p);
+    else if ((long)gx * ((p.M + 15) / 16) >= 512) k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
     else k_splitk_reduce<1><<<dim3(gx, (p.M + 3) / 4), 256, 0, st>>>(p);
   }
 }
@@ -2875,12 +3067,23 @@ static int check_i8(const GemmArgs& p) {
   QD_REQUIRE(!p.bias || (reinterpret_cast<uintptr_t>(p.bias) & 7) == 0, "bias must be 8-B aligned");
   QD_REQUIRE(!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0, "residual must be 16-B aligned");
   QD_REQUIRE((double)p.N * p.K * 2 < 2147483648.0, "weight exceeds the 2 GiB buffer-addressing range");
+  if (epi_gn(p.epi)) {
+    QD_REQUIRE(!(p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU | QD_EPI_GELU_TANH)),
+               "GroupNorm-statistics / per-sample add epilogue: no amax / GEGLU / GELU-tanh");
+    QD_REQUIRE(p.rows_per_sample > 0 && p.rows_per_sample % 64 == 0 && p.M % 64 == 0 && p.ldy == p.N,
+               "GroupNorm-statistics / per-sample add epilogue: rows per sample % 64 == 0, dense output");
+    QD_REQUIRE(!(p.epi & QD_EPI_GNSTATS) || (p.gnp && (reinterpret_cast<uintptr_t>(p.gnp) & 15) == 0),
+               "gn_part must be a 16-B aligned buffer of M / 64 x N float4");
+    QD_REQUIRE(!(p.epi & QD_EPI_CADD) || (p.cadd && p.cadd_ld >= p.N && p.cadd_ld % 4 == 0 &&
+                                          (reinterpret_cast<uintptr_t>(p.cadd) & 7) == 0),
+               "cadd must be an 8-B aligned [n][cadd_ld >= N] fp16 array, cadd_ld % 4 == 0");
+  }
   return 0;
 }
 
 extern "C" long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, int epi) {
   const Plan pl = plan_i8(M, N, K / 2, rows_per_sample, (epi & QD_EPI_AMAX) != 0, (epi & QD_EPI_GEGLU) != 0,
-                          (epi & QD_EPI_AMAX_POST) != 0);
+                          (epi & QD_EPI_AMAX_POST) != 0, epi_gn(epi));
   return split_ws_elems(pl, M, N);
 }
 
@@ -2925,8 +3128,8 @@ extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int ld
 
 extern "C" int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w, int ci, int ci_pad, const void* wt,
                             const float* sw, int co, int kh, int kw, int stride, int pad, int upsample2x,
-                            const void* bias, const void* residual, void* y, int epi, float* amax, float* ws,
-                            long ws_elems, void* stream) {
+                            const void* bias, const void* residual, void* y, int epi, float* amax,
+                            const void* cadd, int cadd_ld, float* gn_part, float* ws, long ws_elems, void* stream) {
   QD_REQUIRE(ci_pad % 64 == 0 && ci_pad >= ci, "int8 conv needs ci_pad % 64 == 0");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(wt) & 15) == 0,
              "x and w must be 16-B aligned");
@@ -2961,6 +3164,9 @@ extern "C" int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w,
   p.sa_rps = Ho * Wo;  // one activation scale per sample
   p.sw = sw;
   p.i8 = 1;
+  p.cadd = (const f16*)cadd;
+  p.cadd_ld = cadd_ld > 0 ? cadd_ld : co;
+  p.gnp = gn_part;
   int rc = check_i8(p);
   if (rc) return rc;
   QD_REQUIRE(stride >= 1 && pad >= 0 && Ho > 0 && Wo > 0, "bad conv geometry");

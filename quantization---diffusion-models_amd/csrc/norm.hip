@@ -269,11 +269,15 @@ __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg
 constexpr float SILU_NEG_BOUND = 0.2786f;
 
 // One block per (n, group): group mean / rstd from the partials (fixed thread -> partial map,
-// fixed reduction tree: deterministic), then per channel the affine coefficients and - when the
+// fixed reduction tree: deterministic).  MODE 0: k_gn_stats' per-channel shifted sums; MODE 1: the
+// 64-row slot moments (mean, M2, min, max) a producing int8 conv's epilogue wrote (gemm.hip
+// QD_EPI_GNSTATS), merged in two passes (Chan: mean = sum of slot means / P, M2 = sum M2 +
+// 64 sum (slot mean - mean)^2, P = Z slots x cg channels).  Then per channel the affine coefficients and - when the
 // output is fake-quantized - its exact amax from the channel's min / max input:
 // out = half([silu](half(x * a + b))) is monotone in x on each side of silu's minimum, so
 // max |out| is |out(x_min)| or |out(x_max)| except when SiLU is on and both extremes map below
 // the bound above; the block then scans those (rare) channels' rows itself.
+template <int MODE>
 __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, GnIn in, int hw, int c, int cg,
                                                   int Z, float eps, const f16* __restrict__ gamma,
                                                   const f16* __restrict__ beta, int silu, int quant,
@@ -315,16 +319,41 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     red[1][t >> 6] = s2;
   }
   __syncthreads();
-  if (t == 0) {
-    const float S1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    const float S2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-    const float cnt = (float)cg * (float)hw;
-    const float m = S1 / cnt;                        // mean of the shifted values
-    const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
-    stat[0] = m + gn_load1(in, c, ni, (long)ni * hw, g0);
-    stat[1] = 1.0f / sqrtf(var + eps);
+  if constexpr (MODE == 0) {
+    if (t == 0) {
+      const float S1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+      const float S2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+      const float cnt = (float)cg * (float)hw;
+      const float m = S1 / cnt;                        // mean of the shifted values
+      const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
+      stat[0] = m + gn_load1(in, c, ni, (long)ni * hw, g0);
+      stat[1] = 1.0f / sqrtf(var + eps);
+    }
+    __syncthreads();
+  } else {
+    // slot moments: s1 summed the slot means (s2 is unused); second pass over the same partials for
+    // the deviations of the slot means from the group mean
+    const float P = (float)Z * (float)cg;
+    const float gmean = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) / P;
+    float q = 0.f;
+    for (int e = t; e < Z * cg; e += 256) {
+      const int z = e / cg, j = e - z * cg;
+      const float4 v = part[((long)ni * Z + z) * c + g0 + j];
+      const float d = v.x - gmean;
+      q += v.y + 64.0f * (d * d);
+    }
+    q = wave_sum(q);
+    __syncthreads();  // (every thread read red[0] above)
+    if ((t & 63) == 0) red[1][t >> 6] = q;
+    __syncthreads();
+    if (t == 0) {
+      const float M2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+      const float var = fmaxf(M2 / (P * 64.0f), 0.f);
+      stat[0] = gmean;
+      stat[1] = 1.0f / sqrtf(var + eps);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int j = t; j < cg; j += 256) {
     const int ch = g0 + j;
     const long i = (long)ni * c + ch;
@@ -674,8 +703,8 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
   // (the coefficient stage recomputes its shift / fallback elements from the raw sources; the
   // apply pass reads the materialised x)
-  k_gn_coeff<<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta, silu,
-                                         qmax > 0 || y8, coef, amax, amax_n);
+  k_gn_coeff<0><<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta,
+                                            silu, qmax > 0 || y8, coef, amax, amax_n);
   const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
   if (fin) {
     const GnIn inx{in.xout, nullptr, c, nullptr, 0, nullptr, 0, nullptr, nullptr};
@@ -764,6 +793,44 @@ extern "C" int qd_groupnorm_fin(const void* y_raw, const float* in_amax, int in_
   GnIn in{(const f16*)y_raw, nullptr, c, in_amax, in_bits ? (1 << (in_bits - 1)) - 1 : 0, (const f16*)cadd, cadd_ld,
           (const f16*)residual, (f16*)x_out};
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
+}
+
+// GroupNorm(+SiLU) whose statistics a producing int8 conv already reduced in its epilogue
+// (gemm.hip QD_EPI_GNSTATS: part[n * hw / 64 + slot][c] = 64-row slot moments of x): the
+// coefficient kernel merges the slots (k_gn_coeff<1>), the apply pass streams x once - two
+// launches and one read of x instead of three launches and two reads.  y8: int8 codes with one
+// scale per sample (the int8-MFMA mode's conv input, = qd_quant_samples_i8 of the fp16 output);
+// else the fp16 output y (no output fake-quant: the test / diagnostic form).
+extern "C" int qd_groupnorm_part(const float* part, const void* x, int n, int hw, int c, int groups, float eps,
+                                 const void* gamma, const void* beta, int silu, void* y, int8_t* y8, float* scales,
+                                 float* ws, void* stream) {
+  QD_REQUIRE(part && x && gamma && beta && ws && (y || (y8 && scales)), "null pointer");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(part) & 15) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0,
+             "partials / workspace must be 16-B aligned");
+  QD_REQUIRE(!y8 || (reinterpret_cast<uintptr_t>(y8) & 7) == 0, "y8 must be 8-B aligned");
+  QD_REQUIRE(hw % 64 == 0 && hw > 0, "slot statistics need hw % 64 == 0");
+  QD_REQUIRE(groups > 0 && c % groups == 0 && c % 8 == 0 && c / groups <= 1024, "bad channel grouping");
+  if (n == 0) return 0;
+  hipStream_t st = S(stream);
+  const int cg = c / groups;
+  const GnGeom g = gn_geom(n, hw, c);
+  float2* coef = reinterpret_cast<float2*>(ws);
+  float* amax = reinterpret_cast<float*>(coef + (long)n * c);
+  float* amax_n = y8 ? amax + (long)n * c : nullptr;
+  const GnIn in{(const f16*)x, nullptr, c, nullptr, 0, nullptr, 0, nullptr, nullptr};
+  k_gn_coeff<1><<<n * groups, 256, 0, st>>>(reinterpret_cast<const float4*>(part), in, hw, c, cg, hw / 64, eps,
+                                            (const f16*)gamma, (const f16*)beta, silu, y8 != nullptr, coef, amax,
+                                            amax_n);
+  const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
+  if (y8) {  // (the qmax argument carries the group count of amax_n[n][group])
+    if (silu) k_gn_apply<0, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, scales);
+    else k_gn_apply<0, 0, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, scales);
+  } else {
+    if (silu) k_gn_apply<0, 1, false><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, 0, amax, (f16*)y);
+    else k_gn_apply<0, 0, false><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, 0, amax, (f16*)y);
+  }
+  QD_CHECK_LAUNCH();
+  return 0;
 }
 
 // ---------------------------------------------------------------------------------------

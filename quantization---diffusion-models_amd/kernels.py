@@ -23,6 +23,8 @@ EPI_AMAX_ZEROED = 16
 EPI_GEGLU = 8
 EPI_GELU_TANH = 32
 EPI_AMAX_POST = 64
+EPI_CADD = 128
+EPI_GNSTATS = 256
 GRAN_ZEROED = 0x100
 
 
@@ -671,9 +673,12 @@ def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, row
 
 
 def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, residual=None, out=None, amax=None,
-              amax_zeroed=False):
+              amax_zeroed=False, chan_add=None, gn_stats=False):
     """NHWC implicit-GEMM conv on int8 codes: xq [N, H, W, Cip] int8 (Cip % 64 == 0), sa [N]
-    fp32 (one scale per sample), wq [Co, kh, kw, Cip] int8, sw [Co] fp32."""
+    fp32 (one scale per sample), wq [Co, kh, kw, Cip] int8, sw [Co] fp32.
+    chan_add: [N, Co] fp16 (row stride may exceed Co) added after the residual (the resnet's time
+    embedding).  gn_stats: also return the consumer GroupNorm's 64-row slot statistics of the
+    output, (y, part [N*Ho*Wo / 64, Co, 4] fp32) for groupnorm_part_i8 (Ho*Wo % 64 == 0)."""
     if xq.dtype != torch.int8 or wq.dtype != torch.int8 or not xq.is_cuda or not xq.is_contiguous():
         raise ValueError("int8 conv operands must be contiguous int8 HIP tensors")
     n, h, w, cip = xq.shape
@@ -685,15 +690,21 @@ def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, 
     if out is None:
         out = _empty((n, ho, wo, co), torch.float16, xq.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
-          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0)
+          (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
+          (EPI_CADD if chan_add is not None else 0) | (EPI_GNSTATS if gn_stats else 0)
     M, Kd = n * ho * wo, kh * kw * cip
+    ld = _cadd_ld(chan_add, n, co, "chan_add")
+    if gn_stats and (ho * wo) % 64:
+        raise ValueError("GroupNorm slot statistics need Ho * Wo % 64 == 0")
+    part = _empty((M // 64, co, 4), torch.float32, xq.device) if gn_stats else None
 
-    def launch(c, y, am, ep, scratch):
+    def launch(c, y, am, ep, scratch, gp):
         _force(c if _OVERRIDE is None else _OVERRIDE)
         try:
             ws, wsn = _i8_ws(M, co, Kd, ho * wo, ep, xq.device, scratch)
             _lib.call("qd_conv2d_i8", _p(xq), _p(sa), n, h, w, ci, cip, _p(wq), _p(sw), co, kh, kw, stride, pad,
-                      1 if upsample2x else 0, _p(bias), _p(residual), _p(y), ep, _p(am), _p(ws), wsn, _stream())
+                      1 if upsample2x else 0, _p(bias), _p(residual), _p(y), ep, _p(am), _p(chan_add), ld, _p(gp),
+                      _p(ws), wsn, _stream())
         finally:
             _force(-1)
 
@@ -702,14 +713,49 @@ def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, 
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
+        tp = torch.empty_like(part) if part is not None else None
         halo = (kh, kw, stride, pad) == (3, 3, 1, 1)
-        cands = list(I8_VARIANTS) + (list(I8_HALO_VARIANTS) if halo else []) + \
-            _i8_split_cands(M, co, Kd, halo)
-        c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+        # (the GroupNorm-statistics epilogue has no ping-pong form)
+        cands = list(I8_VARIANTS) + (list(I8_HALO_VARIANTS) if halo else []) + _i8_split_cands(M, co, Kd, halo)
+        if gn_stats or chan_add is not None:
+            cands = [v for v in cands if not 130 <= v % 1000 <= 134]
+        c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True, tp))
     else:
         c = _TUNE.get(key)
-    launch(c if c is not None else -1, out, amax, epi, False)
-    return out
+    launch(c if c is not None else -1, out, amax, epi, False, part)
+    return (out, part) if gn_stats else out
+
+
+def groupnorm_part_i8(x, part, groups, eps, gamma, beta, silu=False):
+    """GroupNorm(+SiLU) of x [N, H, W, C] from the slot statistics its producing conv reduced
+    (conv2d_i8(..., gn_stats=True)), written as int8 codes with one scale per sample:
+    (codes [N, H, W, C] int8, scales [N] fp32) - groupnorm_nhwc_i8's result without its
+    statistics pass."""
+    _chk(x, "x")
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    if part.dtype != torch.float32 or part.numel() != n * hw // 64 * c * 4:
+        raise ValueError("part must be the producer's [N*HW/64, C, 4] fp32 slot statistics")
+    y8 = _empty(x.shape, torch.int8, x.device)
+    sa = _empty((n,), torch.float32, x.device)
+    ws = _empty((_lib.load().qd_groupnorm_workspace(n, hw, c, groups),), torch.float32, x.device)
+    _lib.call("qd_groupnorm_part", _p(part), _p(x), n, hw, c, groups, float(eps), _p(gamma), _p(beta),
+              1 if silu else 0, None, _p(y8), _p(sa), _p(ws), _stream())
+    return y8, sa
+
+
+def groupnorm_part(x, part, groups, eps, gamma, beta, silu=False):
+    """The fp16 form of groupnorm_part_i8 (tests / diagnostics)."""
+    _chk(x, "x")
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    if part.dtype != torch.float32 or part.numel() != n * hw // 64 * c * 4:
+        raise ValueError("part must be the producer's [N*HW/64, C, 4] fp32 slot statistics")
+    y = _empty(x.shape, torch.float16, x.device)
+    ws = _empty((_lib.load().qd_groupnorm_workspace(n, hw, c, groups),), torch.float32, x.device)
+    _lib.call("qd_groupnorm_part", _p(part), _p(x), n, hw, c, groups, float(eps), _p(gamma), _p(beta),
+              1 if silu else 0, _p(y), None, None, _p(ws), _stream())
+    return y
 
 
 def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):

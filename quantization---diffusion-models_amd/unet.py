@@ -357,23 +357,28 @@ class UNet2DConditionModel(nn.Module):
         skips = [h]
         # block outputs travel as Pending (conv2 / proj_out output quant + residual deferred) so a
         # following GroupNorm materialises them in its statistics pass; other consumers _get()
+        # gn_out (int8-MFMA mode): the block output's next consumer is a single-source GroupNorm
+        # (the resnet's norm1 or the transformer's norm), so the producing conv reduces its statistics
         for blk in self.down_blocks:
+            nres = len(blk.resnets)
             for i, res in enumerate(blk.resnets):
-                h = resnet_fwd(res, h, temb_silu, tp=tps.get(id(res)), pend=True)
+                h = resnet_fwd(res, h, temb_silu, tp=tps.get(id(res)), pend=True, gn_out=True)
                 if blk.attentions is not None:
-                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True)
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True,
+                                        gn_out=i + 1 < nres or blk.downsamplers is None)
                 skips.append(h)
             if blk.downsamplers is not None:
-                h = run_conv(blk.downsamplers[0].conv, _get(h))
+                h = run_conv(blk.downsamplers[0].conv, _get(h), gn=True)
                 skips.append(h)
         mb = self.mid_block
-        h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])), pend=True)
-        h = transformer_fwd(mb.attentions[0], h, ctx_kv, pend=True)
+        h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])), pend=True, gn_out=True)
+        h = transformer_fwd(mb.attentions[0], h, ctx_kv, pend=True, gn_out=True)
         h = resnet_fwd(mb.resnets[1], h, temb_silu, tp=tps.get(id(mb.resnets[1])), pend=True)
         for blk in self.up_blocks:
             for i, res in enumerate(blk.resnets):
                 skip = skips.pop()
-                h = resnet_fwd(res, h, temb_silu, skip=skip, tp=tps.get(id(res)), pend=True)
+                h = resnet_fwd(res, h, temb_silu, skip=skip, tp=tps.get(id(res)), pend=True,
+                               gn_out=blk.attentions is not None)
                 if blk.attentions is not None:
                     h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True)
             if blk.upsamplers is not None:
@@ -401,8 +406,34 @@ class Pending:
         return self.x
 
 
+class GnReady:
+    """An int8-mode conv output x whose consuming GroupNorm's 64-row slot statistics the conv's
+    epilogue already reduced (kernels.conv2d_i8(..., gn_stats=True)): the GroupNorm runs from
+    `part` (kernels.groupnorm_part_i8: no statistics pass over x); any other consumer takes x."""
+    __slots__ = ("x", "part")
+
+    def __init__(self, x, part):
+        self.x, self.part = x, part
+
+
 def _get(h):
-    return h.get() if isinstance(h, Pending) else h
+    if isinstance(h, Pending):
+        return h.get()
+    return h.x if isinstance(h, GnReady) else h
+
+
+def _gn_i8(norm, x, silu):
+    """GroupNorm(+SiLU) -> per-sample int8 codes of a conv input in the int8-MFMA mode: from the
+    producer's slot statistics when it reduced them, else with the statistics pass."""
+    if isinstance(x, GnReady):
+        return K.groupnorm_part_i8(x.x, x.part, norm.num_groups, norm.eps, _f16(norm.weight), _f16(norm.bias),
+                                   silu=silu)
+    return K.groupnorm_nhwc_i8(x, norm.num_groups, norm.eps, _f16(norm.weight), _f16(norm.bias), silu=silu)
+
+
+# int8-MFMA mode: the GroupNorm statistics of conv outputs are reduced in the producing conv's
+# epilogue (GroupNorm = coefficient + apply launches); QD_NO_GN_PART=1: the statistics pass instead
+GN_PART = not os.environ.get("QD_NO_GN_PART")
 
 
 # the GroupNorm-consumer finalize runs on the streaming (> 256 pixels) GroupNorm; smaller levels
@@ -453,21 +484,23 @@ def _conv_weight(layer, co_pad=None):
 
 
 def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=False, c_valid=0, co_pad=None,
-             defer=False, in_amax=None, pend=False):
+             defer=False, in_amax=None, pend=False, gn=False):
     """NHWC conv of an nn.Conv2d or WxAxConv2d with the reference's act fake-quant semantics:
     q_x = act_quant(x) -> y = conv(q_x) + b -> q_y = act_quant(y) -> [+ residual | + temb].
     in_amax: x's per-(n, c) amax, already reduced by its producer (the GEMM epilogue).
     defer=True (no residual): return (y_raw, (amax, bits, chan_add)) instead of finalizing, for
     a consumer that applies the output quant + add on the fly (groupnorm_nhwc fq_in); the spec
-    is None when y is already final.  pend (with residual): return a Pending block output."""
+    is None when y is already final.  pend (with residual): return a Pending block output.
+    gn (int8-MFMA mode): the output feeds a GroupNorm - return a GnReady (final output incl. the
+    residual / chan_add, and its slot statistics) when the conv runs on int8 codes."""
     if isinstance(layer, WxAxConv2d):
         layer._check_supported()
         i8 = layer.i8_operand()
         if isinstance(x, tuple):  # (int8 codes, per-sample scales) from a fused producer
-            return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer)
+            return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer, gn=gn)
         if i8 is not None and co_pad in (None, layer.out_channels) and x.shape[-1] == layer.ci_pad:
             return _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer,
-                                in_amax if x.shape[-1] == layer.in_channels else None)
+                                in_amax if x.shape[-1] == layer.in_channels else None, gn=gn)
     wk, bias = _conv_weight(layer, co_pad)
     stride, pad = layer.stride[0], layer.padding[0]
     ci = layer.weight.shape[1]
@@ -514,13 +547,22 @@ def lin_i8(layer):
         getattr(layer, "_qd_hook", None) is None
 
 
-def _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer, in_amax=None):
+def _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer, in_amax=None, gn=False):
     """int8-MFMA mode conv: per-sample int8 codes of the fp16 NHWC input (or the producer's fused
     (codes, scales)), int8 implicit GEMM with the output (+ bias, + residual) in fp16; the
     time-embedding add is deferred to the consumer like the fake-quant path's (no output
     fake-quant in this mode).  in_amax: x's per-(n, c) amax from its producer's epilogue (the
-    per-sample scale is taken over it instead of a separate reduction pass)."""
+    per-sample scale is taken over it instead of a separate reduction pass).  gn: the output
+    feeds a GroupNorm - the epilogue adds chan_add itself and reduces the GroupNorm's slot
+    statistics (returns a GnReady)."""
     xq, sa = x if isinstance(x, tuple) else K.quant_samples_i8(x, amax_nc=in_amax)
+    hh = xq.shape[1] * (2 if upsample else 1)
+    ww = xq.shape[2] * (2 if upsample else 1)
+    k, s, p = layer.kernel_size[0], layer.stride[0], layer.padding[0]
+    if gn and GN_PART and (((hh + 2 * p - k) // s + 1) * ((ww + 2 * p - k) // s + 1)) % 64 == 0:
+        y, part = K.conv2d_i8(xq, sa, i8[0], i8[1], layer.in_channels, s, p, upsample, bias=layer.bias,
+                              residual=residual, chan_add=chan_add, gn_stats=True)
+        return GnReady(y, part)
     y = K.conv2d_i8(xq, sa, i8[0], i8[1], layer.in_channels, layer.stride[0], layer.padding[0], upsample,
                     bias=layer.bias, residual=residual)
     if chan_add is None:
@@ -642,13 +684,14 @@ def _geglu_operand_i8(layer, i8):
     return op
 
 
-def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False):
+def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False, gn_out=False):
     """diffusers ResnetBlock2D.forward (time_embedding_norm='default', output_scale_factor=1).
     tp: this block's time_emb_proj(silu(temb)) when precomputed by temb_projections().
     The up-block skip concat is never materialised in fp16: norm1 reads both sources and a
     quantized conv_shortcut receives the per-(n, c) fake-quant of the concat directly.
     x may be a Pending block output: norm1 then materialises it (K.groupnorm_fin).  pend: return
-    this block's output as a Pending (its conv2 output quant + residual add deferred)."""
+    this block's output as a Pending (its conv2 output quant + residual add deferred).  gn_out
+    (int8-MFMA mode): the output feeds a GroupNorm (conv2 reduces its statistics: GnReady)."""
     qs = conv_qbits(res.conv_shortcut) if res.conv_shortcut is not None else 0
     q1 = conv_qbits(res.conv1)
     if skip is None and not conv_i8(res.conv1) and _gn_fin_ok(x):
@@ -659,6 +702,7 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False):
             tp = run_linear(res.time_emb_proj, temb_silu)
         sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
         return _resnet_tail(res, h, temb_silu, tp, sc, pend)
+    xr = x
     x, skip = _get(x), _get(skip)
     if skip is not None and qs > 0:
         sc = run_conv(res.conv_shortcut, K.act_quant_cat_nhwc(x, skip, qs), prequant=True)
@@ -667,25 +711,29 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False):
         return _resnet_tail(res, h, temb_silu, tp, sc, pend)
     xin = K.concat_c(x, skip) if skip is not None else x
     if conv_i8(res.conv1):  # int8-MFMA mode: GroupNorm + SiLU emits conv1's int8 codes
-        h = K.groupnorm_nhwc_i8(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight),
-                                _f16(res.norm1.bias), silu=True)
+        h = _gn_i8(res.norm1, xr if skip is None and isinstance(xr, GnReady) else xin, True)
     else:
         h = K.groupnorm_nhwc(xin, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
                              silu=True, q_bits=max(q1, 0))
     if tp is None:
         tp = run_linear(res.time_emb_proj, temb_silu)
     sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
-    return _resnet_tail(res, h, temb_silu, tp, sc, pend)
+    return _resnet_tail(res, h, temb_silu, tp, sc, pend, gn_out)
 
 
-def _resnet_tail(res, h, temb_silu, tp, sc, pend=False):
+def _resnet_tail(res, h, temb_silu, tp, sc, pend=False, gn_out=False):
     """conv1 (+ temb) -> norm2 + SiLU -> conv2 + shortcut, h = silu(norm1(x)) [quantized]."""
     q1 = conv_qbits(res.conv1)
     if tp is None:
         tp = run_linear(res.time_emb_proj, temb_silu)
-    # conv1's output quant + temb add are applied inside norm2 (never materialised)
-    h, spec = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp, defer=True)
+    # conv1's output quant + temb add are applied inside norm2 (never materialised); in the int8
+    # mode conv1's epilogue adds temb and reduces norm2's statistics instead (GnReady)
+    r = run_conv(res.conv1, h, prequant=q1 > 0, chan_add=tp, defer=True, gn=conv_i8(res.conv2))
     q2 = conv_qbits(res.conv2)
+    if isinstance(r, GnReady):
+        h = _gn_i8(res.norm2, r, True)
+        return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc, pend=pend, gn=gn_out)
+    h, spec = r
     if conv_i8(res.conv2):
         h = K.groupnorm_nhwc_i8(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                                 silu=True, fq_in=spec)
@@ -698,14 +746,16 @@ def _resnet_tail(res, h, temb_silu, tp, sc, pend=False):
     else:
         h = K.groupnorm_nhwc(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                              silu=True, q_bits=max(q2, 0), fq_in=spec)
-    return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc, pend=pend)
+    return run_conv(res.conv2, h, prequant=q2 > 0, residual=sc, pend=pend, gn=gn_out)
 
 
-def transformer_fwd(tm, x, ctx_kv, pend=False):
+def transformer_fwd(tm, x, ctx_kv, pend=False, gn_out=False):
     """diffusers Transformer2DModel (continuous input) + BasicTransformerBlock(s).  x may be a
-    Pending block output (the GroupNorm materialises it); pend: return the output as a Pending."""
+    Pending block output (the GroupNorm materialises it); pend: return the output as a Pending.
+    gn_out (int8-MFMA mode): the output feeds a GroupNorm (proj_out reduces its statistics)."""
     t_fq = None  # pending output fake-quant of t (amax, bits, chan_add)
     fin = not tm.linear_proj and not conv_i8(tm.proj_in) and _gn_fin_ok(x)
+    xr = x
     if not fin:
         x = _get(x)
     n, hh, ww, c = (x.y if fin else x).shape
@@ -721,7 +771,7 @@ def transformer_fwd(tm, x, ctx_kv, pend=False):
         h = K.groupnorm_nhwc(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
         t = run_linear(tm.proj_in, h.view(-1, c))
     elif conv_i8(tm.proj_in):
-        h = K.groupnorm_nhwc_i8(x, tm.norm.num_groups, tm.norm.eps, _f16(tm.norm.weight), _f16(tm.norm.bias))
+        h = _gn_i8(tm.norm, xr if isinstance(xr, GnReady) else x, False)
         t = run_conv(tm.proj_in, h).view(-1, c)
     else:
         q = conv_qbits(tm.proj_in)
@@ -744,7 +794,7 @@ def transformer_fwd(tm, x, ctx_kv, pend=False):
             t, in_amax = t
     if tm.linear_proj:
         return run_linear(tm.proj_out, t, residual=x.view(-1, c)).view(n, hh, ww, c)
-    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x, in_amax=in_amax, pend=pend)
+    return run_conv(tm.proj_out, t.view(n, hh, ww, c), residual=x, in_amax=in_amax, pend=pend, gn=gn_out)
 
 
 def _qkv_operand(attn):

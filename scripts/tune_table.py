@@ -114,6 +114,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="sd15,sdxl,sd35")
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--add", action="store_true",
+                    help="keep the committed table, tune only the shapes it lacks (new epilogue keys)")
     ap.add_argument("--retune-i4", action="store_true",
                     help="keep the committed table, re-tune only the linears whose operands include packed int4")
     a = ap.parse_args()
@@ -126,6 +128,11 @@ def main():
         for codes_only in (False, True):  # both W4 operand policies (their keys differ)
             K.W4_CODES_ONLY = codes_only
             run_w4(dev)
+    elif a.add:
+        n0 = K.load_table(OUT)
+        log(f"committed table ({n0} shapes)")
+        for name in a.models.split(","):
+            {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
     else:
         for name in a.models.split(","):
             {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)

@@ -5,6 +5,7 @@ activation codes are additionally pinned to the reference's own per-token fake-q
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from oracle import int8_ref as R
 
@@ -175,6 +176,112 @@ def test_conv2d_i8_bit_exact(cin, cout, ksz, stride, hw, ups, variant, dev):
         k.force_gemm(None)
     got = y.permute(0, 3, 1, 2).cpu().numpy()
     assert np.array_equal(_bits(got), _bits(ref)), np.abs(got.astype(np.float32) - ref.astype(np.float32)).max()
+
+
+# ------------------------------------------------------------------ GroupNorm statistics in the producing conv
+def _slot_stats64(y):
+    """float64 (mean, M2, min, max) of each 64-row slot x column of y [M, C] (fp16 values)."""
+    v = y.astype(np.float64).reshape(-1, 64, y.shape[-1])
+    mean = v.mean(1)
+    return mean, ((v - mean[:, None, :]) ** 2).sum(1), v.min(1), v.max(1)
+
+
+# (cin, cout, k, stride, hw, ups, residual, chan_add): resnet conv1 (+ temb) / conv2 (+ shortcut) at
+# every SD1.5 level, proj_out (1x1 + residual), the downsampler (3x3 s2), the 16x16 / 8x8 split-K
+# shapes (k_splitk_reduce_gn)
+GN_CASES = [(320, 320, 3, 1, 64, False, False, True), (320, 320, 3, 1, 64, False, True, False),
+            (640, 640, 3, 1, 32, False, True, True), (1280, 1280, 3, 1, 16, False, False, True),
+            (1280, 1280, 3, 1, 8, False, True, False), (320, 320, 1, 1, 64, False, True, False),
+            (640, 640, 3, 2, 32, False, False, False), (640, 320, 3, 1, 32, True, True, False)]
+GN_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 140, 141, 142, 3110, 4111, 2142, 6111]
+
+
+@pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups,res,cadd", GN_CASES)
+@pytest.mark.parametrize("variant", GN_FORCE)
+def test_conv2d_i8_groupnorm_statistics_epilogue(cin, cout, ksz, stride, hw, ups, res, cadd, variant, dev):
+    """qd_conv2d_i8 with QD_EPI_CADD / QD_EPI_GNSTATS: the output is bit-identical to the int8
+    oracle's conv (+ residual) followed by the fp16 time-embedding add, whatever the tile / split
+    (the ping-pong ids fall back to lock-step tiles, 115's 32-row waves to 111); the slot statistics
+    match float64 moments of that output (min / max exact, mean and M2 to fp32 summation error)."""
+    k = K()
+    rng = np.random.default_rng(cin + cout * 3 + hw + ksz + stride)
+    n = 2
+    x = rng.standard_normal((n, cin, hw, hw)).astype(np.float16)
+    x[1] *= 3
+    w = (rng.standard_normal((cout, cin, ksz, ksz)) / (cin * ksz * ksz) ** 0.5).astype(np.float16)
+    b = (rng.standard_normal(cout) + 2.0).astype(np.float16)  # offset means: the centred M2 matters
+    xq, sa = R.quant_samples_i8(x)
+    wk = w.transpose(0, 2, 3, 1).reshape(cout, -1)
+    wkq, sw = R.weight_rows_i8(wk)
+    wq = wkq.reshape(cout, ksz, ksz, cin).transpose(0, 3, 1, 2)
+    pad = ksz // 2
+    xin = xq.repeat(2, axis=2).repeat(2, axis=3) if ups else xq
+    H = hw * (2 if ups else 1)
+    ho = (H + 2 * pad - ksz) // stride + 1
+    rsd = rng.standard_normal((n, cout, ho, ho)).astype(np.float16) * 2 if res else None
+    ca = rng.standard_normal((n, 3 * cout)).astype(np.float16) if cadd else None  # a strided [n, Co] view
+    ref = R.conv2d_i8(xin, sa, wq, sw, b, stride, pad, residual=rsd)
+    if cadd:
+        ref = (ref.astype(np.float32) + ca[:, cout:2 * cout, None, None].astype(np.float32)).astype(np.float16)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    xh = t(xq.transpose(0, 2, 3, 1))
+    rh = t(rsd.transpose(0, 2, 3, 1)) if res else None
+    ch = t(ca)[:, cout:2 * cout] if cadd else None
+    k.force_gemm(variant)
+    try:
+        y, part = k.conv2d_i8(xh, t(sa), t(wkq.reshape(cout, ksz, ksz, cin)), t(sw), cin, stride, pad, ups,
+                              bias=t(b), residual=rh, chan_add=ch, gn_stats=True)
+    finally:
+        k.force_gemm(None)
+    got = y.permute(0, 3, 1, 2).cpu().numpy()
+    assert np.array_equal(_bits(got), _bits(ref)), np.abs(got.astype(np.float32) - ref.astype(np.float32)).max()
+    yr = got.transpose(0, 2, 3, 1).reshape(-1, cout)
+    mean, m2, mn, mx = _slot_stats64(yr)
+    p = part.cpu().numpy().astype(np.float64)
+    amax = np.abs(yr.astype(np.float64)).reshape(-1, 64, cout).max(1)
+    assert np.array_equal(p[..., 2], mn) and np.array_equal(p[..., 3], mx)
+    assert np.all(np.abs(p[..., 0] - mean) <= 2 ** -17 * amax + 1e-30)
+    assert np.all(np.abs(p[..., 1] - m2) <= 1e-5 * m2 + 64 * 2 ** -22 * amax ** 2)
+
+
+@pytest.mark.parametrize("c,hw,silu", [(320, 4096, True), (640, 1024, False), (1280, 256, True), (1280, 64, True),
+                                       (960, 1024, True)])
+def test_groupnorm_from_slot_statistics(c, hw, silu, dev):
+    """qd_groupnorm_part: the GroupNorm(+SiLU) from a producing conv's slot statistics against torch
+    (fp32 reference, 2 fp16 ulps as the statistics-pass GroupNorm), its int8 output equal to the
+    per-sample codes of its fp16 output bit for bit, and within one code of the statistics-pass
+    GroupNorm's int8 output (the fp32 summation orders differ)."""
+    k = K()
+    g = torch.Generator().manual_seed(c + hw)
+    n = 2
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half()
+    bet = (0.1 * torch.randn(c, generator=g)).half()
+    gam[::37] = 0.01   # SiLU outputs below the extremes bound: the coefficient kernel's fallback scan
+    bet[::37] = -0.5
+    # producer: a 1x1 int8 conv with residual, its epilogue reducing the slot statistics
+    x = (torch.randn(n, hw, c, generator=g) * 2).half()
+    xq, sa = R.quant_samples_i8(x.numpy())
+    w = (torch.randn(c, c, generator=g) / c ** 0.5).half().numpy()
+    wq, sw = R.weight_rows_i8(w)
+    rsd = (torch.randn(n, hw, c, generator=g) * 3 + 1.5).half()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    side = int(hw ** 0.5)
+    y, part = k.conv2d_i8(t(xq.reshape(n, side, side, c)), t(sa), t(wq.reshape(c, 1, 1, c)), t(sw), c, 1, 0,
+                          residual=rsd.view(n, side, side, c).to(dev), gn_stats=True)
+    yc = y.cpu().float().reshape(n, hw, c).transpose(1, 2).reshape(n, c, hw, 1)
+    ref = F.group_norm(yc, 32, gam.float(), bet.float(), 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    h16 = k.groupnorm_part(y, part, 32, 1e-5, gam.to(dev), bet.to(dev), silu=silu)
+    got = h16.cpu().float().reshape(n, hw, c).transpose(1, 2).reshape(n, c, hw, 1)
+    ok = (got - ref).abs() <= 2 * torch.pow(2.0, torch.floor(torch.log2(ref.abs().clamp(min=6.1e-5))) - 10) + 2e-3
+    assert ok.all(), (got - ref).abs().max()
+    q8, s8 = k.groupnorm_part_i8(y, part, 32, 1e-5, gam.to(dev), bet.to(dev), silu=silu)
+    qr, sr = k.quant_samples_i8(h16)
+    assert torch.equal(s8, sr) and torch.equal(q8, qr)
+    q0, s0 = k.groupnorm_nhwc_i8(y, 32, 1e-5, gam.to(dev), bet.to(dev), silu=silu)
+    assert (q0.int() - q8.int()).abs().max().item() <= 1
+    assert ((s0 - s8).abs() <= 2e-3 * s0).all()
 
 
 # ------------------------------------------------------------------ model level
