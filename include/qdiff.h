@@ -204,7 +204,7 @@ int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const vo
                  int rows_per_sample, float* ws, long ws_elems, void* stream);
 /* NHWC implicit-GEMM conv on int8 codes: x_i8 [N, H, W, Ci_pad] (Ci_pad % 64 == 0), one scale
  * per sample sa[N]; w_i8 [Co][kh][kw][Ci_pad], sw[Co]; geometry / epilogue as qd_conv2d_fwd.
- * QD_EPI_CADD: + cadd[n * cadd_ld + co] after the residual (cadd_ld <= 0: Co).  QD_EPI_GNSTATS:
+ * QD_EPI_CADD: + cadd[n * cadd_ld + co] after the residual (cadd_ld <= 0: Co; 16-B aligned rows).  QD_EPI_GNSTATS:
  * the consumer GroupNorm's slot statistics of the final output into gn_part [N*Ho*Wo / 64][Co]
  * float4 (Ho*Wo % 64 == 0; for qd_groupnorm_part). */
 int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w, int ci, int ci_pad, const void* wt,

@@ -364,45 +364,6 @@ __device__ __forceinline__ void i8_scale(const GemmArgs& p, const i32x4 (&acc)[T
   }
 }
 
-// 16-lane (one DPP row = the fr lanes of one fq group) reductions: xor 1, xor 2, half-row mirror,
-// row mirror - every lane ends with the same value (each step adds a commutative pair)
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dppf<0xB1>(v);
-  v += dppf<0x4E>(v);
-  v += dppf<0x141>(v);
-  v += dppf<0x140>(v);
-  return v;
-}
-__device__ __forceinline__ float row16_min(float v) {
-  v = fminf(v, dppf<0xB1>(v));
-  v = fminf(v, dppf<0x4E>(v));
-  v = fminf(v, dppf<0x141>(v));
-  return fminf(v, dppf<0x140>(v));
-}
-__device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));
-  v = fmaxf(v, dppf<0x4E>(v));
-  v = fmaxf(v, dppf<0x141>(v));
-  return fmaxf(v, dppf<0x140>(v));
-}
-
-// GroupNorm slot moments of one column over 64 rows held as 4 values x 16 lanes (fragments
-// i = 4s .. 4s+3 of a wave, rows 16 i + fr): mean, then the sum of squared deviations from it (two
-// passes over registers: no cancellation), min, max.  All fp32, fixed order (deterministic).
-__device__ __forceinline__ float4 slot_moments(float v0, float v1, float v2, float v3) {
-  const float s = row16_sum(((v0 + v1) + v2) + v3);
-  const float mean = s * (1.0f / 64.0f);
-  const float d0 = v0 - mean, d1 = v1 - mean, d2 = v2 - mean, d3 = v3 - mean;
-  const float m2 = row16_sum(((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
-  const float mn = row16_min(fminf(fminf(v0, v1), fminf(v2, v3)));
-  const float mx = row16_max(fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
-  return make_float4(mean, m2, mn, mx);
-}
-
 // ---- shared epilogue ----------------------------------------------------------------------
 // acc[i][j]: C^T fragment (rows n = n0 + wn0 + 16j + 4fq + r, column m = m0 + wm0 + 16i + fr).
 // LDS halves the epilogue needs: the [BM][BN + 8] fp16 C tile + the per-wave-row column-max
@@ -442,11 +403,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // post-residual amax: the residual is added to the fragments (8-B loads per lane) before the
     // column maxes, and the coalesced pass below stores the tile as it stands
     const bool post = has_res && do_amax && (p.epi & QD_EPI_AMAX_POST) && !geglu && !gtanh;
-    // GroupNorm slot statistics / per-(sample, column) add of the final output: the residual (and
-    // the add) go to the fragments like the post-residual amax (rows_per_sample % WM == 0, host)
+    // GroupNorm slot statistics / per-(sample, column) add of the final output: the coalesced pass
+    // adds the residual and cadd (the tile lies in one sample: rows_per_sample % BM == 0, host),
+    // writes the final tile back to LDS, and the slot moments are reduced from there
     const bool gn = (p.epi & QD_EPI_GNSTATS) && p.gnp && !geglu && !gtanh;
     const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd && !geglu && !gtanh;
-    const bool fres = has_res && (post || gn || cadd);
+    const bool fres = post;
     // amax: the WGM wave rows of the block combine their column maxes in LDS first when the
     // block's rows lie in one sample, so each (sample, column) address takes one atomic per
     // block instead of one per wave row (same-line atomic chains bound this epilogue)
@@ -496,11 +458,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
         const bool col_ok = n < p.N;  // N % 8 == 0: a lane's 4 columns are all in or all out
         f16x4 bq = {};
         if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
-        f16x4 cv = {};
-        if (cadd && col_ok)  // the wave's rows lie in one sample (host check)
-          cv = *reinterpret_cast<const f16x4*>(p.cadd + (long)(min(m0 + wm0, p.M - 1) / p.rows_per_sample) * p.cadd_ld + n);
         float cm[4] = {0.f, 0.f, 0.f, 0.f};
-        f16x4 hs[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int ml = wm0 + i * 16 + fr;
@@ -517,11 +475,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
               for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rv[r]);
             }
           }
-          if (cadd) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)cv[r]);
-          }
-          hs[i] = h;
           if (do_amax) {  // (uniform) the column maxes only when an amax is reduced
             const bool ok = m0 + ml < p.M && col_ok;
 #pragma unroll
@@ -529,25 +482,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
               if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
           }
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
-        }
-        if constexpr (WM % 64 == 0) {
-          if (gn) {  // (uniform) 64-row slots: fragments 4s .. 4s+3 (rows per sample % 64 == 0: a slot
-                     // is all in or all past M)
-#pragma unroll
-            for (int s = 0; s < WM / 64; ++s) {
-              float4 mo[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                mo[r] = slot_moments((float)hs[4 * s][r], (float)hs[4 * s + 1][r], (float)hs[4 * s + 2][r],
-                                     (float)hs[4 * s + 3][r]);
-              const int srow = m0 + wm0 + 64 * s;
-              if (fr == 0 && col_ok && srow < p.M) {
-                float4* dst = reinterpret_cast<float4*>(p.gnp) + (long)(srow / 64) * p.N + n;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) dst[r] = mo[r];
-              }
-            }
-          }
         }
         if (do_amax && !geglu) {
           // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
@@ -582,6 +516,57 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // division); stores / residual loads are 32-bit-offset buffer ops (rows past M fall off the
     // end of the buffer range and are dropped / read 0).
     static_assert(BN % 32 == 0 || BN % 16 == 0, "tile width");
+    // the tile's sample for the per-(sample, column) add (rows_per_sample % BM == 0)
+    const f16* const cadd_row = cadd ? p.cadd + (long)(min(m0, p.M - 1) / p.rows_per_sample) * p.cadd_ld : nullptr;
+    // GroupNorm slot statistics from the final tile in LDS: thread -> (64-row slot, 8-channel
+    // chunk, row phase k of G): rows k, k + G, ... of the slot, shifted by the slot's first row
+    // (no cancellation), then the G phases summed by lane shuffles (G consecutive lanes)
+    auto gn_slots = [&]() {
+      constexpr int SL = BM / 64, NPAIR = SL * CPR16;
+      constexpr int G0 = NT / NPAIR >= 64 ? 64 : NT / NPAIR >= 32 ? 32 : NT / NPAIR >= 16 ? 16 :
+                         NT / NPAIR >= 8 ? 8 : NT / NPAIR >= 4 ? 4 : NT / NPAIR >= 2 ? 2 : 1;
+      static_assert(BM % 64 == 0 && NPAIR * G0 <= NT, "slot geometry");
+      const int t = threadIdx.x;
+      if (t >= NPAIR * G0) return;
+      const int pr = t / G0, k = t - pr * G0;
+      const int s = pr / CPR16, c = pr - s * CPR16;
+      const int row0 = s * 64, n = n0 + c * 8;
+      const f16x8 sh = *reinterpret_cast<const f16x8*>(ct + row0 * LP + c * 8);
+      float s1[8], s2[8], mn[8], mx[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] = s2[j] = 0.f;
+        mn[j] = INFINITY;
+        mx[j] = -INFINITY;
+      }
+#pragma unroll 4
+      for (int rr = k; rr < 64; rr += G0) {
+        const f16x8 v = *reinterpret_cast<const f16x8*>(ct + (row0 + rr) * LP + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = (float)v[j], a = x - (float)sh[j];
+          s1[j] += a;
+          s2[j] += a * a;
+          mn[j] = fminf(mn[j], x);
+          mx[j] = fmaxf(mx[j], x);
+        }
+      }
+#pragma unroll
+      for (int o = G0 / 2; o > 0; o >>= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s1[j] += __shfl_xor(s1[j], o, 64);
+          s2[j] += __shfl_xor(s2[j], o, 64);
+          mn[j] = fminf(mn[j], __shfl_xor(mn[j], o, 64));
+          mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], o, 64));
+        }
+      if (k == 0 && n < p.N && m0 + row0 < p.M) {
+        float4* dst = reinterpret_cast<float4*>(p.gnp) + (long)((m0 + row0) / 64) * p.N + n;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          dst[j] = make_float4((float)sh[j] + s1[j] * (1.0f / 64.0f), s2[j] - s1[j] * s1[j] * (1.0f / 64.0f), mn[j], mx[j]);
+      }
+    };
     if (pre_res) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -593,8 +578,18 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i][r]);
+          if (cadd) {
+            const f16x8 cv = *reinterpret_cast<const f16x8*>(cadd_row + n);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)cv[r]);
+          }
+          if (gn) *reinterpret_cast<f16x8*>(ct + row * LP + c * 8) = v;  // (this thread's own element)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
         }
+      }
+      if (gn) {
+        __syncthreads();
+        gn_slots();
       }
       return;
     }
@@ -631,12 +626,24 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
           }
+          if constexpr (!GG) {
+            if (cadd) {
+              const f16x8 cv = *reinterpret_cast<const f16x8*>(cadd_row + n);
+#pragma unroll
+              for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)cv[r]);
+              if (gn) *reinterpret_cast<f16x8*>(ct + row * LP + c * 8) = v;  // (this thread's own element)
+            }
+          }
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
         }
       }
     };
     if (geglu) pass2(std::integral_constant<int, BN / 16>{}, std::true_type{});
     else pass2(std::integral_constant<int, BN / 8>{}, std::false_type{});
+    if (gn) {
+      __syncthreads();
+      gn_slots();
+    }
   }
 }
 
@@ -2929,9 +2936,9 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 // post: post-residual amax epilogue - the lock-step DMA tiles only (the ping-pong epilogue
 // reduces before its residual add; split-K slabs would run it in the reduce kernel)
-// gn: GroupNorm-statistics / per-(sample, column) add epilogue - lock-step DMA tiles whose wave
-// rows are a multiple of the 64-row slot and lie in one sample, or the halo conv (64-row waves);
-// split-K plans reduce through k_splitk_reduce_gn
+// gn: GroupNorm-statistics / per-(sample, column) add epilogue - lock-step DMA tiles that lie in
+// one sample (rows_per_sample % BM == 0), or the halo conv; split-K plans reduce through
+// k_splitk_reduce_gn (64-row blocks)
 static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu, bool post = false,
                     bool gn = false) {
   if (g_force >= 140 && g_force <= 144 && !geglu && Kh % 288 == 0) {
@@ -2982,8 +2989,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   int var = N % 160 == 0 ? 10 : 11;
   if (g_force >= 110 && g_force <= 117) var = g_force - 100;
   if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
-  if (gn && (rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0 || (kDmaC[var].bm / kDmaC[var].wgm) % 64 != 0))
-    var = 11;
+  if (gn && rows_per_sample % kDmaC[var].bm != 0) var = rows_per_sample % 128 == 0 ? 11 : 15;  // tile in one sample
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];
   Plan pl{1, d.bm, d.bn, var, 1, Kh};
@@ -3074,9 +3080,9 @@ static int check_i8(const GemmArgs& p) {
                "GroupNorm-statistics / per-sample add epilogue: rows per sample % 64 == 0, dense output");
     QD_REQUIRE(!(p.epi & QD_EPI_GNSTATS) || (p.gnp && (reinterpret_cast<uintptr_t>(p.gnp) & 15) == 0),
                "gn_part must be a 16-B aligned buffer of M / 64 x N float4");
-    QD_REQUIRE(!(p.epi & QD_EPI_CADD) || (p.cadd && p.cadd_ld >= p.N && p.cadd_ld % 4 == 0 &&
-                                          (reinterpret_cast<uintptr_t>(p.cadd) & 7) == 0),
-               "cadd must be an 8-B aligned [n][cadd_ld >= N] fp16 array, cadd_ld % 4 == 0");
+    QD_REQUIRE(!(p.epi & QD_EPI_CADD) || (p.cadd && p.cadd_ld >= p.N && p.cadd_ld % 8 == 0 &&
+                                          (reinterpret_cast<uintptr_t>(p.cadd) & 15) == 0),
+               "cadd must be a 16-B aligned [n][cadd_ld >= N] fp16 array, cadd_ld % 8 == 0");
   }
   return 0;
 }

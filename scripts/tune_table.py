@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--add", action="store_true",
                     help="keep the committed table, tune only the shapes it lacks (new epilogue keys)")
+    ap.add_argument("--drop-epi", type=int, default=0,
+                    help="with --add: first drop the entries whose epilogue flags intersect this mask")
     ap.add_argument("--retune-i4", action="store_true",
                     help="keep the committed table, re-tune only the linears whose operands include packed int4")
     a = ap.parse_args()
@@ -130,6 +132,10 @@ def main():
             run_w4(dev)
     elif a.add:
         n0 = K.load_table(OUT)
+        if a.drop_epi:
+            for key in [k for k in K.gemm_choices() if k[0] in ("conv_i8", "linear_i8") and
+                        (k[11] if k[0] == "conv_i8" else k[5]) & a.drop_epi]:
+                del K._TUNE[key]
         log(f"committed table ({n0} shapes)")
         for name in a.models.split(","):
             {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
