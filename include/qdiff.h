@@ -224,11 +224,19 @@ int qd_groupnorm_i8(const void* x, const void* x2, int c1, const float* in_amax,
                     int silu, int8_t* y8, float* scales, float* ws, void* stream);
 /* GroupNorm(+SiLU) of x [N, hw, C] (fp16 NHWC) from the slot statistics its producer wrote
  * (qd_conv2d_i8 with QD_EPI_GNSTATS: part [N * hw / 64][C] float4, hw % 64 == 0): no statistics
- * pass.  y8 + scales: int8 codes, one scale per sample (as qd_groupnorm_i8); else fp16 y.
+ * pass.  x2 (optional): the input is the channel concat x [.., c1] | x2 [.., c - c1] (the UNet
+ * skip concat, never materialised), part2 the second source's slot statistics.  y8 + scales:
+ * int8 codes, one scale per sample (as qd_groupnorm_i8); else fp16 y.  xamax (int8 output only,
+ * optional): the per-(n, c) max |input| [N][C] (for qd_quant_samples_i8_cat).
  * ws: qd_groupnorm_workspace(). */
-int qd_groupnorm_part(const float* part, const void* x, int n, int hw, int c, int groups, float eps,
-                      const void* gamma, const void* beta, int silu, void* y, int8_t* y8, float* scales, float* ws,
-                      void* stream);
+int qd_groupnorm_part(const float* part, const void* x, const float* part2, const void* x2, int c1, int n, int hw,
+                      int c, int groups, float eps, const void* gamma, const void* beta, int silu, void* y,
+                      int8_t* y8, float* scales, float* xamax, float* ws, void* stream);
+/* Per-sample int8 codes (qd_quant_samples_i8 semantics) of the channel concat x [N, rows, c1] |
+ * x2 [N, rows, c - c1] written to y [N, rows, c], the sample scale from the per-(n, c) maxima
+ * amax_nc [N][C] (e.g. qd_groupnorm_part's xamax): no concat copy, no amax pass. */
+int qd_quant_samples_i8_cat(const void* x, const void* x2, int c1, int c, int n, long rows, const float* amax_nc,
+                            int8_t* y, float* scales, void* stream);
 /* qd_layernorm with per-row int8 output (= qd_quant_rows_i8 of the fp16 LayerNorm output). */
 int qd_layernorm_i8(const void* x, int rows, int c, float eps, const void* gamma, const void* beta, int8_t* y8,
                     float* scales, void* stream);

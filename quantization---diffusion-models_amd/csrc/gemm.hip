@@ -403,12 +403,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // post-residual amax: the residual is added to the fragments (8-B loads per lane) before the
     // column maxes, and the coalesced pass below stores the tile as it stands
     const bool post = has_res && do_amax && (p.epi & QD_EPI_AMAX_POST) && !geglu && !gtanh;
-    // GroupNorm slot statistics / per-(sample, column) add of the final output: the coalesced pass
-    // adds the residual and cadd (the tile lies in one sample: rows_per_sample % BM == 0, host),
-    // writes the final tile back to LDS, and the slot moments are reduced from there
+    // GroupNorm slot statistics / per-(sample, column) add of the final output: cadd is added to
+    // the fragments (the tile lies in one sample: rows_per_sample % BM == 0, host; a residual then
+    // goes there first), the coalesced pass adds the residual and writes the final tile back to
+    // LDS, and the slot moments are reduced from there
     const bool gn = (p.epi & QD_EPI_GNSTATS) && p.gnp && !geglu && !gtanh;
     const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd && !geglu && !gtanh;
-    const bool fres = post;
+    const bool fres = post || (has_res && cadd);
+    const f16* const cadd_row = cadd ? p.cadd + (long)(min(m0, p.M - 1) / p.rows_per_sample) * p.cadd_ld : nullptr;
     // amax: the WGM wave rows of the block combine their column maxes in LDS first when the
     // block's rows lie in one sample, so each (sample, column) address takes one atomic per
     // block instead of one per wave row (same-line atomic chains bound this epilogue)
@@ -456,8 +458,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
         const int nl = wn0 + j * 16 + fq * 4;
         const int n = n0 + nl;
         const bool col_ok = n < p.N;  // N % 8 == 0: a lane's 4 columns are all in or all out
-        f16x4 bq = {};
+        f16x4 bq = {}, cv = {};
         if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+        if (cadd && col_ok) cv = *reinterpret_cast<const f16x4*>(cadd_row + n);
         float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -474,6 +477,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
 #pragma unroll
               for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rv[r]);
             }
+          }
+          if (cadd) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)cv[r]);
           }
           if (do_amax) {  // (uniform) the column maxes only when an amax is reduced
             const bool ok = m0 + ml < p.M && col_ok;
@@ -516,8 +523,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // division); stores / residual loads are 32-bit-offset buffer ops (rows past M fall off the
     // end of the buffer range and are dropped / read 0).
     static_assert(BN % 32 == 0 || BN % 16 == 0, "tile width");
-    // the tile's sample for the per-(sample, column) add (rows_per_sample % BM == 0)
-    const f16* const cadd_row = cadd ? p.cadd + (long)(min(m0, p.M - 1) / p.rows_per_sample) * p.cadd_ld : nullptr;
     // GroupNorm slot statistics from the final tile in LDS: thread -> (64-row slot, 8-channel
     // chunk, row phase k of G): rows k, k + G, ... of the slot, shifted by the slot's first row
     // (no cancellation), then the G phases summed by lane shuffles (G consecutive lanes)
@@ -533,23 +538,26 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
       const int row0 = s * 64, n = n0 + c * 8;
       const f16x8 sh = *reinterpret_cast<const f16x8*>(ct + row0 * LP + c * 8);
       float s1[8], s2[8], mn[8], mx[8];
+      // min / max on the fp16 values themselves (exact; packed f16 pairs), sums in f32
+      f16x8 mn8 = sh, mx8 = sh;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s1[j] = s2[j] = 0.f;
-        mn[j] = INFINITY;
-        mx[j] = -INFINITY;
-      }
+      for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
 #pragma unroll 4
       for (int rr = k; rr < 64; rr += G0) {
         const f16x8 v = *reinterpret_cast<const f16x8*>(ct + (row0 + rr) * LP + c * 8);
+        mn8 = __builtin_elementwise_min(mn8, v);
+        mx8 = __builtin_elementwise_max(mx8, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float x = (float)v[j], a = x - (float)sh[j];
+          const float a = (float)v[j] - (float)sh[j];
           s1[j] += a;
           s2[j] += a * a;
-          mn[j] = fminf(mn[j], x);
-          mx[j] = fmaxf(mx[j], x);
         }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mn[j] = (float)mn8[j];
+        mx[j] = (float)mx8[j];
       }
 #pragma unroll
       for (int o = G0 / 2; o > 0; o >>= 1)
@@ -578,11 +586,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i][r]);
-          if (cadd) {
-            const f16x8 cv = *reinterpret_cast<const f16x8*>(cadd_row + n);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)cv[r]);
-          }
           if (gn) *reinterpret_cast<f16x8*>(ct + row * LP + c * 8) = v;  // (this thread's own element)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
         }
@@ -625,14 +628,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
             const f16x8 rq = bload(rrs, m0 + row < p.M ? off : OOB);
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[r]);
-          }
-          if constexpr (!GG) {
-            if (cadd) {
-              const f16x8 cv = *reinterpret_cast<const f16x8*>(cadd_row + n);
-#pragma unroll
-              for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)cv[r]);
-              if (gn) *reinterpret_cast<f16x8*>(ct + row * LP + c * 8) = v;  // (this thread's own element)
-            }
           }
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
         }

@@ -277,12 +277,18 @@ constexpr float SILU_NEG_BOUND = 0.2786f;
 // out = half([silu](half(x * a + b))) is monotone in x on each side of silu's minimum, so
 // max |out| is |out(x_min)| or |out(x_max)| except when SiLU is on and both extremes map below
 // the bound above; the block then scans those (rare) channels' rows itself.
+// MODE 1 with a concatenated input (x | x2 along C, GnIn.c1): channels [0, c1) read their slots
+// from part ([n][Z][c1]), channels [c1, c) from part2 ([n][Z][c - c1]) - each source's own producer
+// wrote them.  xamax (MODE 1, quant): the per-(n, c) max |x| of the INPUT from the channel
+// extremes (the per-sample int8 scale of a conv that reads the same input, e.g. the shortcut).
 template <int MODE>
 __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, GnIn in, int hw, int c, int cg,
                                                   int Z, float eps, const f16* __restrict__ gamma,
                                                   const f16* __restrict__ beta, int silu, int quant,
                                                   float2* __restrict__ coef, float* __restrict__ amax,
-                                                  float* __restrict__ amax_n) {
+                                                  float* __restrict__ amax_n,
+                                                  const float4* __restrict__ part2 = nullptr,
+                                                  float* __restrict__ xamax = nullptr) {
   __shared__ float red[2][4];
   __shared__ float stat[2];
   __shared__ int nflag;
@@ -300,10 +306,16 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
   __syncthreads();
   // one pass over the (z, channel) partials: group sums in registers, channel extremes by LDS
   // integer min / max of the order-preserving image of the float (exact, order-independent)
+  // partial of (slot z, channel g0 + j): one [n][Z][c] array, or the concat's two sources (MODE 1)
+  const int c1 = MODE == 1 ? in.c1 : c;
+  auto pv = [&](int z, int j) {
+    const int ch = g0 + j;
+    return ch < c1 ? part[((long)ni * Z + z) * c1 + ch] : part2[((long)ni * Z + z) * (c - c1) + (ch - c1)];
+  };
   float s1 = 0.f, s2 = 0.f;
   for (int e = t; e < Z * cg; e += 256) {
     const int z = e / cg, j = e - z * cg;
-    const float4 v = part[((long)ni * Z + z) * c + g0 + j];
+    const float4 v = pv(z, j);
     s1 += v.x;
     s2 += v.y;
     if (quant) {
@@ -338,7 +350,7 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     float q = 0.f;
     for (int e = t; e < Z * cg; e += 256) {
       const int z = e / cg, j = e - z * cg;
-      const float4 v = part[((long)ni * Z + z) * c + g0 + j];
+      const float4 v = pv(z, j);
       const float d = v.x - gmean;
       q += v.y + 64.0f * (d * d);
     }
@@ -364,6 +376,7 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const int ia = cmin[j], ib = cmax[j];
     const float mn = __int_as_float(ia ^ ((ia >> 31) & 0x7fffffff));
     const float mx = __int_as_float(ib ^ ((ib >> 31) & 0x7fffffff));
+    if (MODE == 1 && xamax) xamax[i] = fmaxf(fabsf(mn), fabsf(mx));
     const float lo = fabsf(gn_out(mn, k, silu)), hi = fabsf(gn_out(mx, k, silu));
     const float top = fabsf(gn_out(sc >= 0.f ? mx : mn, k, silu));  // largest z
     if (!silu) {
@@ -801,10 +814,18 @@ extern "C" int qd_groupnorm_fin(const void* y_raw, const float* in_amax, int in_
 // launches and one read of x instead of three launches and two reads.  y8: int8 codes with one
 // scale per sample (the int8-MFMA mode's conv input, = qd_quant_samples_i8 of the fp16 output);
 // else the fp16 output y (no output fake-quant: the test / diagnostic form).
-extern "C" int qd_groupnorm_part(const float* part, const void* x, int n, int hw, int c, int groups, float eps,
-                                 const void* gamma, const void* beta, int silu, void* y, int8_t* y8, float* scales,
-                                 float* ws, void* stream) {
+extern "C" int qd_groupnorm_part(const float* part, const void* x, const float* part2, const void* x2, int c1,
+                                 int n, int hw, int c, int groups, float eps, const void* gamma, const void* beta,
+                                 int silu, void* y, int8_t* y8, float* scales, float* xamax, float* ws,
+                                 void* stream) {
   QD_REQUIRE(part && x && gamma && beta && ws && (y || (y8 && scales)), "null pointer");
+  if (x2) {
+    QD_REQUIRE(part2 && c1 % 8 == 0 && c1 > 0 && c1 < c && (reinterpret_cast<uintptr_t>(part2) & 15) == 0,
+               "concat: second source's slot statistics, c1 % 8 == 0");
+  } else {
+    c1 = c;
+  }
+  QD_REQUIRE(!xamax || y8, "the input amax is produced with the int8 output");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(part) & 15) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0,
              "partials / workspace must be 16-B aligned");
   QD_REQUIRE(!y8 || (reinterpret_cast<uintptr_t>(y8) & 7) == 0, "y8 must be 8-B aligned");
@@ -817,10 +838,10 @@ extern "C" int qd_groupnorm_part(const float* part, const void* x, int n, int hw
   float2* coef = reinterpret_cast<float2*>(ws);
   float* amax = reinterpret_cast<float*>(coef + (long)n * c);
   float* amax_n = y8 ? amax + (long)n * c : nullptr;
-  const GnIn in{(const f16*)x, nullptr, c, nullptr, 0, nullptr, 0, nullptr, nullptr};
+  const GnIn in{(const f16*)x, (const f16*)x2, c1, nullptr, 0, nullptr, 0, nullptr, nullptr};
   k_gn_coeff<1><<<n * groups, 256, 0, st>>>(reinterpret_cast<const float4*>(part), in, hw, c, cg, hw / 64, eps,
                                             (const f16*)gamma, (const f16*)beta, silu, y8 != nullptr, coef, amax,
-                                            amax_n);
+                                            amax_n, reinterpret_cast<const float4*>(part2), xamax);
   const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
   if (y8) {  // (the qmax argument carries the group count of amax_n[n][group])
     if (silu) k_gn_apply<0, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, scales);

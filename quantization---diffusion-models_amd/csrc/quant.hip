@@ -880,6 +880,53 @@ __global__ void __launch_bounds__(256) k_sample_apply_i8(const f16* __restrict__
   }
 }
 
+// per-sample codes of the concat x | x2 (8-channel chunks never straddle: c1 % 8 == 0), the sample
+// max over amax[n][0..c) - k_sample_apply_i8's arithmetic, one pass, no concat copy
+__global__ void __launch_bounds__(256) k_cat_apply_i8(const f16* __restrict__ x, const f16* __restrict__ x2, int c1,
+                                                      int c, long rows, const float* __restrict__ amax,
+                                                      int8_t* __restrict__ y, float* __restrict__ sa) {
+  const long n = blockIdx.y;
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int j = threadIdx.x; j < c; j += 256) m = fmaxf(m, amax[n * c + j]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const float s = fq_scale(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])), 127);
+  const double rs = rcp_exact(s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) sa[n] = s;
+  const int cc = c / 8, c2 = c - c1;
+  const long chunks = rows * cc;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < chunks; e += (long)gridDim.x * 256) {
+    const long r = e / cc;
+    const int ch = (int)(e - r * cc) * 8;
+    const long row = n * rows + r;
+    const f16x8 v = *reinterpret_cast<const f16x8*>(ch < c1 ? x + row * c1 + ch : x2 + row * c2 + (ch - c1));
+    unsigned lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo |= (unsigned)(uint8_t)q_i8((float)v[j], s, rs) << (8 * j);
+      hi |= (unsigned)(uint8_t)q_i8((float)v[4 + j], s, rs) << (8 * j);
+    }
+    *reinterpret_cast<uint2*>(y + row * c + ch) = make_uint2(lo, hi);
+  }
+}
+
+extern "C" int qd_quant_samples_i8_cat(const void* x, const void* x2, int c1, int c, int n, long rows,
+                                       const float* amax_nc, int8_t* y, float* scales, void* stream) {
+  QD_REQUIRE(x && x2 && amax_nc && y && scales, "null pointer");
+  QD_REQUIRE(c1 > 0 && c1 < c && c1 % 8 == 0 && c % 8 == 0, "concat split: multiples of 8 channels");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(x2) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(y) & 7) == 0,
+             "alignment");
+  if ((long)n * rows == 0) return 0;
+  const long ch = (rows * (c / 8) + 255) / 256;
+  const int gx = (int)std::min<long>(std::max<long>(1, 1024 / n), ch);
+  k_cat_apply_i8<<<dim3(gx, n), 256, 0, S(stream)>>>((const f16*)x, (const f16*)x2, c1, c, rows, amax_nc, y, scales);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int qd_quant_samples_i8_amax(const void* x, int n, long per_sample, const float* amax_nc, int c,
                                         int8_t* y, float* scales, void* stream) {
   QD_REQUIRE(x && amax_nc && y && scales, "null pointer");

@@ -726,36 +726,61 @@ def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, 
     return (out, part) if gn_stats else out
 
 
-def groupnorm_part_i8(x, part, groups, eps, gamma, beta, silu=False):
-    """GroupNorm(+SiLU) of x [N, H, W, C] from the slot statistics its producing conv reduced
-    (conv2d_i8(..., gn_stats=True)), written as int8 codes with one scale per sample:
-    (codes [N, H, W, C] int8, scales [N] fp32) - groupnorm_nhwc_i8's result without its
-    statistics pass."""
+def _part_args(x, part, x2, part2):
     _chk(x, "x")
-    n, c = x.shape[0], x.shape[-1]
-    hw = x.numel() // (n * c)
-    if part.dtype != torch.float32 or part.numel() != n * hw // 64 * c * 4:
-        raise ValueError("part must be the producer's [N*HW/64, C, 4] fp32 slot statistics")
-    y8 = _empty(x.shape, torch.int8, x.device)
+    n, c1 = x.shape[0], x.shape[-1]
+    c = c1 + (x2.shape[-1] if x2 is not None else 0)
+    hw = x.numel() // (n * c1)
+    for t, cc, name in ((part, c1, "part"), (part2, c - c1, "part2")):
+        if t is None:
+            continue
+        if t.dtype != torch.float32 or t.numel() != n * hw // 64 * cc * 4:
+            raise ValueError(f"{name} must be the producer's [N*HW/64, C, 4] fp32 slot statistics")
+    if x2 is not None:
+        _chk(x2, "x2")
+        if part2 is None or x2.shape[:-1] != x.shape[:-1]:
+            raise ValueError("concat GroupNorm: x2 of the same [N, H, W] with its slot statistics part2")
+    return n, hw, c1, c
+
+
+def groupnorm_part_i8(x, part, groups, eps, gamma, beta, silu=False, x2=None, part2=None, want_xamax=False):
+    """GroupNorm(+SiLU) of x [N, H, W, C] (| x2 along C: the skip concat, not materialised) from
+    the slot statistics its producing conv(s) reduced (conv2d_i8(..., gn_stats=True)), written as
+    int8 codes with one scale per sample: (codes [N, H, W, C] int8, scales [N] fp32) -
+    groupnorm_nhwc_i8's result without its statistics pass.  want_xamax: also return the input's
+    per-(n, c) max |x| [N * C] (for quant_samples_i8_cat)."""
+    n, hw, c1, c = _part_args(x, part, x2, part2)
+    y8 = _empty((*x.shape[:-1], c), torch.int8, x.device)
     sa = _empty((n,), torch.float32, x.device)
+    xam = _empty((n * c,), torch.float32, x.device) if want_xamax else None
     ws = _empty((_lib.load().qd_groupnorm_workspace(n, hw, c, groups),), torch.float32, x.device)
-    _lib.call("qd_groupnorm_part", _p(part), _p(x), n, hw, c, groups, float(eps), _p(gamma), _p(beta),
-              1 if silu else 0, None, _p(y8), _p(sa), _p(ws), _stream())
-    return y8, sa
+    _lib.call("qd_groupnorm_part", _p(part), _p(x), _p(part2), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma),
+              _p(beta), 1 if silu else 0, None, _p(y8), _p(sa), _p(xam), _p(ws), _stream())
+    return ((y8, sa), xam) if want_xamax else (y8, sa)
 
 
-def groupnorm_part(x, part, groups, eps, gamma, beta, silu=False):
+def groupnorm_part(x, part, groups, eps, gamma, beta, silu=False, x2=None, part2=None):
     """The fp16 form of groupnorm_part_i8 (tests / diagnostics)."""
-    _chk(x, "x")
-    n, c = x.shape[0], x.shape[-1]
-    hw = x.numel() // (n * c)
-    if part.dtype != torch.float32 or part.numel() != n * hw // 64 * c * 4:
-        raise ValueError("part must be the producer's [N*HW/64, C, 4] fp32 slot statistics")
-    y = _empty(x.shape, torch.float16, x.device)
+    n, hw, c1, c = _part_args(x, part, x2, part2)
+    y = _empty((*x.shape[:-1], c), torch.float16, x.device)
     ws = _empty((_lib.load().qd_groupnorm_workspace(n, hw, c, groups),), torch.float32, x.device)
-    _lib.call("qd_groupnorm_part", _p(part), _p(x), n, hw, c, groups, float(eps), _p(gamma), _p(beta),
-              1 if silu else 0, _p(y), None, None, _p(ws), _stream())
+    _lib.call("qd_groupnorm_part", _p(part), _p(x), _p(part2), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma),
+              _p(beta), 1 if silu else 0, _p(y), None, None, None, _p(ws), _stream())
     return y
+
+
+def quant_samples_i8_cat(x, x2, amax_nc):
+    """quant_samples_i8 of the channel concat x | x2 ([N, H, W, c1] | [N, H, W, c2]) without the
+    concat copy or an amax pass: amax_nc = the concat's per-(n, c) max |.| [N * C] (e.g.
+    groupnorm_part_i8(..., want_xamax=True)).  Returns (codes [N, H, W, C] int8, scales [N])."""
+    _chk(x, "x")
+    _chk(x2, "x2")
+    n, c1, c = x.shape[0], x.shape[-1], x.shape[-1] + x2.shape[-1]
+    rows = x.numel() // (n * c1)
+    q = _empty((*x.shape[:-1], c), torch.int8, x.device)
+    sa = _empty((n,), torch.float32, x.device)
+    _lib.call("qd_quant_samples_i8_cat", _p(x), _p(x2), c1, c, n, rows, _p(amax_nc), _p(q), _p(sa), _stream())
+    return q, sa
 
 
 def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):

@@ -357,15 +357,14 @@ class UNet2DConditionModel(nn.Module):
         skips = [h]
         # block outputs travel as Pending (conv2 / proj_out output quant + residual deferred) so a
         # following GroupNorm materialises them in its statistics pass; other consumers _get()
-        # gn_out (int8-MFMA mode): the block output's next consumer is a single-source GroupNorm
-        # (the resnet's norm1 or the transformer's norm), so the producing conv reduces its statistics
+        # gn_out (int8-MFMA mode): the block output's next consumer is a GroupNorm (the resnet's
+        # norm1 - over the skip concat in the up blocks - or the transformer's norm), so the producing
+        # conv reduces its statistics; down-block outputs also feed the up blocks' concat GroupNorms
         for blk in self.down_blocks:
-            nres = len(blk.resnets)
             for i, res in enumerate(blk.resnets):
                 h = resnet_fwd(res, h, temb_silu, tp=tps.get(id(res)), pend=True, gn_out=True)
                 if blk.attentions is not None:
-                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True,
-                                        gn_out=i + 1 < nres or blk.downsamplers is None)
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True, gn_out=True)
                 skips.append(h)
             if blk.downsamplers is not None:
                 h = run_conv(blk.downsamplers[0].conv, _get(h), gn=True)
@@ -373,16 +372,17 @@ class UNet2DConditionModel(nn.Module):
         mb = self.mid_block
         h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])), pend=True, gn_out=True)
         h = transformer_fwd(mb.attentions[0], h, ctx_kv, pend=True, gn_out=True)
-        h = resnet_fwd(mb.resnets[1], h, temb_silu, tp=tps.get(id(mb.resnets[1])), pend=True)
+        h = resnet_fwd(mb.resnets[1], h, temb_silu, tp=tps.get(id(mb.resnets[1])), pend=True, gn_out=True)
         for blk in self.up_blocks:
+            nres = len(blk.resnets)
             for i, res in enumerate(blk.resnets):
                 skip = skips.pop()
                 h = resnet_fwd(res, h, temb_silu, skip=skip, tp=tps.get(id(res)), pend=True,
-                               gn_out=blk.attentions is not None)
+                               gn_out=blk.attentions is not None or i + 1 < nres)
                 if blk.attentions is not None:
-                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True)
+                    h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True, gn_out=i + 1 < nres)
             if blk.upsamplers is not None:
-                h = run_conv(blk.upsamplers[0].conv, _get(h), upsample=True)
+                h = run_conv(blk.upsamplers[0].conv, _get(h), upsample=True, gn=True)
         h = _get(h)
         q = conv_qbits(self.conv_out)
         h = K.groupnorm_nhwc(h, self.conv_norm_out.num_groups, self.conv_norm_out.eps,
@@ -702,8 +702,17 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False, gn_out=False):
             tp = run_linear(res.time_emb_proj, temb_silu)
         sc = run_conv(res.conv_shortcut, xin) if res.conv_shortcut is not None else xin
         return _resnet_tail(res, h, temb_silu, tp, sc, pend)
-    xr = x
+    xr, sr = x, skip
     x, skip = _get(x), _get(skip)
+    if skip is not None and GN_PART and conv_i8(res.conv1) and isinstance(xr, GnReady) and isinstance(sr, GnReady) \
+            and conv_i8(res.conv_shortcut):
+        # int8-MFMA mode, up block: norm1 over the skip concat from both producers' slot statistics
+        # (no concat copy, no statistics pass); the shortcut's per-sample codes from the input maxima
+        # the coefficient kernel found (no amax pass)
+        h, xam = K.groupnorm_part_i8(x, xr.part, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight),
+                                     _f16(res.norm1.bias), silu=True, x2=skip, part2=sr.part, want_xamax=True)
+        sc = run_conv(res.conv_shortcut, K.quant_samples_i8_cat(x, skip, xam))
+        return _resnet_tail(res, h, temb_silu, tp, sc, pend, gn_out)
     if skip is not None and qs > 0:
         sc = run_conv(res.conv_shortcut, K.act_quant_cat_nhwc(x, skip, qs), prequant=True)
         h = K.groupnorm_nhwc(x, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),

@@ -284,6 +284,45 @@ def test_groupnorm_from_slot_statistics(c, hw, silu, dev):
     assert ((s0 - s8).abs() <= 2e-3 * s0).all()
 
 
+@pytest.mark.parametrize("c1,c2,hw", [(1280, 1280, 64), (1280, 640, 256), (640, 320, 1024), (320, 320, 4096)])
+def test_groupnorm_concat_from_two_producers(c1, c2, hw, dev):
+    """The up-block resnet norm1 of the int8 mode: GroupNorm(+SiLU) over the skip concat x | skip
+    from both producers' slot statistics (groups may straddle the two sources), int8 output equal to
+    the per-sample codes of its fp16 form bit for bit and within one code of the statistics-pass
+    GroupNorm of the materialised concat; the input maxima it returns equal the concat's per-(n, c)
+    max |.|, and quant_samples_i8_cat equals quant_samples_i8 of the materialised concat."""
+    k = K()
+    g = torch.Generator().manual_seed(c1 + c2 + hw)
+    n, c = 2, c1 + c2
+    side = int(hw ** 0.5)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    def producer(cc, shift):  # a 1x1 int8 conv + residual whose epilogue reduces the slot statistics
+        x = (torch.randn(n, hw, cc, generator=g) * 2).half()
+        xq, sa = R.quant_samples_i8(x.numpy())
+        w = (torch.randn(cc, cc, generator=g) / cc ** 0.5).half().numpy()
+        wq, sw = R.weight_rows_i8(w)
+        rsd = (torch.randn(n, side, side, cc, generator=g) * 3 + shift).half().to(dev)
+        return k.conv2d_i8(t(xq.reshape(n, side, side, cc)), t(sa), t(wq.reshape(cc, 1, 1, cc)), t(sw), cc, 1, 0,
+                           residual=rsd, gn_stats=True)
+
+    x, p1 = producer(c1, 1.5)
+    skip, p2 = producer(c2, -0.5)
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half().to(dev)
+    bet = (0.1 * torch.randn(c, generator=g)).half().to(dev)
+    cat = k.concat_c(x, skip)
+    (q8, s8), xam = k.groupnorm_part_i8(x, p1, 32, 1e-5, gam, bet, silu=True, x2=skip, part2=p2, want_xamax=True)
+    h16 = k.groupnorm_part(x, p1, 32, 1e-5, gam, bet, silu=True, x2=skip, part2=p2)
+    qr, sr = k.quant_samples_i8(h16)
+    assert torch.equal(s8, sr) and torch.equal(q8, qr)
+    q0, s0 = k.groupnorm_nhwc_i8(cat, 32, 1e-5, gam, bet, silu=True)
+    assert (q0.int() - q8.int()).abs().max().item() <= 1 and ((s0 - s8).abs() <= 2e-3 * s0).all()
+    assert torch.equal(xam, cat.float().abs().view(n, -1, c).amax(1).reshape(-1))
+    qc, sc = k.quant_samples_i8_cat(x, skip, xam)
+    qm, sm = k.quant_samples_i8(cat)
+    assert torch.equal(sc, sm) and torch.equal(qc, qm)
+
+
 # ------------------------------------------------------------------ model level
 def _cfgdict(cfg):
     import dataclasses
