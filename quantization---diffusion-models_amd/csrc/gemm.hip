@@ -1806,9 +1806,14 @@ typedef __attribute__((address_space(3))) const f16x8 lds_f16x8_t;
 __device__ __forceinline__ int lds_addr(const void* p) { return (int)(uintptr_t)(lds_char_t*)p; }
 __device__ __forceinline__ f16x8 lds_read16(int addr) { return *(lds_f16x8_t*)(uintptr_t)(unsigned)addr; }
 
-template <int BN, int W, int RING>
-__global__ void __launch_bounds__(512, 1) k_conv_halo_i8(GemmArgs p) {
-  constexpr int BM = 256, NT = 512, NW = 8, WGN = 2;
+// BM 256: 8 waves (4 x 2), one block per CU - the grid at the 64x64 level is a single wave of
+// 256 tiles whose epilogues all run at the same time; BM 128 (round 4): 4 waves (2 x 2) and two
+// blocks per CU (LDS <= 80 KB each), so one block's epilogue runs beside the other's K loop;
+// BM 64 (round 4, W 8 only): 2 waves, one 8x8 image per tile - the 8x8 level, whose 512-row
+// GEMMs otherwise run as split-K implicit GEMMs re-reading each input pixel 9 times
+template <int BN, int W, int RING, int BM = 256>
+__global__ void __launch_bounds__(2 * BM, BM == 256 ? 1 : 2) k_conv_halo_i8(GemmArgs p) {
+  constexpr int NT = 2 * BM, NW = NT / 64, WGN = 2;
   constexpr int WM = 64, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
   constexpr int RB = BM / W;                  // image rows per tile
   constexpr int W2P = (W + 2 + 7) / 8 * 8;    // halo row pitch in pixels (multiple of 8)
@@ -1822,11 +1827,14 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo_i8(GemmArgs p) {
   constexpr int LOOPB = 2 * HB + RING * BB + SCR;
   constexpr int EPIB = epi_lds_halves(BM, BN) * 2;
   constexpr int LDSB = LOOPB > EPIB ? LOOPB : EPIB;
-  static_assert(LDSB <= 163840, "halo + weight ring exceed the 160 KB of LDS");
+  static_assert(LDSB * (BM == 256 ? 1 : 2) <= 163840, "halo + weight ring exceed the 160 KB of LDS");
+  static_assert(BM == 256 || BM == 128 || BM == 64, "tile rows");
   // the next chunk's halo groups (taps 0 .. HL-1) must be older than the weight tile a chunk's
   // last tap waits for (issued at tap 10 - RING); the previous chunk's last taps issue none
   static_assert(RING >= 3 && HL >= 1 && HL <= 10 - RING, "halo staging vs weight ring depth");
-  static_assert(W % 16 == 0 && 64 % W == 0 && WN % 8 == 0, "tile geometry");
+  // W 8 (the 8x8 level): a 16-pixel fragment spans two image rows, so a lane's pixel is
+  // (row fr / W, column fr % W); BM 64 (one image per tile: the halo is one image's rows)
+  static_assert((W % 16 == 0 || (W == 8 && BM == 64)) && 64 % W == 0 && WN % 8 == 0, "tile geometry");
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
   char* const halo = smem;
   char* const ring = smem + 2 * HB;
@@ -1893,7 +1901,8 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo_i8(GemmArgs p) {
   int abase[2][3];
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx) {
-    const int lo = (fr + kx) * RS + ((fq ^ (((fr + kx) >> 1) & 3)) << 4);
+    const int px = (fr / W) * W2P + fr % W + kx;  // the lane's halo pixel (fr < W for W >= 16)
+    const int lo = px * RS + ((fq ^ ((px >> 1) & 3)) << 4);
     abase[0][kx] = lds_addr(halo) + (wm0 / W) * W2P * RS + lo;
     abase[1][kx] = abase[0][kx] + HB;
   }
@@ -2040,19 +2049,23 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo_i8(GemmArgs p) {
   }
 }
 
-template <int BN, int RING>
+template <int BN, int RING, int BM = 256>
 static void launch_halo_i8(const GemmArgs& p, hipStream_t st) {
-  const int nwg = (p.M / 256) * (p.N / BN) * p.splits;
-  if (p.W == 64) k_conv_halo_i8<BN, 64, RING><<<nwg, 512, 0, st>>>(p);
-  else if (p.W == 32) k_conv_halo_i8<BN, 32, RING><<<nwg, 512, 0, st>>>(p);
-  else k_conv_halo_i8<BN, 16, RING><<<nwg, 512, 0, st>>>(p);
+  const int nwg = (p.M / BM) * (p.N / BN) * p.splits;
+  if constexpr (BM == 64) {
+    k_conv_halo_i8<BN, 8, RING, 64><<<nwg, 128, 0, st>>>(p);
+  } else {
+    if (p.W == 64) k_conv_halo_i8<BN, 64, RING, BM><<<nwg, 2 * BM, 0, st>>>(p);
+    else if (p.W == 32) k_conv_halo_i8<BN, 32, RING, BM><<<nwg, 2 * BM, 0, st>>>(p);
+    else k_conv_halo_i8<BN, 16, RING, BM><<<nwg, 2 * BM, 0, st>>>(p);
+  }
 }
 
-// halo kernel applicability: 3x3 / stride 1 / pad 1, 64-channel chunks, whole-row 256-pixel tiles
-static bool halo_ok(const GemmArgs& p, int bn, int chunk = 64) {
-  return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && p.Cip % chunk == 0 && p.N % bn == 0 &&
-         (p.W == 16 || p.W == 32 || p.W == 64) && p.Ho == p.H && p.Wo == p.W && p.H % (256 / p.W) == 0 &&
-         (p.rows_per_sample % 64 == 0);
+// halo kernel applicability: 3x3 / stride 1 / pad 1, 64-channel chunks, whole-row bm-pixel tiles
+static bool halo_ok(const GemmArgs& p, int bn, int chunk = 64, int bm = 256) {
+  const bool w_ok = bm == 64 ? (p.W == 8 && p.H == 8 && chunk == 32) : (p.W == 16 || p.W == 32 || p.W == 64);
+  return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && p.Cip % chunk == 0 && p.N % bn == 0 && w_ok &&
+         p.Ho == p.H && p.Wo == p.W && p.H % (bm / p.W) == 0 && (p.rows_per_sample % 64 == 0);
 }
 
 // split-K reduction + epilogue: block = 4*RPT rows x 256 columns (64 column quads x 4 row
@@ -2306,9 +2319,9 @@ extern "C" int qd_gemm_force(int variant) {
   const int v = variant >= 1000 ? variant % 1000 : variant, sp = variant >= 1000 ? variant / 1000 : 0;
   QD_REQUIRE(v == -1 || (v >= 0 && v < 4) ||
                  (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 203) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
-                 (v >= 130 && v <= 134) || (v >= 140 && v <= 144),
+                 (v >= 130 && v <= 134) || (v >= 140 && v <= 149),
              "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..117, fp8: 120..123), 200-203 halo conv, "
-             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-144); + 1000 * s: split-K count s (1 = unsplit)");
+             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-149); + 1000 * s: split-K count s (1 = unsplit)");
   QD_REQUIRE(sp <= 32, "qd_gemm_force: split count above 32");
   g_force = v;
   g_split = sp;
@@ -2936,15 +2949,18 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // k_splitk_reduce_gn (64-row blocks)
 static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu, bool post = false,
                     bool gn = false) {
-  if (g_force >= 140 && g_force <= 144 && !geglu && Kh % 288 == 0) {
+  if (g_force >= 140 && g_force <= 149 && !geglu && Kh % 288 == 0) {
     // int8 halo conv (applicability checked at launch): 140 BN 160 / 141 BN 128 (3-slot weight
-    // ring), 142 / 143 / 144 BN 160 with 4 / 5 / 6 slots; K splits over whole 64-code chunks
-    // while the blocks fit one resident round (1 block / CU)
-    const int bn = g_force == 141 ? 128 : 160;
-    if (N % bn == 0 && M % 256 == 0) {
-      const long tiles_mn = (long)(M / 256) * (N / bn);
+    // ring), 142 / 143 / 144 BN 160 with 4 / 5 / 6 slots (256-pixel tiles); 145 / 146 / 147:
+    // 128-pixel tiles, two blocks per CU - BN 160 with 4 / 3 slots, BN 128 with 3; 148 / 149: one
+    // 8x8 image per tile (64 pixels), BN 160 / 128, 3 slots; K splits over whole 64-code chunks
+    // while the blocks fit one resident round
+    const int bn = g_force == 141 || g_force == 147 || g_force == 149 ? 128 : 160;
+    const int bm = g_force >= 148 ? 64 : g_force >= 145 ? 128 : 256;
+    if (N % bn == 0 && M % bm == 0) {
+      const long tiles_mn = (long)(M / bm) * (N / bn);
       const int nc = Kh / 288;
-      Plan pl{2, 256, bn, g_force - 140, 1, nc};
+      Plan pl{2, bm, bn, g_force - 140, 1, nc};
       int fsp;
       if (forced_split(nc, 1, fsp)) {  // explicit split count (tuner candidate)
         pl.splits = fsp;
@@ -2953,7 +2969,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
       }
       for (int sp = 2; sp <= nc; ++sp) {
         if (nc % sp != 0) continue;
-        if (tiles_mn * sp > 256) break;
+        if (tiles_mn * sp > 256L * (bm == 256 ? 1 : bm == 128 ? 2 : 3)) break;
         pl.splits = sp;
         pl.kps = nc / sp;
       }
@@ -3013,7 +3029,7 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   const bool post = (p.epi & QD_EPI_AMAX_POST) != 0, gn = epi_gn(p.epi);
   Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post,
                     gn);
-  if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 32))) {  // int8 halo conv not applicable
+  if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 32, pl.bm))) {  // int8 halo conv not applicable
     const int f = g_force;
     g_force = -1;
     pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post, gn);
@@ -3029,6 +3045,11 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
     if (pl.var == 2) launch_halo_i8<160, 4>(p, st);
     else if (pl.var == 3) launch_halo_i8<160, 5>(p, st);
     else if (pl.var == 4) launch_halo_i8<160, 6>(p, st);
+    else if (pl.var == 5) launch_halo_i8<160, 4, 128>(p, st);
+    else if (pl.var == 6) launch_halo_i8<160, 3, 128>(p, st);
+    else if (pl.var == 7) launch_halo_i8<128, 3, 128>(p, st);
+    else if (pl.var == 8) launch_halo_i8<160, 3, 64>(p, st);
+    else if (pl.var == 9) launch_halo_i8<128, 3, 64>(p, st);
     else if (pl.bn == 160) launch_halo_i8<160, 3>(p, st);
     else launch_halo_i8<128, 3>(p, st);
   };

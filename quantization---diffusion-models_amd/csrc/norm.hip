@@ -271,8 +271,8 @@ constexpr float SILU_NEG_BOUND = 0.2786f;
 // One block per (n, group): group mean / rstd from the partials (fixed thread -> partial map,
 // fixed reduction tree: deterministic).  MODE 0: k_gn_stats' per-channel shifted sums; MODE 1: the
 // 64-row slot moments (mean, M2, min, max) a producing int8 conv's epilogue wrote (gemm.hip
-// QD_EPI_GNSTATS), merged in two passes (Chan: mean = sum of slot means / P, M2 = sum M2 +
-// 64 sum (slot mean - mean)^2, P = Z slots x cg channels).  Then per channel the affine coefficients and - when the
+// QD_EPI_GNSTATS), merged in one pass as shifted sums about the group's first slot mean
+// (sum (x - K) = 64 sum (mean_i - K), sum (x - K)^2 = sum (M2_i + 64 (mean_i - K)^2)).  Then per channel the affine coefficients and - when the
 // output is fake-quantized - its exact amax from the channel's min / max input:
 // out = half([silu](half(x * a + b))) is monotone in x on each side of silu's minimum, so
 // max |out| is |out(x_min)| or |out(x_max)| except when SiLU is on and both extremes map below
@@ -312,12 +312,22 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const int ch = g0 + j;
     return ch < c1 ? part[((long)ni * Z + z) * c1 + ch] : part2[((long)ni * Z + z) * (c - c1) + (ch - c1)];
   };
+  // MODE 1: one pass of shifted sums over the slots (shift K1 = the group's first slot mean):
+  // sum over rows of (x - K1) = 64 sum (mean_i - K1), of (x - K1)^2 = sum (M2_i + 64 (mean_i - K1)^2)
+  // - then MODE 0's finalisation with the shift K1
+  const float K1 = MODE == 1 ? pv(0, 0).x : 0.f;
   float s1 = 0.f, s2 = 0.f;
   for (int e = t; e < Z * cg; e += 256) {
     const int z = e / cg, j = e - z * cg;
     const float4 v = pv(z, j);
-    s1 += v.x;
-    s2 += v.y;
+    if constexpr (MODE == 0) {
+      s1 += v.x;
+      s2 += v.y;
+    } else {
+      const float d = v.x - K1;
+      s1 += 64.0f * d;
+      s2 += v.y + 64.0f * (d * d);
+    }
     if (quant) {
       const int a = __float_as_int(v.z), b = __float_as_int(v.w);
       atomicMin(&cmin[j], a ^ ((a >> 31) & 0x7fffffff));
@@ -331,41 +341,16 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     red[1][t >> 6] = s2;
   }
   __syncthreads();
-  if constexpr (MODE == 0) {
-    if (t == 0) {
-      const float S1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-      const float S2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-      const float cnt = (float)cg * (float)hw;
-      const float m = S1 / cnt;                        // mean of the shifted values
-      const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
-      stat[0] = m + gn_load1(in, c, ni, (long)ni * hw, g0);
-      stat[1] = 1.0f / sqrtf(var + eps);
-    }
-    __syncthreads();
-  } else {
-    // slot moments: s1 summed the slot means (s2 is unused); second pass over the same partials for
-    // the deviations of the slot means from the group mean
-    const float P = (float)Z * (float)cg;
-    const float gmean = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) / P;
-    float q = 0.f;
-    for (int e = t; e < Z * cg; e += 256) {
-      const int z = e / cg, j = e - z * cg;
-      const float4 v = pv(z, j);
-      const float d = v.x - gmean;
-      q += v.y + 64.0f * (d * d);
-    }
-    q = wave_sum(q);
-    __syncthreads();  // (every thread read red[0] above)
-    if ((t & 63) == 0) red[1][t >> 6] = q;
-    __syncthreads();
-    if (t == 0) {
-      const float M2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-      const float var = fmaxf(M2 / (P * 64.0f), 0.f);
-      stat[0] = gmean;
-      stat[1] = 1.0f / sqrtf(var + eps);
-    }
-    __syncthreads();
+  if (t == 0) {
+    const float S1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    const float S2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    const float cnt = (float)cg * (float)hw;
+    const float m = S1 / cnt;                        // mean of the shifted values
+    const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
+    stat[0] = m + (MODE == 0 ? gn_load1(in, c, ni, (long)ni * hw, g0) : K1);
+    stat[1] = 1.0f / sqrtf(var + eps);
   }
+  __syncthreads();
   for (int j = t; j < cg; j += 256) {
     const int ch = g0 + j;
     const long i = (long)ni * c + ch;

@@ -348,7 +348,7 @@ def _i8_split_cands(M, N, K, halo=False):
         return []
     out = [v + 1000 * s for v in I8_SPLIT_VARIANTS for s in SPLIT_COUNTS]
     if halo:
-        out += [v + 1000 * s for v in (142, 143) for s in (1, 2, 3, 4, 5, 6)]
+        out += [v + 1000 * s for v in (142, 143, 145, 148) for s in (1, 2, 4, 5, 10)]
     return out
 
 
@@ -501,7 +501,9 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 # split gives identical bits - the tuner below only picks the fastest.
 I8_VARIANTS = (110, 111, 112, 113, 114, 115, 116, 117,  # qd_gemm_force ids: LDS-DMA variants 10-17 (64-B rows)
                130, 131, 132, 133, 134)  # ping-pong 256 x {256, 320, 192, 160, 128}
-I8_HALO_VARIANTS = (140, 141, 142, 143, 144)  # 3x3 conv, activation halo staged once per 64-code chunk (BN 160 / 128; 142-144 deeper weight rings)
+# 3x3 conv, activation halo staged once per 64-code chunk: 256-pixel tiles (BN 160 / 128; 142-144 deeper
+# weight rings), 145-147 128-pixel tiles with two blocks per CU, 148 / 149 one 8x8 image per tile
+I8_HALO_VARIANTS = (140, 141, 142, 143, 144, 145, 146, 147, 148, 149)
 
 
 def quant_rows_i8(x2d, out=None, scales=None):

@@ -132,13 +132,16 @@ def main():
             run_w4(dev)
     elif a.add:
         n0 = K.load_table(OUT)
+        dropped = {}
         if a.drop_epi:
             for key in [k for k in K.gemm_choices() if k[0] in ("conv_i8", "linear_i8") and
                         (k[11] if k[0] == "conv_i8" else k[5]) & a.drop_epi]:
-                del K._TUNE[key]
+                dropped[key] = K._TUNE.pop(key)
         log(f"committed table ({n0} shapes)")
         for name in a.models.split(","):
             {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)
+        for key, ch in dropped.items():  # shapes these runs do not meet keep their committed choice
+            K._TUNE.setdefault(key, ch)
     else:
         for name in a.models.split(","):
             {"sd15": run_sd15, "sdxl": run_sdxl, "sd35": run_sd35}[name](dev)

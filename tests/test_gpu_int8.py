@@ -151,7 +151,8 @@ def test_linear_i8_post_residual_amax_and_fused_scale(variant, dev):
                                                         (1280, 1280, 3, 1, 8, False), (960, 320, 3, 1, 16, False),
                                                         (320, 320, 3, 1, 64, False), (640, 640, 3, 1, 32, False),
                                                         (1280, 1280, 3, 1, 16, False), (640, 320, 3, 1, 32, True)])
-@pytest.mark.parametrize("variant", I8_FORCE + [140, 141, 142, 143, 144] + I8_SPLIT_FORCE + [1142, 2142, 3143, 5142])
+@pytest.mark.parametrize("variant", I8_FORCE + [140, 141, 142, 143, 144, 145, 146, 147, 148, 149] + I8_SPLIT_FORCE +
+                         [1142, 2142, 3143, 5142, 2145, 4145, 1148, 4148, 10148])
 def test_conv2d_i8_bit_exact(cin, cout, ksz, stride, hw, ups, variant, dev):
     k = K()
     rng = np.random.default_rng(cin * 7 + cout + ksz)
@@ -193,7 +194,8 @@ GN_CASES = [(320, 320, 3, 1, 64, False, False, True), (320, 320, 3, 1, 64, False
             (640, 640, 3, 1, 32, False, True, True), (1280, 1280, 3, 1, 16, False, False, True),
             (1280, 1280, 3, 1, 8, False, True, False), (320, 320, 1, 1, 64, False, True, False),
             (640, 640, 3, 2, 32, False, False, False), (640, 320, 3, 1, 32, True, True, False)]
-GN_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 140, 141, 142, 3110, 4111, 2142, 6111]
+GN_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 140, 141, 142, 145, 146, 147, 148, 149, 3110, 4111, 2142,
+            2145, 5148, 6111]
 
 
 @pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups,res,cadd", GN_CASES)
