@@ -11,6 +11,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 using namespace qd;
 
@@ -347,6 +348,272 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
   }
 }
 
+// 32x32x16 form of the swapped-operand kernel for narrow heads (d = DP - 8: SD1.5's d = 40).
+// The 16x16x32 kernel above is VALU-issue bound at d = 40: per 64-key tile a wave issues 28 MFMAs
+// (each holds the SIMD's issue for 8 cycles), two cross-lane max reductions and 32 exponentials for
+// its 32 queries.  Here a wave owns 32 queries as the 32 columns of v_mfma_f32_32x32x16 accumulators:
+//   * S^T = K Q^T in 2 (key blocks) x DP/16 MFMAs: 6 at DP = 48 instead of 16 (QK^T depth 48, not 64);
+//   * the running max rides in the QK^T MFMA: K column d (depth padding) is 1.0 and Q column d holds
+//     -m, the lane's running max rounded to fp16 (every shift m_new - m_old between two fp16 values is
+//     exact in fp32, so P = exp2(s - m) and the O rescales stay consistent); no seed registers;
+//   * a lane holds 32 scores of ONE query (its partner lane l ^ 32 the other 32), so the online
+//     softmax needs one in-register max tree; the cross-lane max (v_permlane32_swap) runs only on
+//     the rare tiles that move the running max (wave-uniform test on the lane maxima = the same
+//     decision as on the query maxima); the first tile is peeled (it always sets the max);
+//   * P^T leaves the accumulator as the B operand of O^T += V^T P^T with no lane movement (registers
+//     8s..8s+7 of key block jb = k-step s; element j of lane half h is key 32jb + 16s + 8(j>>2) + 4h
+//     + (j&3)), V^T comes from the row-major V tile with ds_read_b64_tr_b16 in that k order;
+//   * O^T rows d..DV-1 of the last 32-row block are padding except row d = sum(P) (V column d = 1.0).
+// Per wave and 64-key tile: 6 + 2 * DV/32 MFMAs (14 at d = 40 vs 28), 6 ds_read_b128 + 8 * DV/32
+// transposed reads, 32 v_exp_f32 + 16 packs as before.
+constexpr int v_stride32(int dv) { return (dv + 31) / 64 * 64 + 32; }  // 16 x odd dwords per row
+
+template <int DP, int DV, int NB, int NW>
+__global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
+                                                int ldk, const f16* __restrict__ v, int ldv,
+                                                f16* __restrict__ o, int ldo, int heads, int sq, int skv,
+                                                float scale_log2) {
+  static_assert(DP % 16 == 0 && DV % 32 == 0 && DP <= DV && NB == 2, "k_attn32 shapes");
+  constexpr int d = DP - 8;                 // head_dim; depth d is the running-max column
+  constexpr int KS = DP / 16;               // QK^T k-steps of 16
+  constexpr int KCH = DP / 8;               // 16-B chunks per staged K / V row
+  constexpr int KCHP = (KCH + 7) / 8 * 8;   // K row padded so the XOR swizzle stays in the row
+  constexpr int VST = v_stride32(DV);
+  constexpr int KSZ = KV_T * KCHP * 8, VSZ = KV_T * VST;
+  constexpr int NT = NW * 64;
+  constexpr int NL = (KV_T * (KCH - 1) + NT - 1) / NT;  // staged chunks per thread (d / 8 per row)
+  constexpr int DB = DV / 32;               // 32-row O^T blocks
+  __shared__ __attribute__((aligned(16))) f16 smem[NB * (KSZ + VSZ)];
+
+  constexpr int QB = NW * 32;
+  const int nqb = (sq + QB - 1) / QB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int bh = wg / nqb;
+  const int b = bh / heads, h = bh % heads;
+  const int q0 = (wg - bh * nqb) * QB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5, fr = lane & 15;
+
+  const f16* qb = q + (long)b * sq * ldq + h * d;
+  const f16* kb = k + (long)b * skv * ldk + h * d;
+  const f16* vb = v + (long)b * skv * ldv + h * d;
+  f16* ob = o + (long)b * sq * ldo + h * d;
+  const int qrow = q0 + wid * 32 + lr;
+
+  // B operand of S^T: Q[qrow][16ks + 8lh .. +8] * scale * log2(e); the last chunk of lane half 1
+  // is the padding chunk d / 8 whose element 0 carries -m
+  f16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int c = 2 * s + lh;
+    f16x8 val = {};
+    if (qrow < sq && c < KCH - 1) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) val[e] = (f16)((float)val[e] * scale_log2);
+    qf[s] = val;
+  }
+
+  // padding, written once: K chunk d/8 = {1, 0, ..}, further chunks 0; V column d = 1.0, columns > d 0
+  for (int i = tid; i < NB * KV_T * (KCHP - KCH + 1); i += NT) {
+    const int np = KCHP - KCH + 1;
+    const int bf = i / (KV_T * np), row = (i / np) % KV_T, c = KCH - 1 + i % np;
+    f16x8 z = {};
+    if (c == KCH - 1) z[0] = (f16)1.0f;
+    *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + ((c ^ (row & 7)) << 3)) = z;
+  }
+  for (int i = tid; i < NB * KV_T * (VST - d); i += NT) {
+    const int bf = i / (KV_T * (VST - d)), row = (i / (VST - d)) % KV_T, col = d + i % (VST - d);
+    smem[bf * (KSZ + VSZ) + KSZ + row * VST + col] = (f16)(col == d ? 1.0f : 0.0f);
+  }
+
+  const unsigned kbytes = (unsigned)(((long)(skv - 1) * ldk + d) * 2);
+  const unsigned vbytes = (unsigned)(((long)(skv - 1) * ldv + d) * 2);
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kb, 0, kbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vb, 0, vbytes, 0x00020000);
+  unsigned koff[NL], voff[NL];
+  int kdst[NL], vdst[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int e = tid + i * NT, row = e / (KCH - 1), c = e % (KCH - 1);
+    const bool ok = e < KV_T * (KCH - 1);
+    koff[i] = (unsigned)(row * ldk + c * 8) * 2u;
+    voff[i] = (unsigned)(row * ldv + c * 8) * 2u;
+    kdst[i] = ok ? row * KCHP * 8 + ((c ^ (row & 7)) << 3) : -1;
+    vdst[i] = ok ? KSZ + row * VST + c * 8 : -1;
+  }
+  f16x8 kst[NL], vst[NL];
+  auto load_tile = [&](int kv0) {
+    const unsigned ks0 = (unsigned)(kv0 * ldk) * 2u, vs0 = (unsigned)(kv0 * ldv) * 2u;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      kst[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, (int)(koff[i] + ks0), 0, 0));
+      vst[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, (int)(voff[i] + vs0), 0, 0));
+    }
+  };
+  auto store_tile = [&](f16* base) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+      if (kdst[i] >= 0) {
+        *reinterpret_cast<f16x8*>(base + kdst[i]) = kst[i];
+        *reinterpret_cast<f16x8*>(base + vdst[i]) = vst[i];
+      }
+  };
+
+  f32x16 oacc[DB];
+#pragma unroll
+  for (int j = 0; j < DB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[j][r] = 0.f;
+  float mrow = 0.f;  // running max (log2 domain), an fp16 value; -mrow sits in qf[KS - 1][0] of lane half 1
+
+  int kread[2][KS];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int row = jb * 32 + lr, c = 2 * s + lh;
+      kread[jb][s] = row * KCHP * 8 + ((c ^ (row & 7)) << 3);
+    }
+  // 16-lane group g = lane >> 4 reads rows 4lh + (0..3) (+8 for elements 4..7) x columns 16(g & 1) + 0..15
+  const int vread = KSZ + (4 * lh + (fr >> 2)) * VST + 16 * ((lane >> 4) & 1) + (fr & 3) * 4;
+
+  const int ntiles = (skv + KV_T - 1) / KV_T;
+  auto tile = [&](const f16* ks, int kv0, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    f32x16 sacc[2];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(ks + kread[jb][s]);
+        sacc[jb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], s == 0 ? f32x16{} : sacc[jb], 0, 0, 0);
+      }
+    if (kv0 + KV_T > skv) {
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kv0 + jb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= skv) sacc[jb][r] = -INFINITY;
+    }
+    // lane max of the 32 scores: a depth-4 tree of three-input maxes
+    float lmx;
+    {
+      const f32x16& a = sacc[0];
+      const f32x16& c = sacc[1];
+      const float t0 = max3f(a[0], a[1], a[2]), t1 = max3f(a[3], a[4], a[5]), t2 = max3f(a[6], a[7], a[8]);
+      const float t3 = max3f(a[9], a[10], a[11]), t4 = max3f(a[12], a[13], a[14]), t5 = max3f(a[15], c[0], c[1]);
+      const float t6 = max3f(c[2], c[3], c[4]), t7 = max3f(c[5], c[6], c[7]), t8 = max3f(c[8], c[9], c[10]);
+      const float t9 = max3f(c[11], c[12], c[13]), t10 = maxf_raw(c[14], c[15]);
+      lmx = max3f(max3f(t0, t1, t2), max3f(t3, t4, t5), max3f(max3f(t6, t7, t8), t9, t10));
+    }
+    // deferred rescale as in k_attn (threshold 8, log2 domain); the first tile always sets the max
+    if (FIRST || __any(lmx > 8.0f)) {
+      const float mx = xmax32(lmx);  // the query max relative to mrow (lanes l, l ^ 32)
+      const float mnew = (float)(f16)fminf(mrow + (FIRST ? mx : fmaxf(mx, 0.f)), 60000.f);
+      const float dd = mnew - mrow;  // exact: both fp16 values
+      if (!FIRST) {
+        const float alpha = __builtin_amdgcn_exp2f(-dd);
+#pragma unroll
+        for (int j = 0; j < DB; ++j) oacc[j] *= alpha;
+      }
+      sacc[0] -= dd;
+      sacc[1] -= dd;
+      mrow = mnew;
+      if (lh) qf[KS - 1][0] = (f16)(-mnew);
+    }
+    f16x8 pf[2][2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pf[jb][s][e] = (f16)__builtin_amdgcn_exp2f(sacc[jb][8 * s + e]);
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < DB; ++j) {
+          const f16* vp = ks + vread + (32 * jb + 16 * s) * VST + 32 * j;
+          const f16x4 lo = tr_read(vp);
+          const f16x4 hi = tr_read(vp + 8 * VST);
+          const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          oacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[jb][s], oacc[j], 0, 0, 0);
+        }
+  };
+
+  // K/V double buffer, tile loop unrolled x2 after the peeled first tile; one barrier per tile
+  f16* const b0 = smem;
+  f16* const b1 = smem + KSZ + VSZ;
+  load_tile(0);
+  __syncthreads();  // padding writes above
+  store_tile(b0);
+  __syncthreads();
+  if (ntiles > 1) load_tile(KV_T);
+  tile(b0, 0, std::true_type{});
+  int t = 1;
+  for (; t + 1 < ntiles; t += 2) {  // tiles t (b1) and t + 1 (b0)
+    store_tile(b1);
+    __syncthreads();
+    load_tile((t + 1) * KV_T);
+    tile(b1, t * KV_T, std::false_type{});
+    store_tile(b0);
+    __syncthreads();
+    if (t + 2 < ntiles) load_tile((t + 2) * KV_T);
+    tile(b0, (t + 1) * KV_T, std::false_type{});
+  }
+  if (t < ntiles) {  // odd tail
+    store_tile(b1);
+    __syncthreads();
+    tile(b1, t * KV_T, std::false_type{});
+  }
+  // ---- epilogue: lane holds O^T rows 32j + 8(r>>2) + 4lh + (r&3) of query qrow; row d = sum(P) ----
+  constexpr int dj = d >> 5, dw = d & 31, dh = (dw >> 2) & 1, drr = (dw & 3) + 4 * (dw >> 3);
+  const float lsum = __shfl(oacc[dj][drr], lr + 32 * dh, 64);
+  if (qrow < sq) {
+    const float inv = 1.0f / lsum;
+#pragma unroll
+    for (int j = 0; j < DB; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * j + 8 * g + 4 * lh;
+        if (dd < d) {
+          f16x4 w;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) w[r] = (f16)(oacc[j][4 * g + r] * inv);
+          *reinterpret_cast<f16x4*>(ob + (long)qrow * ldo + dd) = w;
+        }
+      }
+  }
+}
+
+// tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2) of k_attn;
+// 6 = k_attn (heuristic) instead of k_attn32 at d = 40; 7 / 8 = k_attn32 with 4 / 8 waves; unset: heuristic
+static int attn_forced() {
+  static const int forced = [] {
+    const char* e = getenv("QD_ATTN_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  return forced;
+}
+
+template <int DP, int DV>
+static void launch32(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                     int ldo, int b, int heads, int sq, int skv, float scale, hipStream_t st) {
+  const float sl2 = scale * 1.4426950408889634f;
+  const int forced = attn_forced();
+  // 8 waves (256 queries share each staged K / V tile) while the grid keeps >= 512 blocks
+  if (forced == 8 || (forced != 7 && (long)((sq + 255) / 256) * b * heads >= 512)) {
+    k_attn32<DP, DV, 2, 8><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
+  } else {
+    k_attn32<DP, DV, 2, 4><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
+        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
+  }
+}
+
 template <int DP, int DV>
 static void launch(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                    int ldo, int b, int heads, int sq, int skv, int d, float scale, int causal, hipStream_t st) {
@@ -365,11 +632,7 @@ static void launch(const void* q, int ldq, const void* k, int ldk, const void* v
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
     return;
   } else {
-  // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2); unset: heuristic
-  static const int forced = [] {
-    const char* e = getenv("QD_ATTN_CFG");
-    return e ? atoi(e) : 0;
-  }();
+  const int forced = attn_forced();
   if (forced == 1) {
     k_attn<DP, DV, NB, 8, 2><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, d, sl2);
@@ -433,6 +696,11 @@ static int attention_impl(const void* q, int ldq, const void* k, int ldk, const 
   hipStream_t st = S(stream);
   const int c = causal;
   // DP: QK^T depth (multiple of 32 >= d); DV: PV rows, a multiple of 16 > d (row d = denominator)
+  if (!c && d == 40 && attn_forced() < 6) {  // head_dim 40: the 32x32x16 kernel (DP = 48)
+    launch32<48, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, scale, st);
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
   if (d <= 32) launch<32, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
   else if (d <= 40) launch<64, 48>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
   else if (d <= 56) launch<64, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, d, scale, c, st);
