@@ -8,6 +8,7 @@ echo "[rc] tests rc=$rc"
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/rc_smoke.log 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py > gpurun_out/rc_bench_sd15.log 2>&1 || exit 1
+timeout -k 10 300 python3 bench.py --mode w8a8-sq-int8 > gpurun_out/rc_bench_int8.log 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py --model sdxl --steps 2 > gpurun_out/rc_bench_sdxl.log 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py --model sd35 --denoise-steps 10 --steps 2 > gpurun_out/rc_bench_sd35.log 2>&1 || exit 1
 bash scripts/prof_bench.sh rc 300 || exit 1
