@@ -377,7 +377,9 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   constexpr int d = DP - 8;                 // head_dim; depth d is the running-max column
   constexpr int KS = DP / 16;               // QK^T k-steps of 16
   constexpr int KCH = DP / 8;               // 16-B chunks per staged K / V row
-  constexpr int KCHP = (KCH + 7) / 8 * 8;   // K row padded so the XOR swizzle stays in the row
+  // K rows padded to an odd number of 16-B chunks (no swizzle): the 16 rows a ds_read_b128 lane group
+  // reads (rows {0-3, 12-15, 20-27} + 32jb of one chunk) fall on 16 distinct 16-B bank slots
+  constexpr int KCHP = KCH | 1;
   constexpr int VST = v_stride32(DV);
   constexpr int KSZ = KV_T * KCHP * 8, VSZ = KV_T * VST;
   constexpr int NT = NW * 64;
@@ -421,7 +423,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
     const int bf = i / (KV_T * np), row = (i / np) % KV_T, c = KCH - 1 + i % np;
     f16x8 z = {};
     if (c == KCH - 1) z[0] = (f16)1.0f;
-    *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + ((c ^ (row & 7)) << 3)) = z;
+    *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + c * 8) = z;
   }
   for (int i = tid; i < NB * KV_T * (VST - d); i += NT) {
     const int bf = i / (KV_T * (VST - d)), row = (i / (VST - d)) % KV_T, col = d + i % (VST - d);
@@ -440,7 +442,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
     const bool ok = e < KV_T * (KCH - 1);
     koff[i] = (unsigned)(row * ldk + c * 8) * 2u;
     voff[i] = (unsigned)(row * ldv + c * 8) * 2u;
-    kdst[i] = ok ? row * KCHP * 8 + ((c ^ (row & 7)) << 3) : -1;
+    kdst[i] = ok ? row * KCHP * 8 + c * 8 : -1;
     vdst[i] = ok ? KSZ + row * VST + c * 8 : -1;
   }
   f16x8 kst[NL], vst[NL];
@@ -474,7 +476,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int row = jb * 32 + lr, c = 2 * s + lh;
-      kread[jb][s] = row * KCHP * 8 + ((c ^ (row & 7)) << 3);
+      kread[jb][s] = row * KCHP * 8 + c * 8;
     }
   // 16-lane group g = lane >> 4 reads rows 4lh + (0..3) (+8 for elements 4..7) x columns 16(g & 1) + 0..15
   const int vread = KSZ + (4 * lh + (fr >> 2)) * VST + 16 * ((lane >> 4) & 1) + (fr & 3) * 4;

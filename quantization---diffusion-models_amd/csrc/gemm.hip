@@ -82,10 +82,29 @@ struct GemmArgs {
   const f16* cadd;
   int cadd_ld;
   float* gnp;
+  // block order (tile_of): 0 = split fastest, then N tiles (one XCD's blocks share A rows); 1 = M
+  // tiles fastest (one XCD's blocks share a weight slice) - set by the host when the weights are
+  // the larger operand (the low UNet levels: 1280 x 11520 weights against 2048 x 1280 activations)
+  int mfast;
 };
 
 constexpr int BK = 64;
 constexpr unsigned OOB = 0x80000000u;
+
+// block (XCD-remapped index wg) -> (M tile, N tile, K split); see GemmArgs::mfast
+__device__ __forceinline__ void tile_of(const GemmArgs& p, int wg, int nbm, int nbn, int& bm, int& bn, int& split) {
+  if (p.mfast) {
+    bm = wg % nbm;
+    const int r = wg / nbm;
+    split = r % p.splits;
+    bn = r / p.splits;
+  } else {
+    const int tile = wg / p.splits;
+    split = wg - tile * p.splits;
+    bm = tile / nbn;
+    bn = tile - bm * nbn;
+  }
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
@@ -657,8 +676,8 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
+  int bm, bn, split;
+  tile_of(p, wg, nbm, nbn, bm, bn, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
@@ -1032,8 +1051,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
+  int bm, bn, split;
+  tile_of(p, wg, nbm, nbn, bm, bn, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
@@ -1246,8 +1265,8 @@ __global__ void __launch_bounds__(512, 2) k_gemm_pp(GemmArgs p) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
+  int bm, bn, split;
+  tile_of(p, wg, nbm, nbn, bm, bn, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
@@ -1493,8 +1512,8 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
+  int bm, bn, split;
+  tile_of(p, wg, nbm, nbn, bm, bn, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int img = m0 / (p.Ho * p.Wo), oh0 = (m0 - img * p.Ho * p.Wo) / W;
   const int c_beg = split * p.kps, c_end = c_beg + p.kps;  // 64-channel chunks of this split
@@ -1637,8 +1656,8 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
+  int bm, bn, split;
+  tile_of(p, wg, nbm, nbn, bm, bn, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int img = m0 / (p.Ho * p.Wo), oh0 = (m0 - img * p.Ho * p.Wo) / W;
   const int c_beg = split * p.kps, nch = p.kps;
@@ -1845,8 +1864,8 @@ __global__ void __launch_bounds__(2 * BM, BM == 256 ? 1 : 2) k_conv_halo_i8(Gemm
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = wg / p.splits, split = wg - tile * p.splits;
-  const int bm = tile / nbn, bn = tile - bm * nbn;
+  int bm, bn, split;
+  tile_of(p, wg, nbm, nbn, bm, bn, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int img = m0 / (p.Ho * W), oh0 = (m0 - img * p.Ho * W) / W;
   const int c_beg = split * p.kps, nch = p.kps;  // 64-code chunks of this split
@@ -2719,6 +2738,17 @@ static void launch_gemv(const GemmArgs& p, int fmt, int cpl, hipStream_t st) {
   else launch_gemv_fmt<QD_WFMT_I4>(p, cpl, st);
 }
 
+// M-fastest block order when the weight operand outweighs the activation operand (GemmArgs::mfast);
+// QD_NO_MFAST=1 keeps the split / N-fastest order everywhere (A/B knob)
+static int block_order(const GemmArgs& p, bool linear) {
+  static const bool off = [] {
+    const char* e = getenv("QD_NO_MFAST");
+    return e && atoi(e) != 0;
+  }();
+  if (off) return 0;
+  return (double)p.N * p.K > (double)p.M * (linear ? p.K : p.Cip) ? 1 : 0;
+}
+
 static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 ? (long)pl.splits * M * N : 0; }
 
 template <int AMODE>
@@ -2746,6 +2776,7 @@ static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t
   }
   p.splits = pl.splits;
   p.kps = pl.kps;
+  p.mfast = block_order(p, AMODE == AM_LINEAR);
   if (pl.splits == 1) {
     launch_tile<AMODE, false>(p, pl, fmt, st);
   } else {
@@ -3041,6 +3072,7 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   }
   p.splits = pl.splits;
   p.kps = pl.kps;
+  p.mfast = block_order(p, AMODE == AM_LINEAR);
   auto halo = [&]() {  // the kernel reads p.splits itself (int32 slabs when split)
     if (pl.var == 2) launch_halo_i8<160, 4>(p, st);
     else if (pl.var == 3) launch_halo_i8<160, 5>(p, st);
