@@ -445,21 +445,23 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
     kdst[i] = ok ? row * KCHP * 8 + c * 8 : -1;
     vdst[i] = ok ? KSZ + row * VST + c * 8 : -1;
   }
-  f16x8 kst[NL], vst[NL];
-  auto load_tile = [&](int kv0) {
+  // two register staging sets: tile t + 2 is loaded while tile t is computed and stored to LDS
+  // after tile t + 1, so an L2 round trip has two tiles of compute to land in
+  f16x8 kst[2][NL], vst[2][NL];
+  auto load_tile = [&](int set, int kv0) {
     const unsigned ks0 = (unsigned)(kv0 * ldk) * 2u, vs0 = (unsigned)(kv0 * ldv) * 2u;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      kst[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, (int)(koff[i] + ks0), 0, 0));
-      vst[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, (int)(voff[i] + vs0), 0, 0));
+      kst[set][i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, (int)(koff[i] + ks0), 0, 0));
+      vst[set][i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, (int)(voff[i] + vs0), 0, 0));
     }
   };
-  auto store_tile = [&](f16* base) {
+  auto store_tile = [&](int set, f16* base) {
 #pragma unroll
     for (int i = 0; i < NL; ++i)
       if (kdst[i] >= 0) {
-        *reinterpret_cast<f16x8*>(base + kdst[i]) = kst[i];
-        *reinterpret_cast<f16x8*>(base + vdst[i]) = vst[i];
+        *reinterpret_cast<f16x8*>(base + kdst[i]) = kst[set][i];
+        *reinterpret_cast<f16x8*>(base + vdst[i]) = vst[set][i];
       }
   };
 
@@ -546,28 +548,33 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
         }
   };
 
-  // K/V double buffer, tile loop unrolled x2 after the peeled first tile; one barrier per tile
+  // K/V double buffer in LDS (odd tiles in b1 / staging set 1, even tiles in b0 / set 0), tile
+  // loop unrolled x2 after the peeled first tile; one barrier per tile
   f16* const b0 = smem;
   f16* const b1 = smem + KSZ + VSZ;
-  load_tile(0);
+  load_tile(0, 0);
   __syncthreads();  // padding writes above
-  store_tile(b0);
+  store_tile(0, b0);
   __syncthreads();
-  if (ntiles > 1) load_tile(KV_T);
+  load_tile(1, KV_T);
+  load_tile(0, 2 * KV_T);
   tile(b0, 0, std::true_type{});
   int t = 1;
   for (; t + 1 < ntiles; t += 2) {  // tiles t (b1) and t + 1 (b0)
-    store_tile(b1);
+    // (unconditional loads - past the last tile they read zeros off the buffer's end - so every
+    // path through the loop has the same loads in flight and the staging stores wait for their
+    // own set only, vmcnt(2))
+    store_tile(1, b1);
     __syncthreads();
-    load_tile((t + 1) * KV_T);
+    load_tile(1, (t + 2) * KV_T);
     tile(b1, t * KV_T, std::false_type{});
-    store_tile(b0);
+    store_tile(0, b0);
     __syncthreads();
-    if (t + 2 < ntiles) load_tile((t + 2) * KV_T);
+    load_tile(0, (t + 3) * KV_T);
     tile(b0, (t + 1) * KV_T, std::false_type{});
   }
   if (t < ntiles) {  // odd tail
-    store_tile(b1);
+    store_tile(1, b1);
     __syncthreads();
     tile(b1, t * KV_T, std::false_type{});
   }
