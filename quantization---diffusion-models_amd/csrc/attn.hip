@@ -368,13 +368,15 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
 // transposed reads, 32 v_exp_f32 + 16 packs as before.
 constexpr int v_stride32(int dv) { return (dv + 31) / 64 * 64 + 32; }  // 16 x odd dwords per row
 
-template <int DP, int DV, int NB, int NW>
+template <int D, int DP, int DV, int NB, int NW>
 __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                 int ldk, const f16* __restrict__ v, int ldv,
                                                 f16* __restrict__ o, int ldo, int heads, int sq, int skv,
                                                 float scale_log2) {
-  static_assert(DP % 16 == 0 && DV % 32 == 0 && DP <= DV && NB == 2, "k_attn32 shapes");
-  constexpr int d = DP - 8;                 // head_dim; depth d is the running-max column
+  static_assert(DP % 16 == 0 && DV % 32 == 0 && NB == 2, "k_attn32 shapes");
+  constexpr int d = D;                      // head_dim; depth d is the running-max column
+  constexpr int CD = D / 8;                 // data chunks per row; chunk CD holds the ones column
+  static_assert(D % 8 == 0 && DP >= D + 8 && D < DV, "k_attn32 head geometry");
   constexpr int KS = DP / 16;               // QK^T k-steps of 16
   constexpr int KCH = DP / 8;               // 16-B chunks per staged K / V row
   // K rows padded to an odd number of 16-B chunks (no swizzle): the 16 rows a ds_read_b128 lane group
@@ -383,7 +385,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   constexpr int VST = v_stride32(DV);
   constexpr int KSZ = KV_T * KCHP * 8, VSZ = KV_T * VST;
   constexpr int NT = NW * 64;
-  constexpr int NL = (KV_T * (KCH - 1) + NT - 1) / NT;  // staged chunks per thread (d / 8 per row)
+  constexpr int NL = (KV_T * CD + NT - 1) / NT;  // staged chunks per thread (d / 8 per row)
   constexpr int DB = DV / 32;               // 32-row O^T blocks
   __shared__ __attribute__((aligned(16))) f16 smem[NB * (KSZ + VSZ)];
 
@@ -411,18 +413,18 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   for (int s = 0; s < KS; ++s) {
     const int c = 2 * s + lh;
     f16x8 val = {};
-    if (qrow < sq && c < KCH - 1) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + c * 8);
+    if (qrow < sq && c < CD) val = *reinterpret_cast<const f16x8*>(qb + (long)qrow * ldq + c * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) val[e] = (f16)((float)val[e] * scale_log2);
     qf[s] = val;
   }
 
   // padding, written once: K chunk d/8 = {1, 0, ..}, further chunks 0; V column d = 1.0, columns > d 0
-  for (int i = tid; i < NB * KV_T * (KCHP - KCH + 1); i += NT) {
-    const int np = KCHP - KCH + 1;
-    const int bf = i / (KV_T * np), row = (i / np) % KV_T, c = KCH - 1 + i % np;
+  for (int i = tid; i < NB * KV_T * (KCHP - CD); i += NT) {
+    const int np = KCHP - CD;
+    const int bf = i / (KV_T * np), row = (i / np) % KV_T, c = CD + i % np;
     f16x8 z = {};
-    if (c == KCH - 1) z[0] = (f16)1.0f;
+    if (c == CD) z[0] = (f16)1.0f;
     *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + c * 8) = z;
   }
   for (int i = tid; i < NB * KV_T * (VST - d); i += NT) {
@@ -438,8 +440,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   int kdst[NL], vdst[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int e = tid + i * NT, row = e / (KCH - 1), c = e % (KCH - 1);
-    const bool ok = e < KV_T * (KCH - 1);
+    const int e = tid + i * NT, row = e / CD, c = e % CD;
+    const bool ok = e < KV_T * CD;
     koff[i] = (unsigned)(row * ldk + c * 8) * 2u;
     voff[i] = (unsigned)(row * ldv + c * 8) * 2u;
     kdst[i] = ok ? row * KCHP * 8 + c * 8 : -1;
@@ -470,7 +472,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   for (int j = 0; j < DB; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[j][r] = 0.f;
-  float mrow = 0.f;  // running max (log2 domain), an fp16 value; -mrow sits in qf[KS - 1][0] of lane half 1
+  float mrow = 0.f;  // running max (log2 domain), an fp16 value; -mrow sits in qf[CD / 2][0] of lane half CD & 1
 
   int kread[2][KS];
 #pragma unroll
@@ -525,7 +527,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
       sacc[0] -= dd;
       sacc[1] -= dd;
       mrow = mnew;
-      if (lh) qf[KS - 1][0] = (f16)(-mnew);
+      if (lh == (CD & 1)) qf[CD / 2][0] = (f16)(-mnew);
     }
     f16x8 pf[2][2];
 #pragma unroll
@@ -599,7 +601,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
 }
 
 // tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2) of k_attn;
-// 6 = k_attn (heuristic) instead of k_attn32 at d = 40; 7 / 8 = k_attn32 with 4 / 8 waves; unset: heuristic
+// 6 = k_attn (heuristic) instead of k_attn32 at d = 40 / 80; 7 / 8 = k_attn32 with 4 / 8 waves;
+// unset: heuristic
 static int attn_forced() {
   static const int forced = [] {
     const char* e = getenv("QD_ATTN_CFG");
@@ -608,17 +611,17 @@ static int attn_forced() {
   return forced;
 }
 
-template <int DP, int DV>
+template <int D, int DP, int DV>
 static void launch32(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                      int ldo, int b, int heads, int sq, int skv, float scale, hipStream_t st) {
   const float sl2 = scale * 1.4426950408889634f;
   const int forced = attn_forced();
   // 8 waves (256 queries share each staged K / V tile) while the grid keeps >= 512 blocks
   if (forced == 8 || (forced != 7 && (long)((sq + 255) / 256) * b * heads >= 512)) {
-    k_attn32<DP, DV, 2, 8><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
+    k_attn32<D, DP, DV, 2, 8><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
   } else {
-    k_attn32<DP, DV, 2, 4><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
+    k_attn32<D, DP, DV, 2, 4><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
   }
 }
@@ -705,8 +708,14 @@ static int attention_impl(const void* q, int ldq, const void* k, int ldk, const 
   hipStream_t st = S(stream);
   const int c = causal;
   // DP: QK^T depth (multiple of 32 >= d); DV: PV rows, a multiple of 16 > d (row d = denominator)
-  if (!c && d == 40 && attn_forced() < 6) {  // head_dim 40: the 32x32x16 kernel (DP = 48)
-    launch32<48, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, scale, st);
+  // the 32x32x16 kernel (QK^T depth: head dims + the running-max column, PV rows: head dims + the
+  // denominator row, both rounded up) at head_dim 40 / 80 (at 64 - DP 80, DV 96 - it measured
+  // slower than k_attn: profiles/r04m_attn_ab.log); QD_ATTN_CFG 1-6 select k_attn, 7 / 8 force
+  // k_attn32 with 4 / 8 waves
+  const int fc = attn_forced();
+  if (!c && (fc == 0 || fc == 7 || fc == 8) && (d == 40 || d == 80)) {
+    if (d == 40) launch32<40, 48, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, scale, st);
+    else launch32<80, 96, 96>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, scale, st);
     QD_CHECK_LAUNCH();
     return 0;
   }
