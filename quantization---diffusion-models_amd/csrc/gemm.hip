@@ -2738,15 +2738,16 @@ static void launch_gemv(const GemmArgs& p, int fmt, int cpl, hipStream_t st) {
   else launch_gemv_fmt<QD_WFMT_I4>(p, cpl, st);
 }
 
-// M-fastest block order when the weight operand outweighs the activation operand (GemmArgs::mfast);
+// M-fastest block order when the weight operand's bytes outweigh the activation operand's
+// (GemmArgs::mfast; wbytes / abytes: bytes per element of each, in the K the GemmArgs carry);
 // QD_NO_MFAST=1 keeps the split / N-fastest order everywhere (A/B knob)
-static int block_order(const GemmArgs& p, bool linear) {
+static int block_order(const GemmArgs& p, bool linear, double wbytes, double abytes) {  // (convs: linear false)
   static const bool off = [] {
     const char* e = getenv("QD_NO_MFAST");
     return e && atoi(e) != 0;
   }();
   if (off) return 0;
-  return (double)p.N * p.K > (double)p.M * (linear ? p.K : p.Cip) ? 1 : 0;
+  return (double)p.N * p.K * wbytes > (double)p.M * (linear ? p.K : p.Cip) * abytes ? 1 : 0;
 }
 
 static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 ? (long)pl.splits * M * N : 0; }
@@ -2776,7 +2777,9 @@ static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t
   }
   p.splits = pl.splits;
   p.kps = pl.kps;
-  p.mfast = block_order(p, AMODE == AM_LINEAR);
+  // (convs only: with the rule on the linears too, SD3.5-L ran 3.8 % slower end to end - its
+  // small-M context-stream projections, int4 or fp16 buffer alike - profiles/r04p_ab_mfast_sd35.log)
+  p.mfast = AMODE == AM_LINEAR ? 0 : block_order(p, false, 2.0, 2.0);
   if (pl.splits == 1) {
     launch_tile<AMODE, false>(p, pl, fmt, st);
   } else {
@@ -3072,7 +3075,7 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   }
   p.splits = pl.splits;
   p.kps = pl.kps;
-  p.mfast = block_order(p, AMODE == AM_LINEAR);
+  p.mfast = AMODE == AM_LINEAR ? 0 : block_order(p, false, 1.0, 1.0);  // int8 codes on both sides (half view)
   auto halo = [&]() {  // the kernel reads p.splits itself (int32 slabs when split)
     if (pl.var == 2) launch_halo_i8<160, 4>(p, st);
     else if (pl.var == 3) launch_halo_i8<160, 5>(p, st);
