@@ -486,9 +486,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   const int vread = KSZ + (4 * lh + (fr >> 2)) * VST + 16 * ((lane >> 4) & 1) + (fr & 3) * 4;
 
   const int ntiles = (skv + KV_T - 1) / KV_T;
-  auto tile = [&](const f16* ks, int kv0, auto first_tag) {
-    constexpr bool FIRST = decltype(first_tag)::value;
-    f32x16 sacc[2];
+  // S'^T = K (c Q)^T - m of the 64-key tile at ks (kv0 = its first key), keys past skv -> -inf
+  auto qk = [&](const f16* ks, int kv0, f32x16 (&sacc)[2]) {
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -503,6 +502,12 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
         for (int r = 0; r < 16; ++r)
           if (kv0 + jb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= skv) sacc[jb][r] = -INFINITY;
     }
+  };
+  // online softmax of one tile's scores + O^T += V^T P^T from the tile's V at ks
+  // (a software-pipelined form - QK^T of tile t + 1 issued before the softmax of tile t, three LDS
+  // buffers - measured 339 vs 250 us: its 165 VGPRs leave one 8-wave block per CU)
+  auto softmax_pv = [&](const f16* ks, f32x16 (&sacc)[2], auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
     // lane max of the 32 scores: a depth-4 tree of three-input maxes
     float lmx;
     {
@@ -550,35 +555,42 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
         }
   };
 
-  // K/V double buffer in LDS (odd tiles in b1 / staging set 1, even tiles in b0 / set 0), tile
-  // loop unrolled x2 after the peeled first tile; one barrier per tile
-  f16* const b0 = smem;
-  f16* const b1 = smem + KSZ + VSZ;
-  load_tile(0, 0);
-  __syncthreads();  // padding writes above
-  store_tile(0, b0);
-  __syncthreads();
-  load_tile(1, KV_T);
-  load_tile(0, 2 * KV_T);
-  tile(b0, 0, std::true_type{});
-  int t = 1;
-  for (; t + 1 < ntiles; t += 2) {  // tiles t (b1) and t + 1 (b0)
-    // (unconditional loads - past the last tile they read zeros off the buffer's end - so every
-    // path through the loop has the same loads in flight and the staging stores wait for their
-    // own set only, vmcnt(2))
-    store_tile(1, b1);
-    __syncthreads();
-    load_tile(1, (t + 2) * KV_T);
-    tile(b1, t * KV_T, std::false_type{});
+  {
+    auto tile = [&](const f16* ks, int kv0, auto first_tag) {
+      f32x16 sacc[2];
+      qk(ks, kv0, sacc);
+      softmax_pv(ks, sacc, first_tag);
+    };
+    // K/V double buffer in LDS (odd tiles in b1 / staging set 1, even tiles in b0 / set 0), tile
+    // loop unrolled x2 after the peeled first tile; one barrier per tile
+    f16* const b0 = smem;
+    f16* const b1 = smem + KSZ + VSZ;
+    load_tile(0, 0);
+    __syncthreads();  // padding writes above
     store_tile(0, b0);
     __syncthreads();
-    load_tile(0, (t + 3) * KV_T);
-    tile(b0, (t + 1) * KV_T, std::false_type{});
-  }
-  if (t < ntiles) {  // odd tail
-    store_tile(1, b1);
-    __syncthreads();
-    tile(b1, t * KV_T, std::false_type{});
+    load_tile(1, KV_T);
+    load_tile(0, 2 * KV_T);
+    tile(b0, 0, std::true_type{});
+    int t = 1;
+    for (; t + 1 < ntiles; t += 2) {  // tiles t (b1) and t + 1 (b0)
+      // (unconditional loads - past the last tile they read zeros off the buffer's end - so every
+      // path through the loop has the same loads in flight and the staging stores wait for their
+      // own set only, vmcnt(2))
+      store_tile(1, b1);
+      __syncthreads();
+      load_tile(1, (t + 2) * KV_T);
+      tile(b1, t * KV_T, std::false_type{});
+      store_tile(0, b0);
+      __syncthreads();
+      load_tile(0, (t + 3) * KV_T);
+      tile(b0, (t + 1) * KV_T, std::false_type{});
+    }
+    if (t < ntiles) {  // odd tail
+      store_tile(1, b1);
+      __syncthreads();
+      tile(b1, t * KV_T, std::false_type{});
+    }
   }
   // ---- epilogue: lane holds O^T rows 32j + 8(r>>2) + 4lh + (r&3) of query qrow; row d = sum(P) ----
   constexpr int dj = d >> 5, dw = d & 31, dh = (dw >> 2) & 1, drr = (dw & 3) + 4 * (dw >> 3);
