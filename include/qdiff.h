@@ -77,6 +77,10 @@ int qd_act_apply(const void* x, void* y, int layout, int n, int c, int h, int w,
  * call unless amax_zeroed). */
 int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,
                           float* amax, int amax_zeroed, void* y, void* stream);
+/* qd_act_quant_cat_nhwc's apply pass with the per-(n, c) maxima of [x | x2] already known
+ * (amax [n*(c1+c2)], e.g. qd_groupnorm_xamax over the same concat): no column-max pass. */
+int qd_act_apply_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,
+                          const float* amax, void* y, void* stream);
 
 /* ---------------- weight fake-quant (offline, on device) ----------------------------- */
 /* Row-group absmax RTN of quantize_weight_absmax / _per_channel_ / _per_tensor_
@@ -250,6 +254,12 @@ int qd_layernorm_i8(const void* x, int rows, int c, float eps, const void* gamma
 int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
                  float eps, const void* gamma, const void* beta, int silu, int q_bits,
                  void* y, float* ws, void* stream);
+/* qd_groupnorm (q_bits > 0) that also writes xamax [n*c] = max |x| per (sample, channel) of the
+ * input x | x2 (from the statistics pass's channel extremes; exact): the up blocks' skip-concat
+ * shortcut quant then needs no column-max pass of its own (qd_act_apply_cat_nhwc). */
+int qd_groupnorm_xamax(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
+                       float eps, const void* gamma, const void* beta, int silu, int q_bits,
+                       void* y, float* xamax, float* ws, void* stream);
 /* qd_groupnorm on the finalized output of the conv that feeds it, recomputed on the fly from
  * the raw conv output y_raw [N, HW, C]: x = half(fq(y_raw; in_amax[n][c], in_bits) + cadd[n][c])
  * (in_bits 0: no quantization; cadd [N][cadd_ld] may be NULL) - the q_y = output_quant(y) of

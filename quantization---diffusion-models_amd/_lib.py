@@ -28,6 +28,7 @@ SIGNATURES = {
     "qd_act_fakequant": [P, P, I, I, I, I, I, I, I, I, P, P],
     "qd_act_apply": [P, P, I, I, I, I, I, I, I, I, P, P],
     "qd_act_quant_cat_nhwc": [P, I, P, I, I, I, I, P, I, P, P],
+    "qd_act_apply_cat_nhwc": [P, I, P, I, I, I, I, P, P, P],
     "qd_weight_quant": [P, I, I, I, I, P, P, P, P],
     "qd_pack_int4": [P, I, I, P, P],
     "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
@@ -35,6 +36,7 @@ SIGNATURES = {
     "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, I, P, P],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
+    "qd_groupnorm_xamax": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P, P],
     "qd_groupnorm_fq_in": [P, P, I, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_groupnorm_fin": [P, P, I, P, P, I, P, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_layernorm": [P, I, I, F, P, P, P, P],

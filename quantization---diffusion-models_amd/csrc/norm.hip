@@ -279,8 +279,8 @@ constexpr float SILU_NEG_BOUND = 0.2786f;
 // the bound above; the block then scans those (rare) channels' rows itself.
 // MODE 1 with a concatenated input (x | x2 along C, GnIn.c1): channels [0, c1) read their slots
 // from part ([n][Z][c1]), channels [c1, c) from part2 ([n][Z][c - c1]) - each source's own producer
-// wrote them.  xamax (MODE 1, quant): the per-(n, c) max |x| of the INPUT from the channel
-// extremes (the per-sample int8 scale of a conv that reads the same input, e.g. the shortcut).
+// wrote them.  xamax (quant): the per-(n, c) max |x| of the INPUT from the channel extremes (the
+// input quant of a conv that reads the same input, e.g. the up blocks' skip-concat shortcut).
 template <int MODE>
 __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ part, GnIn in, int hw, int c, int cg,
                                                   int Z, float eps, const f16* __restrict__ gamma,
@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const int ia = cmin[j], ib = cmax[j];
     const float mn = __int_as_float(ia ^ ((ia >> 31) & 0x7fffffff));
     const float mx = __int_as_float(ib ^ ((ib >> 31) & 0x7fffffff));
-    if (MODE == 1 && xamax) xamax[i] = fmaxf(fabsf(mn), fabsf(mx));
+    if (xamax) xamax[i] = fmaxf(fabsf(mn), fabsf(mx));
     const float lo = fabsf(gn_out(mn, k, silu)), hi = fabsf(gn_out(mx, k, silu));
     const float top = fabsf(gn_out(sc >= 0.f ? mx : mn, k, silu));  // largest z
     if (!silu) {
@@ -654,7 +654,7 @@ extern "C" int qd_groupnorm_workspace(int n, int hw, int c, int groups) {
 
 static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float eps, const void* gamma,
                          const void* beta, int silu, int q_bits, void* y, float* ws, hipStream_t st,
-                         int8_t* y8 = nullptr, float* sa8 = nullptr) {
+                         int8_t* y8 = nullptr, float* sa8 = nullptr, float* xamax = nullptr) {
   QD_REQUIRE(in.x && gamma && beta && (y || y8) && ws, "null pointer");
   QD_REQUIRE(!y8 || (sa8 && q_bits == 0), "int8 output: scales needed, no fake-quant bits");
   QD_REQUIRE(groups > 0 && c % groups == 0, "groups must divide C");
@@ -676,7 +676,9 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   QD_REQUIRE(!fin || (!in.x2 && !(in.res && in.cadd) && !y8), "materialised input: no concat / int8 output, residual or temb");
   const bool xf = !fin && (in.qmax > 0 || in.cadd);
   // (the residual-input form always takes the streaming passes: its statistics pass writes x)
-  if (const int G = y8 || fin ? 0 : gn_fused_groups(n, hw, c, groups)) {
+  QD_REQUIRE(!xamax || q_bits > 0 || y8, "the input amax comes from the quantized output's channel extremes");
+  // (xamax: the three-pass form, whose coefficient kernel reduces the channel extremes)
+  if (const int G = y8 || fin || xamax ? 0 : gn_fused_groups(n, hw, c, groups)) {
     const dim3 gf(groups / G, n);
 #define QD_GN_FUSED(XFV, SV, QV)                                                                               \
   k_gn_fused<XFV, SV, QV><<<gf, 256, 0, st>>>(in, hw, c, cg, G, eps, (const f16*)gamma, (const f16*)beta, qmax, \
@@ -702,7 +704,7 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
   // (the coefficient stage recomputes its shift / fallback elements from the raw sources; the
   // apply pass reads the materialised x)
   k_gn_coeff<0><<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta,
-                                            silu, qmax > 0 || y8, coef, amax, amax_n);
+                                            silu, qmax > 0 || y8, coef, amax, amax_n, nullptr, xamax);
   const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
   if (fin) {
     const GnIn inx{in.xout, nullptr, c, nullptr, 0, nullptr, 0, nullptr, nullptr};
@@ -746,6 +748,20 @@ extern "C" int qd_groupnorm(const void* x, const void* x2, int c1, int n, int hw
   else c1 = c;
   GnIn in{(const f16*)x, (const f16*)x2, c1, nullptr, 0, nullptr, 0, nullptr, nullptr};
   return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream));
+}
+
+// qd_groupnorm (q_bits > 0) that also writes xamax[n * c + ch] = max |input| of each (sample, channel)
+// of x | x2, from the statistics pass's channel extremes: the input quant of the skip-concat shortcut
+// without its own column-max pass (qd_act_apply_cat_nhwc)
+extern "C" int qd_groupnorm_xamax(const void* x, const void* x2, int c1, int n, int hw, int c, int groups,
+                                  float eps, const void* gamma, const void* beta, int silu, int q_bits,
+                                  void* y, float* xamax, float* ws, void* stream) {
+  QD_REQUIRE(xamax && q_bits > 0, "xamax output needs a quantized GroupNorm output");
+  if (x2) QD_REQUIRE(c1 % 8 == 0 && c1 > 0 && c1 < c, "bad concat split (must be a multiple of 8)");
+  else c1 = c;
+  GnIn in{(const f16*)x, (const f16*)x2, c1, nullptr, 0, nullptr, 0, nullptr, nullptr};
+  return run_groupnorm(in, n, hw, c, groups, eps, gamma, beta, silu, q_bits, y, ws, S(stream), nullptr, nullptr,
+                       xamax);
 }
 
 extern "C" int qd_groupnorm_i8(const void* x, const void* x2, int c1, const float* in_amax, int in_bits,

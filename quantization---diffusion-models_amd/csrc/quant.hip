@@ -651,6 +651,22 @@ extern "C" int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int 
   return 0;
 }
 
+// qd_act_quant_cat_nhwc's apply pass with the per-(n, c) maxima of [x | x2] given (amax [n][c1 + c2],
+// e.g. from qd_groupnorm_xamax over the same concat): no column-max pass
+extern "C" int qd_act_apply_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,
+                                     const float* amax, void* y, void* stream) {
+  QD_REQUIRE(x && x2 && y && amax, "null pointer");
+  QD_REQUIRE(c1 % 8 == 0 && c2 % 8 == 0 && c1 > 0 && c2 > 0, "concat widths must be multiples of 8");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "bad n_bits");
+  const int c = c1 + c2;
+  if ((long)n * hw == 0) return 0;
+  const CrGeom g = cr_geom(n, hw, c);
+  k_apply_nhwc<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, S(stream)>>>((const f16*)x, (const f16*)x2, c1, (f16*)y,
+                                                                        hw, c, c, qmax_of(n_bits), g.rpb, amax);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---------------------------------------------------------------------------------------
 // SmoothQuant calibration + fold
 // ---------------------------------------------------------------------------------------

@@ -123,6 +123,20 @@ def act_apply_nhwc(x, amax, n_bits, out=None, c_valid=0):
     return y
 
 
+def act_apply_cat_nhwc(x, x2, n_bits, amax, out=None):
+    """act_quant_cat_nhwc with the per-(n, c) maxima of [x | x2] given (amax [N*(C1+C2)] fp32, e.g.
+    from groupnorm_nhwc(..., want_xamax=True) over the same concat): the apply pass only."""
+    _chk(x, "x")
+    _chk(x2, "x2")
+    n, c1, c2 = x.shape[0], x.shape[-1], x2.shape[-1]
+    hw = x.numel() // (n * c1)
+    if x2.numel() // (n * c2) != hw:
+        raise ValueError("concat sources differ in N / HW")
+    y = out if out is not None else _empty((*x.shape[:-1], c1 + c2), torch.float16, x.device)
+    _lib.call("qd_act_apply_cat_nhwc", _p(x), c1, _p(x2), c2, n, hw, n_bits, _p(amax), _p(y), _stream())
+    return y
+
+
 def act_quant_cat_nhwc(x, x2, n_bits, out=None):
     """Per-(n, c) fake-quant of the NHWC channel concat [x | x2] into one [N, H, W, C1+C2] tensor."""
     _chk(x, "x")
@@ -799,11 +813,14 @@ def fq_finalize(y, amax, n_bits, residual=None, chan_add=None, out=None):
 
 
 # ---------------------------------------------------------------- norms / elementwise
-def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, out=None, fq_in=None):
+def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, out=None, fq_in=None,
+                   want_xamax=False):
     """GroupNorm(+SiLU)(+per-(n,c) output fake-quant) of NHWC x (| x2 along C).
     fq_in = (amax [N*C] fp32, bits, cadd [N, C] or None): x is a RAW conv output and the
     normalised input is its finalized value half(fq(x) + cadd) (fq_finalize semantics),
-    recomputed on the fly instead of materialised."""
+    recomputed on the fly instead of materialised.
+    want_xamax (q_bits > 0, no fq_in): return (out, xamax) with xamax [N*C] = the input's exact
+    per-(n, c) max |x| from the statistics pass (qd_groupnorm_xamax)."""
     _chk(x, "x")
     n = x.shape[0]
     c1 = x.shape[-1]
@@ -821,6 +838,13 @@ def groupnorm_nhwc(x, groups, eps, gamma, beta, silu=False, q_bits=0, x2=None, o
         _lib.call("qd_groupnorm_fq_in", _p(x), _p(amax), bits, _p(cadd), ld, n, hw, c, groups, float(eps),
                   _p(gamma), _p(beta), 1 if silu else 0, q_bits, _p(out), _p(ws), _stream())
         return out
+    if want_xamax:
+        if q_bits <= 0:
+            raise ValueError("want_xamax needs a quantized GroupNorm output (q_bits > 0)")
+        xamax = _empty((n * c,), torch.float32, x.device)
+        _lib.call("qd_groupnorm_xamax", _p(x), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma), _p(beta),
+                  1 if silu else 0, q_bits, _p(out), _p(xamax), _p(ws), _stream())
+        return out, xamax
     _lib.call("qd_groupnorm", _p(x), _p(x2), c1, n, hw, c, groups, float(eps), _p(gamma), _p(beta),
               1 if silu else 0, q_bits, _p(out), _p(ws), _stream())
     return out

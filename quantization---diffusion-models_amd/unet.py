@@ -714,9 +714,17 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False, gn_out=False):
         sc = run_conv(res.conv_shortcut, K.quant_samples_i8_cat(x, skip, xam))
         return _resnet_tail(res, h, temb_silu, tp, sc, pend, gn_out)
     if skip is not None and qs > 0:
+        q1n = max(conv_qbits(res.conv1), 0)
+        if q1n > 0 and XAMAX_GN and x.shape[1] * x.shape[2] > 256:
+            # norm1 first: its statistics pass's channel extremes give the concat's exact per-(n, c)
+            # maxima, so the shortcut's input quant is the apply pass alone (no column-max pass)
+            h, xam = K.groupnorm_nhwc(x, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight),
+                                      _f16(res.norm1.bias), silu=True, q_bits=q1n, x2=skip, want_xamax=True)
+            sc = run_conv(res.conv_shortcut, K.act_apply_cat_nhwc(x, skip, qs, xam), prequant=True)
+            return _resnet_tail(res, h, temb_silu, tp, sc, pend)
         sc = run_conv(res.conv_shortcut, K.act_quant_cat_nhwc(x, skip, qs), prequant=True)
         h = K.groupnorm_nhwc(x, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight), _f16(res.norm1.bias),
-                             silu=True, q_bits=max(conv_qbits(res.conv1), 0), x2=skip)
+                             silu=True, q_bits=q1n, x2=skip)
         return _resnet_tail(res, h, temb_silu, tp, sc, pend)
     xin = K.concat_c(x, skip) if skip is not None else x
     if conv_i8(res.conv1):  # int8-MFMA mode: GroupNorm + SiLU emits conv1's int8 codes
@@ -933,6 +941,7 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
 # the post-residual amax epilogue runs unsplit (no split-K slabs): used where M is large enough
 # that the GEMM would not split anyway (the 64x64 and 32x32 levels of SD1.5 at CFG batch 8)
 AMAX_POST_MIN_ROWS = 8192
+XAMAX_GN = not os.environ.get("QD_NO_XAMAX_GN")  # A/B switch: the concat shortcut's column-max pass
 AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
 LN_FQ = not os.environ.get("QD_NO_LN_FQ")  # A/B switch: proj_in finalize as its own pass before norm1
 I8_AMAX_FUSE = not os.environ.get("QD_NO_I8_AMAX_FUSE")  # A/B switch: proj_out's int8 scale by its own pass

@@ -473,6 +473,29 @@ def test_groupnorm_two_sources(dev):
     assert torch.equal(y1, y2)
 
 
+@pytest.mark.parametrize("hw,c1,c2", [(4096, 640, 320), (1024, 1280, 640), (300, 320, 320), (4096, 320, 320)])
+def test_groupnorm_xamax_feeds_concat_quant(hw, c1, c2, dev):
+    """qd_groupnorm_xamax: the up blocks' norm1 over the skip concat also returns the input's exact
+    per-(n, c) max |x| (channel extremes of its statistics pass); the shortcut's input quant from it
+    (qd_act_apply_cat_nhwc) equals qd_act_quant_cat_nhwc (its own column-max pass) bit for bit, and
+    the GroupNorm output is unchanged."""
+    k = K()
+    g = torch.Generator().manual_seed(hw + c1)
+    n = 2
+    a = (torch.randn(n, hw, c1, generator=g) * 2).half().to(dev)
+    b2 = (torch.randn(n, hw, c2, generator=g) * 3).half().to(dev)
+    b2[1, :, 7] = 0  # an all-zero channel (amax clamp)
+    c = c1 + c2
+    gam = (1 + 0.1 * torch.randn(c, generator=g)).half().to(dev)
+    bet = (0.1 * torch.randn(c, generator=g)).half().to(dev)
+    y0 = k.groupnorm_nhwc(a, 32, 1e-5, gam, bet, silu=True, q_bits=8, x2=b2)
+    y1, xam = k.groupnorm_nhwc(a, 32, 1e-5, gam, bet, silu=True, q_bits=8, x2=b2, want_xamax=True)
+    assert torch.equal(y0, y1)
+    exact = torch.cat([a, b2], -1).float().abs().amax(1).reshape(-1)
+    assert torch.equal(xam, exact)
+    assert torch.equal(k.act_apply_cat_nhwc(a, b2, 8, xam), k.act_quant_cat_nhwc(a, b2, 8))
+
+
 @pytest.mark.parametrize("rows,c", [(77, 320), (4096, 640), (33, 1280), (5, 2048), (8195, 320), (20001, 160), (3, 3072)])
 def test_layernorm(rows, c, dev):
     k = K()
