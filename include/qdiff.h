@@ -124,6 +124,7 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
                                 sum of squared deviations from it, min, max), fp32 - the consuming
                                 GroupNorm (qd_groupnorm_part) needs no statistics pass over the
                                 tensor; rows_per_sample % 64 == 0, never ping-pong tiles */
+#define QD_EPI_LN 512        /* (set by qd_linear_ln / qd_linear_i8_ln) */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
@@ -206,6 +207,24 @@ int qd_quant_samples_i8_amax(const void* x, int n, long per_sample, const float*
 int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
                  const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
                  int rows_per_sample, float* ws, long ws_elems, void* stream);
+/* Row-complete LayerNorm epilogue (diffusers BasicTransformerBlock: attn.to_out + residual ->
+ * norm2 / norm3): y = the qd_linear_fwd / qd_linear_i8 output with QD_EPI_RESIDUAL (epi must
+ * hold it; no amax / GEGLU / GELU-tanh), AND LayerNorm(y) over each row (gamma / beta fp16 [N],
+ * eps) in the same launch - one block owns whole rows (N == 320: the 128 x 320 tiles, unsplit), so
+ * the LayerNorm reads the final tile from LDS instead of a second pass over y.  ln_y8 == NULL:
+ * ln_y [M][N] fp16 = qd_layernorm's value; else ln_y8 [M][N] int8 + ln_sa8 [M] fp32 = qd_layernorm_i8's
+ * codes and scales (the consumer linear's per-token operand).  Bit-identical to the unfused
+ * qd_linear_fwd / qd_linear_i8 + qd_layernorm(_i8) sequence (same per-lane chunk sums and lane
+ * butterfly as the grouped-row LayerNorm).  Returns QD_ERR_ARG for any other N (callers fall back). */
+int qd_linear_ln(const void* x, int M, int K, int lda, const void* w, int wfmt, const void* wscale,
+                 const void* wscale_t, int group, const void* bias, const void* residual, void* y, int N, int ldy,
+                 int epi, const void* ln_gamma, const void* ln_beta, float ln_eps, void* ln_y, int8_t* ln_y8,
+                 float* ln_sa8, float* ws, long ws_elems, void* stream);
+int qd_linear_i8_ln(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                    const void* bias, const void* residual, void* y, int N, int ldy, int epi, const void* ln_gamma,
+                    const void* ln_beta, float ln_eps, void* ln_y, int8_t* ln_y8, float* ln_sa8, void* stream);
+/* 1 when qd_linear_ln / qd_linear_i8_ln take this N (a row-complete tile exists), else 0. */
+int qd_linear_ln_ok(int N);
 /* NHWC implicit-GEMM conv on int8 codes: x_i8 [N, H, W, Ci_pad] (Ci_pad % 64 == 0), one scale
  * per sample sa[N]; w_i8 [Co][kh][kw][Ci_pad], sw[Co]; geometry / epilogue as qd_conv2d_fwd.
  * QD_EPI_CADD: + cadd[n * cadd_ld + co] after the residual (cadd_ld <= 0: Co; 16-B aligned rows).  QD_EPI_GNSTATS:

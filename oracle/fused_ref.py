@@ -266,6 +266,17 @@ def layernorm_fq(a, outs):
     return [Out("t", t, ulps=0), _ln(t, a["eps"], a["gamma"], a["beta"])]
 
 
+def linear_ln(a, outs):
+    """kernels.linear_ln -> (y, h): y as linear() with the residual; h = LayerNorm of y - of the
+    launch's own y when given (outs[0]: the tensor a separate LayerNorm launch would read, so the
+    check isolates the normalisation), else of the reference y.  fp16 h only: the int8 codes form
+    (i8_out) is pinned bit-exactly against the two-launch sequence by tests/test_gpu_int8.py."""
+    la = dict(x2d=a["x2d"], weight=a["weight"], wfmt="f16", bias=a.get("bias"), residual=a["residual"])
+    res = linear(la, None)
+    y_in = outs[0] if outs else res[0].ref
+    return res + [_ln(y_in, a["eps"], a["gamma"], a["beta"])]
+
+
 def attention(a, outs):
     """kernels.attention: SDPA (fp32, one rounding); flash-style P in fp16: 4 ulp + 1e-3."""
     q, k, v, heads = a["q"], a["k"], a["v"], a["heads"]
@@ -309,6 +320,7 @@ def silu(a, outs):
 # launch name -> (oracle, output names in the wrapper's return order)
 LAUNCHES = {
     "linear": linear,
+    "linear_ln": linear_ln,
     "conv2d_nhwc": conv2d_nhwc,
     "fq_finalize": fq_finalize,
     "groupnorm_nhwc": groupnorm_nhwc,

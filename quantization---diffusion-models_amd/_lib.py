@@ -79,6 +79,9 @@ SIGNATURES = {
     "qd_quant_samples_i8": [P, I, ctypes.c_long, P, P, P, I, P],
     "qd_quant_samples_i8_amax": [P, I, ctypes.c_long, P, I, P, P, P],
     "qd_linear_i8": [P, P, I, I, I, P, P, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
+    "qd_linear_ln": [P, I, I, I, P, I, P, P, I, P, P, P, I, I, I, P, P, F, P, P, P, P, ctypes.c_long, P],
+    "qd_linear_i8_ln": [P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, P, P, P, P],
+    "qd_linear_ln_ok": [I],
     "qd_conv2d_i8": [P, P, I, I, I, I, I, P, P, I, I, I, I, I, I, P, P, P, I, P, P, I, P, P, ctypes.c_long, P],
     "qd_groupnorm_part": [P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, P, P, P, P],
     "qd_quant_samples_i8_cat": [P, P, I, I, I, ctypes.c_long, P, P, P, P],

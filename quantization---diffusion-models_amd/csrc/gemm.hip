@@ -86,6 +86,15 @@ struct GemmArgs {
   // tiles fastest (one XCD's blocks share a weight slice) - set by the host when the weights are
   // the larger operand (the low UNet levels: 1280 x 11520 weights against 2048 x 1280 activations)
   int mfast;
+  // row-complete LayerNorm epilogue (QD_EPI_LN; BN == N tiles, unsplit, residual path): LayerNorm of
+  // each final output row read back from the LDS tile - fp16 into ln_y [M][N], or the int8 codes
+  // ln_y8 [M][N] + per-row scales ln_sa8 [M] (norm.hip k_ln_rows MODE 0 / 1 arithmetic)
+  const f16* ln_g;
+  const f16* ln_b;
+  float ln_eps;
+  f16* ln_y;
+  int8_t* ln_y8;
+  float* ln_sa8;
 };
 
 constexpr int BK = 64;
@@ -389,6 +398,14 @@ __device__ __forceinline__ void i8_scale(const GemmArgs& p, const i32x4 (&acc)[T
 // slots of the amax combine (WGM x BN floats, WGM <= 8)
 constexpr int epi_lds_halves(int bm, int bn) { return bm * (bn + 8) + 16 * bn; }
 
+// grouped-row LayerNorm geometry of a row of BN columns (norm.hip ln_rows_geom): LPR lanes per row,
+// P 16-B chunks per lane (lane l owns chunks l, l + LPR, ...); 0 = no such geometry
+constexpr int ln_lpr(int bn) {
+  return bn % 8 ? 0 : (bn / 8) % 8 == 0 && bn / 64 <= 5 ? 8 : (bn / 8) % 16 == 0 && bn / 128 <= 5 ? 16 :
+                      (bn / 8) % 32 == 0 && bn / 256 <= 5 ? 32 : (bn / 8) % 64 == 0 && bn / 512 <= 5 ? 64 : 0;
+}
+constexpr int ln_per(int bn) { return ln_lpr(bn) ? bn / 8 / ln_lpr(bn) : 0; }
+
 template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM][TN], f16* smem, int m0, int n0,
                                               int wm0, int wn0, int split) {
@@ -427,6 +444,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // goes there first), the coalesced pass adds the residual and writes the final tile back to
     // LDS, and the slot moments are reduced from there
     const bool gn = (p.epi & QD_EPI_GNSTATS) && p.gnp && !geglu && !gtanh;
+    // row-complete LayerNorm (host: BN == N, n0 == 0, residual, no amax): the final tile is written
+    // back to LDS by the coalesced pass like the GroupNorm slots' and normalised row by row from there
+    constexpr bool LN_OK = BN == 320 && ln_lpr(BN) != 0;  // (the tiles ln_var plans; others compile it out)
+    const bool ln = LN_OK && (p.epi & QD_EPI_LN) && !geglu && !gtanh;
     const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd && !geglu && !gtanh;
     const bool fres = post || (has_res && cadd);
     const f16* const cadd_row = cadd ? p.cadd + (long)(min(m0, p.M - 1) / p.rows_per_sample) * p.cadd_ld : nullptr;
@@ -594,6 +615,79 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           dst[j] = make_float4((float)sh[j] + s1[j] * (1.0f / 64.0f), s2[j] - s1[j] * s1[j] * (1.0f / 64.0f), mn[j], mx[j]);
       }
     };
+    // LayerNorm rows from the final tile in LDS: a wave takes 64 / LPR rows at a time, LPR lanes per
+    // row, lane lr owning chunks lr, lr + LPR, ... - k_ln_rows' lane map, sums and butterflies, so
+    // the output is bit-identical to the separate LayerNorm launch over y
+    auto ln_rows = [&]() {
+      constexpr int LPR = LN_OK ? ln_lpr(BN) : 8, P = LN_OK ? ln_per(BN) : 1, RPW = 64 / LPR, NWV = NT / 64;
+      const int wv = threadIdx.x >> 6, lr = lane % LPR, rw = lane / LPR;
+      f16x8 g[P], b[P];
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        g[i] = *reinterpret_cast<const f16x8*>(p.ln_g + (lr + i * LPR) * 8);
+        b[i] = *reinterpret_cast<const f16x8*>(p.ln_b + (lr + i * LPR) * 8);
+      }
+      const float inv_c = (float)BN;
+      for (int r0 = wv * RPW; r0 < BM; r0 += NWV * RPW) {
+        const int row = r0 + rw;
+        const long m = (long)m0 + row;
+        const bool ok = m < p.M;
+        f16x8 v[P];
+#pragma unroll
+        for (int i = 0; i < P; ++i) v[i] = *reinterpret_cast<const f16x8*>(ct + row * LP + (lr + i * LPR) * 8);
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sm += (float)v[i][e];
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+        const float mean = sm / inv_c;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float a = (float)v[i][e] - mean;
+            q = fmaf(a, a, q);
+          }
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        const float rstd = 1.0f / sqrtf(q / inv_c + p.ln_eps);
+        f16x8 o8[P];
+        float mx = 0.f;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            o8[i][e] = to_f16(fmaf(((float)v[i][e] - mean) * rstd, (float)g[i][e], (float)b[i][e]));
+            mx = fmaxf(mx, fabsf((float)o8[i][e]));
+          }
+        if (p.ln_y8) {
+#pragma unroll
+          for (int o = LPR / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+          const float s8 = fq_scale(mx, 127);
+          const double r8 = rcp_exact(s8);
+          if (ok && lr == 0) p.ln_sa8[m] = s8;
+#pragma unroll
+          for (int i = 0; i < P; ++i) {
+            unsigned lo = 0, hi = 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const f16 tq = (f16)(float)((double)(float)o8[i][e] * r8);
+              const unsigned qv = (unsigned)(uint8_t)(int8_t)__builtin_rintf((float)tq);
+              if (e < 4) lo |= qv << (8 * e);
+              else hi |= qv << (8 * (e - 4));
+            }
+            if (ok) *reinterpret_cast<uint2*>(p.ln_y8 + m * BN + (lr + i * LPR) * 8) = make_uint2(lo, hi);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < P; ++i)
+            if (ok) *reinterpret_cast<f16x8*>(p.ln_y + m * BN + (lr + i * LPR) * 8) = o8[i];
+        }
+      }
+    };
     if (pre_res) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -605,13 +699,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           f16x8 v = *reinterpret_cast<const f16x8*>(ct + row * LP + c * 8);
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i][r]);
-          if (gn) *reinterpret_cast<f16x8*>(ct + row * LP + c * 8) = v;  // (this thread's own element)
+          if (gn || ln) *reinterpret_cast<f16x8*>(ct + row * LP + c * 8) = v;  // (this thread's own element)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, m0 + row < p.M ? (int)off : (int)OOB, 0, 0);
         }
       }
-      if (gn) {
-        __syncthreads();
-        gn_slots();
+      if (gn || ln) __syncthreads();
+      if (gn) gn_slots();
+      if constexpr (LN_OK) {
+        if (ln) ln_rows();
       }
       return;
     }
@@ -2318,6 +2413,9 @@ static constexpr DmaVar kDmaC[] = {
     // epilogue (GELU VALU, output stores) can run beside the other block's MFMAs
     {128, 256, 2, 2, 3, 0, 1.00, 32},  // 16
     {256, 128, 2, 2, 3, 0, 1.00, 32},  // 17
+    // row-complete LayerNorm epilogue (QD_EPI_LN, N = 320): 64-row tiles, 4 waves, 72 KB - two blocks
+    // per CU, so one block's epilogue (residual, y, LayerNorm) runs beside the other's K loop
+    {64, 320, 1, 4, 3, 0, 1.00, 32},   // 18
 };
 static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
 static int g_split = 0;   // with a forced DMA / ping-pong / halo variant: exact split-K count (0 = the fit rule)
@@ -2423,7 +2521,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
         }
       }
     }
-  } else if (g_force >= 100 && g_force < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0])) &&
+  } else if (g_force >= 100 && g_force < 118 &&  // (118: the LayerNorm epilogue's tile, ln_var only)
              (!quant_w || (w4 && w4g % kDmaC[g_force - 100].bkt == 0 && kDmaC[g_force - 100].pipe == 0))) {
     const DmaVar& d = kDmaC[g_force - 100];
     const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
@@ -2517,6 +2615,9 @@ static void launch_dma(const GemmArgs& p, int var, hipStream_t st, int fmt = QD_
     case 14: launch_dma_v<14, AMODE, SPLIT>(p, st); break;
     case 16: launch_dma_v<16, AMODE, SPLIT>(p, st); break;
     case 17: launch_dma_v<17, AMODE, SPLIT>(p, st); break;
+    case 18:
+      if constexpr (AMODE == AM_LINEAR && !SPLIT) launch_dma_v<18, AMODE, SPLIT>(p, st);
+      break;
     default: launch_dma_v<15, AMODE, SPLIT>(p, st); break;
   }
 }
@@ -2752,8 +2853,26 @@ static int block_order(const GemmArgs& p, bool linear, double wbytes, double aby
 
 static long split_ws_elems(const Plan& pl, int M, int N) { return pl.splits > 1 ? (long)pl.splits * M * N : 0; }
 
+// row-complete LayerNorm epilogue (QD_EPI_LN): an LDS-DMA variant whose tile is the whole row -
+// 64 x 320 (variant 18, two blocks per CU) or 128 x 320 (fp16: variant 1, two 64-deep stages, or
+// 12, four 32-deep; int8: 12); a forced variant (qd_gemm_force 100 + v) is taken when it is one of
+// them; -1 = no row-complete tile for N
+static int ln_var(int N, bool i8) {
+  if (N != 320) return -1;
+  const int fv = g_force - 100;
+  if (fv == 18 || fv == 12 || (!i8 && fv == 1)) return fv;
+  return 18;
+}
+
 template <int AMODE>
 static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t st) {
+  if (p.epi & QD_EPI_LN) {  // (host checks: F16 weights, N with a row-complete tile)
+    p.splits = 1;
+    p.kps = p.K;
+    p.mfast = 0;
+    launch_dma<AMODE, false>(p, ln_var(p.N, false), st, fmt);
+    return;
+  }
   const bool post = (p.epi & QD_EPI_AMAX_POST) != 0;
   const int w4g = fmt == QD_WFMT_I4 && p.bscale_t != nullptr && AMODE == AM_LINEAR ? p.group : 0;
   Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
@@ -2833,10 +2952,44 @@ extern "C" long qd_gemm_workspace(int M, int N, int K, int wfmt, int group, int 
   return split_ws_elems(pl, M, N);
 }
 
-extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
-                             const void* wscale, const void* wscale_t, int group, const void* bias,
-                             const void* residual, void* y, int N, int ldy, int epi, float* amax,
-                             int rows_per_sample, float* ws, long ws_elems, void* stream) {
+struct LnArgs {
+  const void *g, *b;
+  float eps;
+  void* y;
+  int8_t* y8;
+  float* sa8;
+};
+
+static int check_ln(const GemmArgs& p, const LnArgs& ln) {
+  QD_REQUIRE(ln_var(p.N, false) >= 0, "row-complete LayerNorm epilogue: no tile for this N (qd_linear_ln_ok)");
+  QD_REQUIRE((p.epi & QD_EPI_RESIDUAL) && !(p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU | QD_EPI_GELU_TANH)),
+             "row-complete LayerNorm epilogue: residual, no amax / GEGLU / GELU-tanh");
+  QD_REQUIRE(p.ldy == p.N, "row-complete LayerNorm epilogue: dense output (ldy == N)");
+  QD_REQUIRE(ln.g && ln.b && (reinterpret_cast<uintptr_t>(ln.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(ln.b) & 15) == 0,
+             "LayerNorm gamma / beta: 16-B aligned fp16 [N]");
+  QD_REQUIRE(ln.y8 ? (ln.sa8 && (reinterpret_cast<uintptr_t>(ln.y8) & 7) == 0)
+                   : (ln.y && (reinterpret_cast<uintptr_t>(ln.y) & 15) == 0),
+             "LayerNorm output: ln_y (16-B aligned fp16) or ln_y8 (8-B aligned) + ln_sa8");
+  return 0;
+}
+
+static void set_ln(GemmArgs& p, const LnArgs& ln) {
+  p.epi |= QD_EPI_LN;
+  p.ln_g = (const f16*)ln.g;
+  p.ln_b = (const f16*)ln.b;
+  p.ln_eps = ln.eps;
+  p.ln_y = (f16*)ln.y;
+  p.ln_y8 = ln.y8;
+  p.ln_sa8 = ln.sa8;
+}
+
+extern "C" int qd_linear_ln_ok(int N) { return ln_var(N, false) >= 0 ? 1 : 0; }
+
+static int linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt, const void* wscale,
+                      const void* wscale_t, int group, const void* bias, const void* residual, void* y, int N,
+                      int ldy, int epi, float* amax, int rows_per_sample, float* ws, long ws_elems, void* stream,
+                      const LnArgs* ln) {
+  QD_REQUIRE(!(epi & QD_EPI_LN), "QD_EPI_LN is set by qd_linear_ln");
   GemmArgs p{};
   p.a = (const f16*)x;
   p.lda = lda;
@@ -2857,6 +3010,11 @@ extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w
   p.epi = epi;
   int rc = check_common(p, wfmt);
   if (rc) return rc;
+  if (ln) {
+    QD_REQUIRE(wfmt == QD_WFMT_F16, "row-complete LayerNorm epilogue: fp16 weights (the dequantized buffer)");
+    if ((rc = check_ln(p, *ln))) return rc;
+    set_ln(p, *ln);
+  }
   QD_REQUIRE(lda >= K && lda % 8 == 0 && ldy >= ((epi & QD_EPI_GEGLU) ? N / 2 : N), "bad leading dimensions");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "x must be 16-B aligned");
   QD_REQUIRE((double)M * lda * 2 < 2147483648.0, "activation exceeds the 2 GiB buffer-addressing range");
@@ -2866,11 +3024,28 @@ extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
   static const bool gemv_off = getenv("QD_NO_GEMV") != nullptr;  // A/B switch: tile GEMM for every M
-  const int cpl = gemv_off ? 0 : gemv_cpl(p);
+  const int cpl = gemv_off || ln ? 0 : gemv_cpl(p);
   if (cpl) launch_gemv(p, wfmt, cpl, S(stream));
   else run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
+                             const void* wscale, const void* wscale_t, int group, const void* bias,
+                             const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                             int rows_per_sample, float* ws, long ws_elems, void* stream) {
+  return linear_fwd(x, M, K, lda, w, wfmt, wscale, wscale_t, group, bias, residual, y, N, ldy, epi, amax,
+                    rows_per_sample, ws, ws_elems, stream, nullptr);
+}
+
+extern "C" int qd_linear_ln(const void* x, int M, int K, int lda, const void* w, int wfmt, const void* wscale,
+                            const void* wscale_t, int group, const void* bias, const void* residual, void* y, int N,
+                            int ldy, int epi, const void* ln_gamma, const void* ln_beta, float ln_eps, void* ln_y,
+                            int8_t* ln_y8, float* ln_sa8, float* ws, long ws_elems, void* stream) {
+  const LnArgs ln{ln_gamma, ln_beta, ln_eps, ln_y, ln_y8, ln_sa8};
+  return linear_fwd(x, M, K, lda, w, wfmt, wscale, wscale_t, group, bias, residual, y, N, ldy, epi, nullptr, 0, ws,
+                    ws_elems, stream, &ln);
 }
 
 extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt,
@@ -2970,6 +3145,9 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
     case 15: launch_i8_v<15, AMODE, SPLIT>(p, st); break;
     case 16: launch_i8_v<16, AMODE, SPLIT>(p, st); break;
     case 17: launch_i8_v<17, AMODE, SPLIT>(p, st); break;
+    case 18:
+      if constexpr (AMODE == AM_LINEAR && !SPLIT) launch_i8_v<18, AMODE, SPLIT>(p, st);
+      break;
     default: launch_i8_v<11, AMODE, SPLIT>(p, st); break;
   }
 }
@@ -3060,6 +3238,13 @@ static bool epi_gn(int epi) { return (epi & (QD_EPI_GNSTATS | QD_EPI_CADD)) != 0
 
 template <int AMODE>
 static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
+  if (p.epi & QD_EPI_LN) {
+    p.splits = 1;
+    p.kps = p.K;
+    p.mfast = 0;
+    launch_i8<AMODE, false>(p, ln_var(p.N, true), st);
+    return;
+  }
   const bool post = (p.epi & QD_EPI_AMAX_POST) != 0, gn = epi_gn(p.epi);
   Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post,
                     gn);
@@ -3144,9 +3329,10 @@ extern "C" long qd_gemm_i8_workspace(int M, int N, int K, int rows_per_sample, i
   return split_ws_elems(pl, M, N);
 }
 
-extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
-                            const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
-                            int rows_per_sample, float* ws, long ws_elems, void* stream) {
+static int linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                     const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                     int rows_per_sample, float* ws, long ws_elems, void* stream, const LnArgs* ln) {
+  QD_REQUIRE(!(epi & QD_EPI_LN), "QD_EPI_LN is set by qd_linear_i8_ln");
   QD_REQUIRE(K % 64 == 0 && K > 0, "int8 GEMM needs K % 64 == 0");
   QD_REQUIRE(lda >= K && lda % 16 == 0, "int8 GEMM needs lda >= K, lda % 16 == 0");
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
@@ -3171,6 +3357,10 @@ extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int ld
   p.i8 = 1;
   int rc = check_i8(p);
   if (rc) return rc;
+  if (ln) {
+    if ((rc = check_ln(p, *ln))) return rc;
+    set_ln(p, *ln);
+  }
   QD_REQUIRE(ldy >= ((epi & QD_EPI_GEGLU) ? N / 2 : N), "bad ldy");
   QD_REQUIRE((double)M * lda < 2147483648.0, "activation exceeds the 2 GiB buffer-addressing range");
   if (M == 0) return 0;
@@ -3181,6 +3371,21 @@ extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int ld
   run_i8<AM_LINEAR>(p, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                            const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
+                            int rows_per_sample, float* ws, long ws_elems, void* stream) {
+  return linear_i8(x, sa, M, K, lda, w, sw, bias, residual, y, N, ldy, epi, amax, rows_per_sample, ws, ws_elems,
+                   stream, nullptr);
+}
+
+extern "C" int qd_linear_i8_ln(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                               const void* bias, const void* residual, void* y, int N, int ldy, int epi,
+                               const void* ln_gamma, const void* ln_beta, float ln_eps, void* ln_y, int8_t* ln_y8,
+                               float* ln_sa8, void* stream) {
+  const LnArgs ln{ln_gamma, ln_beta, ln_eps, ln_y, ln_y8, ln_sa8};
+  return linear_i8(x, sa, M, K, lda, w, sw, bias, residual, y, N, ldy, epi, nullptr, 0, nullptr, 0, stream, &ln);
 }
 
 extern "C" int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w, int ci, int ci_pad, const void* wt,

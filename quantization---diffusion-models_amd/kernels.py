@@ -442,6 +442,97 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     return out
 
 
+# qd_gemm_force ids of the row-complete tiles the LayerNorm epilogue runs on: 64 x 320 with two
+# blocks per CU (118), 128 x 320 with two 64-deep LDS stages (101, fp16 only) / four 32-deep (112)
+LN_VARIANTS = (118, 101, 112)
+LN_I8_VARIANTS = (118, 112)
+_LN_OK = {}
+
+
+def linear_ln_ok(n):
+    """True when linear_ln / linear_i8_ln take an output width of n (a row-complete tile exists)."""
+    if n not in _LN_OK:
+        _LN_OK[n] = bool(_lib.load().qd_linear_ln_ok(n))
+    return _LN_OK[n]
+
+
+def _ln_outs(M, N, i8_out, device, alloc=None):
+    alloc = alloc or _empty  # (tuning scratch: torch.empty - outside the step arena's allocation sequence)
+    if i8_out:
+        return None, alloc((M, N), torch.int8, device), alloc((M,), torch.float32, device)
+    return alloc((M, N), torch.float16, device), None, None
+
+
+def linear_ln(x2d, weight, residual, gamma, beta, eps, bias=None, i8_out=False):
+    """(y, h) in ONE launch: y = linear(x2d, weight, "f16", bias=bias, residual=residual) and
+    h = layernorm(y, eps, gamma, beta) - or, i8_out, h = layernorm_i8(y, ...) = (codes, scales) -
+    bit-identical to the two calls (diffusers attn.to_out + residual -> norm2 / norm3).  weight:
+    fp16 [N, K] (a quantized layer's dequantized buffer); linear_ln_ok(N) must hold."""
+    if x2d.dtype != torch.float16 or not x2d.is_cuda or x2d.dim() != 2 or x2d.stride(1) != 1:
+        raise ValueError("x must be a 2-D fp16 HIP tensor with unit column stride")
+    _chk(weight, "weight")
+    _chk(residual, "residual")
+    M, K = x2d.shape
+    N = weight.shape[0]
+    out = _empty((M, N), torch.float16, x2d.device)
+    h, h8, sa8 = _ln_outs(M, N, i8_out, x2d.device)
+    epi = (EPI_BIAS if bias is not None else 0) | EPI_RESIDUAL
+
+    def launch(c, y, hh, hh8, ss8):
+        _force(c if _OVERRIDE is None else _OVERRIDE)
+        try:
+            _lib.call("qd_linear_ln", _p(x2d), M, K, x2d.stride(0), _p(weight), WFMT["f16"], None, None, 0, _p(bias),
+                      _p(residual), _p(y), N, N, epi, _p(gamma), _p(beta), float(eps), _p(hh), _p(hh8), _p(ss8),
+                      None, 0, _stream())
+        finally:
+            _force(-1)
+
+    key = ("linear_ln", M, N, K, x2d.stride(0), epi, bool(i8_out))
+    _USED.add(key)
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        th, th8, ts8 = _ln_outs(M, N, i8_out, x2d.device, lambda sh, dt, d: torch.empty(sh, dtype=dt, device=d))
+        c = _choose(key, list(LN_VARIANTS), lambda c: launch(c, ty, th, th8, ts8))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else -1, out, h, h8, sa8)
+    return out, ((h8, sa8) if i8_out else h)
+
+
+def linear_i8_ln(xq, sa, wq, sw, residual, gamma, beta, eps, bias=None, i8_out=True):
+    """linear_ln on int8 codes: y = linear_i8(xq, sa, wq, sw, bias=bias, residual=residual) and its
+    LayerNorm h (fp16, or (codes, scales) with i8_out) in one launch, bit-identical to the two calls."""
+    if xq.dtype != torch.int8 or wq.dtype != torch.int8 or not xq.is_cuda:
+        raise ValueError("int8 GEMM operands must be int8 HIP tensors")
+    if xq.dim() != 2 or xq.stride(1) != 1 or not wq.is_contiguous():
+        raise ValueError("xq must be 2-D with unit column stride, wq contiguous")
+    _chk(residual, "residual")
+    M, Kd = xq.shape
+    N = wq.shape[0]
+    out = _empty((M, N), torch.float16, xq.device)
+    h, h8, sa8 = _ln_outs(M, N, i8_out, xq.device)
+    epi = (EPI_BIAS if bias is not None else 0) | EPI_RESIDUAL
+
+    def launch(c, y, hh, hh8, ss8):
+        _force(c if _OVERRIDE is None else _OVERRIDE)
+        try:
+            _lib.call("qd_linear_i8_ln", _p(xq), _p(sa), M, Kd, xq.stride(0), _p(wq), _p(sw), _p(bias), _p(residual),
+                      _p(y), N, N, epi, _p(gamma), _p(beta), float(eps), _p(hh), _p(hh8), _p(ss8), _stream())
+        finally:
+            _force(-1)
+
+    key = ("linear_i8_ln", M, N, Kd, xq.stride(0), epi, bool(i8_out))
+    _USED.add(key)
+    if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
+        ty = torch.empty_like(out)
+        th, th8, ts8 = _ln_outs(M, N, i8_out, xq.device, lambda sh, dt, d: torch.empty(sh, dtype=dt, device=d))
+        c = _choose(key, list(LN_I8_VARIANTS), lambda c: launch(c, ty, th, th8, ts8))
+    else:
+        c = _TUNE.get(key)
+    launch(c if c is not None else -1, out, h, h8, sa8)
+    return out, ((h8, sa8) if i8_out else h)
+
+
 def geglu_interleave_rows(n2, device):
     """Row permutation for the fused GEGLU epilogue: 16-row blocks [hidden b | gate b]."""
     half = n2 // 2

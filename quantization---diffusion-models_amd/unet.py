@@ -909,14 +909,13 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
         h = ln(blk.norm1, i8_qkv)
     q, k, v = self_attn_qkv(a1, h, n, s)
     o = K.attention(q, k, v, a1.heads)
-    t = run_linear(a1.to_out[0], o.view(-1, c), residual=t)
     a2 = blk.attn2
-    h = ln(blk.norm2, lin_i8(a2.to_q) and a2.to_q.output_quant_name == "None")
+    t, h = _out_ln(a1.to_out[0], o.view(-1, c), t, blk.norm2, lin_i8(a2.to_q) and a2.to_q.output_quant_name == "None")
     q = run_linear(a2.to_q, h).view(n, s, c)
     k, v = ctx_kv[id(a2)]
     o = K.attention(q, k, v, a2.heads)
-    t = run_linear(a2.to_out[0], o.view(-1, c), residual=t)
-    h = ln(blk.norm3, lin_i8(blk.ff.net[0].proj) and blk.ff.net[0].proj.output_quant_name == "None")
+    pj = blk.ff.net[0].proj
+    t, h = _out_ln(a2.to_out[0], o.view(-1, c), t, blk.norm3, lin_i8(pj) and pj.output_quant_name == "None")
     g = ff_geglu(blk.ff.net[0].proj, h)
     fo = blk.ff.net[2]
     if want_amax and lin_i8(fo) and fo.output_quant_name == "None" and g.shape[0] >= I8_MIN_ROWS:
@@ -938,6 +937,30 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
     return run_linear(fo, g, residual=t)
 
 
+def _out_ln(layer, x2d, t, norm, i8_next):
+    """(t', h): t' = run_linear(layer, x2d, residual=t) (attn.to_out + the residual stream) and
+    h = norm(t') - the per-token int8 codes of the consumer linear when i8_next - as ONE launch
+    (kernels.linear_ln / linear_i8_ln: the GEMM's row-complete tile normalises its own rows) where a
+    row-complete tile takes the width, else the linear and the LayerNorm launches; bit-identical."""
+    big = t.shape[0] >= I8_MIN_ROWS
+    i8h = bool(i8_next) and big
+    g, b = _f16(norm.weight), _f16(norm.bias)
+    if LN_EPI and big and K.linear_ln_ok(t.shape[1]):
+        if lin_i8(layer) and layer.output_quant_name == "None":  # int8-MFMA linear (run_linear's i8 path)
+            wq, sw = layer.i8_operand()
+            xq, sa = K.quant_rows_i8(x2d)
+            return K.linear_i8_ln(xq, sa, wq, sw, t, g, b, norm.eps, bias=layer.bias, i8_out=i8h)
+        op = _fake_quant_gemm_operand(layer)
+        if op is not None:
+            w, fmt, _, _, wf = op
+            w16 = w if fmt == "f16" else wf
+            if w16 is not None:
+                bias = layer.bias if isinstance(layer, WxAxLinear) else _f16(layer.bias)
+                return K.linear_ln(x2d, w16, t, g, b, norm.eps, bias=bias, i8_out=i8h)
+    t = run_linear(layer, x2d, residual=t)
+    return t, (K.layernorm_i8 if i8h else K.layernorm)(t, norm.eps, g, b)
+
+
 # the post-residual amax epilogue runs unsplit (no split-K slabs): used where M is large enough
 # that the GEMM would not split anyway (the 64x64 and 32x32 levels of SD1.5 at CFG batch 8)
 AMAX_POST_MIN_ROWS = 8192
@@ -945,6 +968,7 @@ XAMAX_GN = not os.environ.get("QD_NO_XAMAX_GN")  # A/B switch: the concat shortc
 AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
 LN_FQ = not os.environ.get("QD_NO_LN_FQ")  # A/B switch: proj_in finalize as its own pass before norm1
 I8_AMAX_FUSE = not os.environ.get("QD_NO_I8_AMAX_FUSE")  # A/B switch: proj_out's int8 scale by its own pass
+LN_EPI = not os.environ.get("QD_NO_LN_EPI")  # A/B switch: to_out + residual and norm2 / norm3 as two launches
 
 
 def _fake_quant_gemm_operand(layer):

@@ -172,8 +172,8 @@ def test_c2_fused_launch_sequence_teacher_forced(c2):
             args = {k: cpu(v) for k, v in bound.arguments.items() if k != "out"}
             ret = fn(*a, **kw)
             torch.cuda.synchronize()
-            outs = FR.LAUNCHES[name](args, None)
             rets = list(ret) if isinstance(ret, tuple) else [ret]
+            outs = FR.LAUNCHES[name](args, [cpu(r) for r in rets])
             got = {}
             i = 0
             for o in outs:
@@ -205,7 +205,7 @@ def test_c2_fused_launch_sequence_teacher_forced(c2):
     print(f"[c2] fused launches checked in {time.time() - t0:.1f}s: {dict(sorted(counts.items()))}; "
           f"largest |err| / bound: " + ", ".join(f"{k} {v:.2f}" for k, v in top), flush=True)
     # every fused form the bench's step runs at this workload was exercised
-    for name in ("linear", "conv2d_nhwc", "groupnorm_fin", "groupnorm_nhwc", "layernorm", "layernorm_fq",
+    for name in ("linear", "linear_ln", "conv2d_nhwc", "groupnorm_fin", "groupnorm_nhwc", "layernorm", "layernorm_fq",
                  "attention"):
         assert counts.get(name, 0) > 0, (name, counts)
     assert counts["attention"] == 32, counts

@@ -551,3 +551,35 @@ def test_int8_codes_survive_device_moves():
     conv = model.pipeline.unet.down_blocks[0].resnets[0].conv1
     conv.weight.mul_(1.0)
     assert conv.i8_operand() is None and conv.quantise_act and conv.output_quant_name == "per_channel"
+
+
+@pytest.mark.parametrize("M,Kd", [(4096, 320), (300, 320), (77, 1280)])
+@pytest.mark.parametrize("i8_out", [True, False])
+@pytest.mark.parametrize("variant", [None, 118, 112])
+def test_linear_i8_ln_bit_exact(M, Kd, i8_out, variant, dev):
+    """int8 to_out + residual with the next LayerNorm in its epilogue: y bit-exact to the int8 oracle,
+    h bit-identical to layernorm_i8 / layernorm of y (the unfused launches)."""
+    k = K()
+    N = 320
+    rng = np.random.default_rng(M + Kd + 7)
+    x = rng.standard_normal((M, Kd)).astype(np.float16)
+    w = (rng.standard_normal((N, Kd)) / Kd ** 0.5).astype(np.float16)
+    b = rng.standard_normal(N).astype(np.float16)
+    res = (rng.standard_normal((M, N)) * 3).astype(np.float16)
+    gamma = (1 + 0.1 * rng.standard_normal(N)).astype(np.float16)
+    beta = (0.1 * rng.standard_normal(N)).astype(np.float16)
+    xq, sa = R.quant_rows_i8(x)
+    wq, sw = R.weight_rows_i8(w)
+    ref = R.linear_i8(xq, sa, wq, sw, b, res)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    k.force_gemm(variant)
+    try:
+        y, h = k.linear_i8_ln(t(xq), t(sa), t(wq), t(sw), t(res), t(gamma), t(beta), 1e-5, bias=t(b), i8_out=i8_out)
+    finally:
+        k.force_gemm(None)
+    assert np.array_equal(_bits(y.cpu().numpy()), _bits(ref))
+    if i8_out:
+        q0, s0 = k.layernorm_i8(y, 1e-5, t(gamma), t(beta))
+        assert torch.equal(h[0], q0) and torch.equal(h[1], s0)
+    else:
+        assert torch.equal(h, k.layernorm(y, 1e-5, t(gamma), t(beta)))

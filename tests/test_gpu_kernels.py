@@ -843,3 +843,34 @@ def test_cfg_pndm_step_bit_exact_vs_torch_pndm(dev):
         rl = ref.step(u + 7.5 * (cc - u), int(ts[i]), rl)
         got = k.nhwc_to_nchw(lat, c).cpu()
         assert same_bits(got.numpy(), rl.numpy()), (i, (got.float() - rl.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("M,Kd", [(4096, 320), (300, 320), (77, 1280), (32768, 320)])
+@pytest.mark.parametrize("variant", [None, 118, 101, 112])
+@pytest.mark.parametrize("bias,i8_out", [(True, False), (False, False), (True, True)])
+def test_linear_ln_equals_linear_then_layernorm(M, Kd, variant, bias, i8_out, dev):
+    """The row-complete LayerNorm epilogue (attn.to_out + residual -> norm2 / norm3 in one launch):
+    y and h bit-identical to linear() followed by layernorm() / layernorm_i8(), every row-complete
+    tile, ragged M (rows past M) included."""
+    k = K()
+    N = 320
+    g = torch.Generator().manual_seed(M + Kd)
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+    b = torch.randn(N, generator=g).half().to(dev) if bias else None
+    r = (torch.randn(M, N, generator=g) * 3).half().to(dev)
+    gamma = (1 + 0.1 * torch.randn(N, generator=g)).half().to(dev)
+    beta = (0.1 * torch.randn(N, generator=g)).half().to(dev)
+    assert k.linear_ln_ok(N) and not k.linear_ln_ok(640)
+    k.force_gemm(variant)
+    try:
+        y, h = k.linear_ln(x, w, r, gamma, beta, 1e-5, bias=b, i8_out=i8_out)
+    finally:
+        k.force_gemm(None)
+    y0 = k.linear(x, w, "f16", bias=b, residual=r)
+    assert torch.equal(y, y0)
+    if i8_out:
+        q0, s0 = k.layernorm_i8(y0, 1e-5, gamma, beta)
+        assert torch.equal(h[0], q0) and torch.equal(h[1], s0)
+    else:
+        assert torch.equal(h, k.layernorm(y0, 1e-5, gamma, beta))
