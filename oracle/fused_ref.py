@@ -238,7 +238,11 @@ def groupnorm_nhwc(a, outs):
     if a.get("fq_in") is not None:
         amax, bits, cadd = a["fq_in"]
         x = finalize(x, amax, bits, chan_add=cadd)
-    return _gn_chain(x, a["groups"], a["eps"], a["gamma"], a["beta"], a.get("silu", False), a.get("q_bits", 0))
+    res = _gn_chain(x, a["groups"], a["eps"], a["gamma"], a["beta"], a.get("silu", False), a.get("q_bits", 0))
+    if a.get("want_xamax"):  # the input's exact per-(n, c) max |x| (the concat shortcut's amax): bit-exact
+        n, c = x.shape[0], x.shape[-1]
+        res.append(Out("xamax", x.float().abs().reshape(n, -1, c).amax(dim=1).reshape(-1), ulps=0))
+    return res
 
 
 def groupnorm_fin(a, outs):
