@@ -815,6 +815,79 @@ static void launch_rows_i8(const f16* x, long rows, int c, int ldx, int8_t* y, i
   else k_quant_rows_i8<PER, 1><<<(int)((rows + 3) / 4), 256, 0, st>>>(x, rows, c, ldx, y, ldy, sa);
 }
 
+// grouped rows (every C = 8 * LPR * P, LPR in {8..64} lanes per row, P <= 5 16-B chunks per lane:
+// SD's 320 / 640 / 1280 / 2560): a wave holds 64 / LPR rows at once, lane l of a row owning chunks
+// l, l + LPR, ... (all 64 lanes carry data; the one-row-per-wave kernel above leaves 24 of 64 idle
+// at C 320), IT row groups per wave with every load issued before the first reduction.  The row max
+// is order-free, so the codes and scales equal k_quant_rows_i8's bit for bit.
+template <int LPR, int P, int IT>
+__global__ void __launch_bounds__(256) k_quant_rows_g(const f16* __restrict__ x, long rows, int c, int ldx,
+                                                      int8_t* __restrict__ y, int ldy, float* __restrict__ sa) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, lr = lane % LPR, rw = lane / LPR;
+  const long wrow0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW * IT;
+  f16x8 v[IT][P];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const long row = wrow0 + (long)it * RPW + rw;
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+      v[it][i] = row < rows ? *reinterpret_cast<const f16x8*>(x + row * ldx + (lr + i * LPR) * 8) : (f16x8){};
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const long row = wrow0 + (long)it * RPW + rw;
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)v[it][i][e]));
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float s = fq_scale(m, 127);
+    const double rs = rcp_exact(s);
+    if (row < rows) {
+      if (lr == 0) sa[row] = s;
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        unsigned lo = 0, hi = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lo |= (unsigned)(uint8_t)q_i8((float)v[it][i][e], s, rs) << (8 * e);
+          hi |= (unsigned)(uint8_t)q_i8((float)v[it][i][4 + e], s, rs) << (8 * e);
+        }
+        *reinterpret_cast<uint2*>(y + row * ldy + (lr + i * LPR) * 8) = make_uint2(lo, hi);
+      }
+    }
+  }
+}
+
+static bool launch_rows_g(const f16* x, long rows, int c, int ldx, int8_t* y, int ldy, float* sa, hipStream_t st) {
+  static const bool off = getenv("QD_QROWS_OLD") != nullptr;  // A/B switch: the one-row-per-wave kernel
+  if (off) return false;
+  const int ch = c / 8;
+  int lpr = 0, per = 0;
+  for (int l = 8; l <= 64 && !lpr; l *= 2)
+    if (ch % l == 0 && ch / l <= 5) {
+      lpr = l;
+      per = ch / l;
+    }
+  if (!lpr) return false;
+  const long rpw = 64 / lpr;
+  // two row groups per wave while the grid keeps >= 1024 blocks
+  const bool two = (rows + 4 * rpw * 2 - 1) / (4 * rpw * 2) >= 1024;
+  const int grid = (int)((rows + 4 * rpw * (two ? 2 : 1) - 1) / (4 * rpw * (two ? 2 : 1)));
+#define QD_QRG(L, PP)                                                                                   \
+  if (lpr == L && per == PP) {                                                                          \
+    if (two) k_quant_rows_g<L, PP, 2><<<grid, 256, 0, st>>>(x, rows, c, ldx, y, ldy, sa);               \
+    else k_quant_rows_g<L, PP, 1><<<grid, 256, 0, st>>>(x, rows, c, ldx, y, ldy, sa);                   \
+    return true;                                                                                        \
+  }
+  QD_QRG(8, 5) QD_QRG(16, 5) QD_QRG(32, 3) QD_QRG(32, 5) QD_QRG(64, 5)
+#undef QD_QRG
+  return false;
+}
+
 extern "C" int qd_quant_rows_i8(const void* x, long rows, int c, int ldx, int8_t* y, int ldy, float* scales,
                                 void* stream) {
   QD_REQUIRE(x && y && scales, "null pointer");
@@ -825,6 +898,10 @@ extern "C" int qd_quant_rows_i8(const void* x, long rows, int c, int ldx, int8_t
   const int per = (c / 8 + 63) / 64;
   const f16* xp = (const f16*)x;
   hipStream_t st = S(stream);
+  if (launch_rows_g(xp, rows, c, ldx, y, ldy, scales, st)) {
+    QD_CHECK_LAUNCH();
+    return 0;
+  }
   if (per <= 1) launch_rows_i8<1>(xp, rows, c, ldx, y, ldy, scales, st);
   else if (per <= 2) launch_rows_i8<2>(xp, rows, c, ldx, y, ldy, scales, st);
   else if (per <= 4) launch_rows_i8<4>(xp, rows, c, ldx, y, ldy, scales, st);

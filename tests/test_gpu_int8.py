@@ -583,3 +583,18 @@ def test_linear_i8_ln_bit_exact(M, Kd, i8_out, variant, dev):
         assert torch.equal(h[0], q0) and torch.equal(h[1], s0)
     else:
         assert torch.equal(h, k.layernorm(y, 1e-5, t(gamma), t(beta)))
+
+
+@pytest.mark.parametrize("rows,c", [(32768, 320), (1000, 640), (77, 1280), (300, 2560), (64, 5120), (77, 768),
+                                    (9, 64)])
+def test_quant_rows_i8_grouped_and_wide(rows, c, dev):
+    """Per-token codes for every row width the UNet / CLIP quantize (the grouped-row kernel at
+    C = 8 * LPR * P, the one-row-per-wave kernel elsewhere): bit-exact to the oracle, zero rows
+    (scale from the 1e-5 floor) and ragged row counts included."""
+    k = K()
+    rng = np.random.default_rng(rows * 7 + c)
+    x = (rng.standard_normal((rows, c)) * rng.uniform(0.1, 30, (rows, 1))).astype(np.float16)
+    x[rows // 2] = 0
+    q, s = k.quant_rows_i8(torch.from_numpy(x).to(dev))
+    qr, sr = R.quant_rows_i8(x)
+    assert np.array_equal(q.cpu().numpy(), qr) and np.array_equal(s.cpu().numpy(), sr)
