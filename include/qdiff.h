@@ -178,6 +178,16 @@ int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const 
 int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
                    const void* residual, const void* chan_add, int chan_add_ld, void* out,
                    void* stream);
+/* qd_conv2d_fwd (epi = QD_EPI_AMAX [| QD_EPI_AMAX_ZEROED | QD_EPI_BIAS]) followed by
+ * qd_fq_finalize(y, amax, ..., n_bits, residual, chan_add, chan_add_ld, out = y): when the plan splits
+ * K and a sample's Ho*Wo rows (<= 256, a multiple of 32) fit one reduction block, the split-K
+ * reduction finalizes the output itself (column maxima in LDS, no atomics, no finalize launch);
+ * otherwise the two launches run.  y = the final output, amax = the per-(n, co) maxima; bit-identical
+ * to the two calls either way. */
+int qd_conv2d_fq(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh, int kw,
+                 int stride, int pad, int upsample2x, const void* bias, int n_bits, const void* residual,
+                 const void* chan_add, int chan_add_ld, void* y, int epi, float* amax, float* ws, long ws_elems,
+                 void* stream);
 
 /* ---------------- int8-MFMA W8A8 mode ------------------------------------------------ */
 /* The reference's W8A8 is fake-quant (fp16 F.linear / F.conv2d on dequantized operands,

@@ -95,6 +95,13 @@ struct GemmArgs {
   f16* ln_y;
   int8_t* ln_y8;
   float* ln_sa8;
+  // conv output fake-quant + residual / per-sample add fused into the split-K reduction
+  // (qd_conv2d_fq): requested with fq_qmax > 0; run_gemm sets fq_done when its plan split K and
+  // the reduction finalized the output (else the caller launches qd_fq_finalize)
+  int fq_qmax;
+  const f16* fq_cadd;
+  int fq_cadd_ld;
+  int fq_done;
 };
 
 constexpr int BK = 64;
@@ -2276,6 +2283,87 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   }
 }
 
+// split-K reduction fused with the conv output fake-quant and the residual / per-sample add
+// (qd_conv2d_fq; the low UNet levels, whose convs split K): block = one sample's rows (RPT * 32 =
+// rows_per_sample <= 256) x 32 columns, thread = 4 columns x RPT rows (8 column quads x 32 row
+// groups, rows rg + 32 rr).  h = half(sum of the slabs in split order + bias) exactly as
+// k_splitk_reduce; the column maxima of h over the sample (the QD_EPI_AMAX value, also written to
+// amax) are reduced in LDS with no atomics, then x = half(fq(h) + residual) or half(fq(h) + cadd)
+// with k_finalize's arithmetic: bit-identical to k_splitk_reduce + qd_fq_finalize.
+template <int RPT>
+__global__ void __launch_bounds__(256) k_splitk_reduce_fq(GemmArgs p) {
+  __shared__ float red[32][33];  // [row group][column]
+  __shared__ float scs[32];
+  __shared__ double scr[32];
+  const int cq = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int nl = cq * 4, n = blockIdx.x * 32 + nl;  // N % 32 == 0 (host)
+  const long mb = (long)blockIdx.y * p.rows_per_sample;
+  const long mn = (long)p.M * p.N;
+  f16x4 bq = {};
+  if ((p.epi & QD_EPI_BIAS) && p.bias) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
+  f32x4 s[RPT];
+  long off[RPT];
+#pragma unroll
+  for (int rr = 0; rr < RPT; ++rr) {
+    off[rr] = (mb + rg + rr * 32) * p.N + n;
+    s[rr] = *reinterpret_cast<const f32x4*>(p.part + off[rr]);
+  }
+  for (int k = 1; k < p.splits; ++k) {
+    f32x4 t[RPT];
+#pragma unroll
+    for (int rr = 0; rr < RPT; ++rr) t[rr] = *reinterpret_cast<const f32x4*>(p.part + k * mn + off[rr]);
+#pragma unroll
+    for (int rr = 0; rr < RPT; ++rr) s[rr] += t[rr];
+  }
+  f16x4 h[RPT];
+  float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int rr = 0; rr < RPT; ++rr)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      h[rr][r] = (f16)(s[rr][r] + (float)bq[r]);
+      cm[r] = fmaxf(cm[r], fabsf((float)h[rr][r]));
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[rg][nl + r] = cm[r];
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float m = 0.f;
+    for (int g = 0; g < 32; ++g) m = fmaxf(m, red[g][threadIdx.x]);
+    const float sc = fq_scale(m, p.fq_qmax);
+    scs[threadIdx.x] = sc;
+    scr[threadIdx.x] = rcp_exact(sc);
+    if (p.amax) p.amax[(long)blockIdx.y * p.N + blockIdx.x * 32 + threadIdx.x] = m;
+  }
+  __syncthreads();
+  const bool has_res = p.res != nullptr;
+  f16x4 ca = {};
+  if (!has_res && p.fq_cadd) ca = *reinterpret_cast<const f16x4*>(p.fq_cadd + (long)blockIdx.y * p.fq_cadd_ld + n);
+#pragma unroll
+  for (int rr = 0; rr < RPT; ++rr) {
+    const long m = mb + rg + rr * 32;
+    f16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = fq_apply_r((float)h[rr][r], scs[nl + r], scr[nl + r]);
+    if (has_res) {
+      const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + m * p.ldy + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (f16)((float)o[r] + (float)rq[r]);
+    } else if (p.fq_cadd) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (f16)((float)o[r] + (float)ca[r]);
+    }
+    *reinterpret_cast<f16x4*>(p.y + m * p.ldy + n) = o;
+  }
+}
+
+// whether k_splitk_reduce_fq takes this plan's output (whole samples of <= 256 rows per block)
+static int fq_rpt(const GemmArgs& p) {
+  if (p.fq_qmax <= 0 || p.i8 || p.N % 32 || p.ldy != p.N || p.rows_per_sample <= 0 || p.M % p.rows_per_sample) return 0;
+  const int r = p.rows_per_sample % 32 ? 0 : p.rows_per_sample / 32;
+  return r == 1 || r == 2 || r == 4 || r == 8 ? r : 0;
+}
+
 // split-K reduction + epilogue with the GroupNorm slot statistics (QD_EPI_GNSTATS) and the
 // per-(sample, column) add (QD_EPI_CADD): block = one 64-row slot x 64 columns; thread (cq, rg)
 // owns 4 columns x rows 4 rg .. 4 rg + 3 (16 column quads x 16 row groups).  Slabs summed in split
@@ -2905,7 +2993,14 @@ static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t
     p.part = ws;
     launch_tile<AMODE, true>(p, pl, fmt, st);
     const int gx = (p.N + 255) / 256;
-    if ((long)gx * ((p.M + 15) / 16) >= 512) {
+    if (const int r = fq_rpt(p)) {
+      const dim3 g(p.N / 32, p.M / p.rows_per_sample);
+      if (r == 1) k_splitk_reduce_fq<1><<<g, 256, 0, st>>>(p);
+      else if (r == 2) k_splitk_reduce_fq<2><<<g, 256, 0, st>>>(p);
+      else if (r == 4) k_splitk_reduce_fq<4><<<g, 256, 0, st>>>(p);
+      else k_splitk_reduce_fq<8><<<g, 256, 0, st>>>(p);
+      p.fq_done = 1;
+    } else if ((long)gx * ((p.M + 15) / 16) >= 512) {
       k_splitk_reduce<4><<<dim3(gx, (p.M + 15) / 16), 256, 0, st>>>(p);
     } else {
       k_splitk_reduce<1><<<dim3(gx, (p.M + 3) / 4), 256, 0, st>>>(p);
@@ -3048,10 +3143,16 @@ extern "C" int qd_linear_ln(const void* x, int M, int K, int lda, const void* w,
                     ws_elems, stream, &ln);
 }
 
-extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt,
-                             int co, int kh, int kw, int stride, int pad, int upsample2x,
-                             const void* bias, const void* residual, void* y, int epi, float* amax,
-                             float* ws, long ws_elems, void* stream) {
+struct FqArgs {
+  int n_bits;
+  const void* residual;
+  const void* cadd;
+  int cadd_ld;
+};
+
+static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh, int kw,
+                    int stride, int pad, int upsample2x, const void* bias, const void* residual, void* y, int epi,
+                    float* amax, float* ws, long ws_elems, void* stream, const FqArgs* fq) {
   GemmArgs p{};
   const int H = upsample2x ? 2 * h : h, W = upsample2x ? 2 * w : w;
   const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
@@ -3092,6 +3193,12 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
   p.b_bytes = (unsigned)((long)co * p.K * 2);
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)n * co, S(stream));
+  if (fq) {  // the finalize's operands ride with the reduction (fq_rpt decides at the split plan)
+    p.fq_qmax = (1 << (fq->n_bits - 1)) - 1;
+    p.res = (const f16*)fq->residual;
+    p.fq_cadd = (const f16*)fq->cadd;
+    p.fq_cadd_ld = fq->cadd_ld > 0 ? fq->cadd_ld : co;
+  }
   if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && !upsample2x) {
     // a pointwise conv IS a GEMM over the NHWC pixel rows (x [N*H*W][Ci_pad]): no tap decode
     p.lda = ci_pad;
@@ -3102,7 +3209,32 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
     run_gemm<AM_CONV_ANY>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
   }
   QD_CHECK_LAUNCH();
+  if (fq && !p.fq_done)  // unsplit plan: the GEMM reduced the amax, the finalize is its own pass
+    return qd_fq_finalize(y, amax, n, Ho * Wo, co, fq->n_bits, fq->residual, fq->cadd, fq->cadd_ld, y, stream);
   return 0;
+}
+
+extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt,
+                             int co, int kh, int kw, int stride, int pad, int upsample2x,
+                             const void* bias, const void* residual, void* y, int epi, float* amax,
+                             float* ws, long ws_elems, void* stream) {
+  return conv_fwd(x, n, h, w, ci, ci_pad, wt, co, kh, kw, stride, pad, upsample2x, bias, residual, y, epi, amax, ws,
+                  ws_elems, stream, nullptr);
+}
+
+extern "C" int qd_conv2d_fq(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh,
+                            int kw, int stride, int pad, int upsample2x, const void* bias, int n_bits,
+                            const void* residual, const void* chan_add, int chan_add_ld, void* y, int epi, float* amax,
+                            float* ws, long ws_elems, void* stream) {
+  QD_REQUIRE((epi & QD_EPI_AMAX) && amax && !(epi & (QD_EPI_RESIDUAL | QD_EPI_AMAX_POST)),
+             "qd_conv2d_fq: epi = QD_EPI_AMAX [| QD_EPI_AMAX_ZEROED | QD_EPI_BIAS], the residual is an argument");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "qd_conv2d_fq: 2 <= n_bits <= 16");
+  QD_REQUIRE(!residual || (reinterpret_cast<uintptr_t>(residual) & 15) == 0, "residual must be 16-B aligned");
+  QD_REQUIRE(!chan_add || ((reinterpret_cast<uintptr_t>(chan_add) & 15) == 0 && (chan_add_ld <= 0 || chan_add_ld >= co)),
+             "chan_add: 16-B aligned rows, ld >= Co");
+  const FqArgs fq{n_bits, residual, chan_add, chan_add_ld};
+  return conv_fwd(x, n, h, w, ci, ci_pad, wt, co, kh, kw, stride, pad, upsample2x, bias, nullptr, y, epi, amax, ws,
+                  ws_elems, stream, &fq);
 }
 
 // ---- int8 x int8 GEMM / conv (the int8-MFMA W8A8 mode) --------------------------------------

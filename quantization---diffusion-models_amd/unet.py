@@ -522,6 +522,18 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
             amax = K.act_absmax(y, "per_channel", K.NHWC)
         else:
             amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
+            pend_gn = pend and residual is not None and chan_add is None and ho * wo > 256
+            if FQ_REDUCE and not (defer and residual is None) and not pend_gn:
+                # the output is finalized right away (a Pending at <= 256 pixels is: no GroupNorm
+                # statistics pass takes it): conv + finalize as one call, the split-K reduction
+                # finalizing the output where the plan splits
+                xo = K.conv2d_fq(x, wk, ci, q, amax, stride, pad, upsample, bias=bias, amax_zeroed=zeroed,
+                                 residual=residual, chan_add=chan_add)
+                if pend and residual is not None and chan_add is None:
+                    pn = Pending(xo, amax, q, residual)
+                    pn.x = xo
+                    return pn
+                return xo
             y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)
         if defer and residual is None:
             return y, (amax, q, chan_add)
@@ -968,6 +980,7 @@ XAMAX_GN = not os.environ.get("QD_NO_XAMAX_GN")  # A/B switch: the concat shortc
 AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
 LN_FQ = not os.environ.get("QD_NO_LN_FQ")  # A/B switch: proj_in finalize as its own pass before norm1
 I8_AMAX_FUSE = not os.environ.get("QD_NO_I8_AMAX_FUSE")  # A/B switch: proj_out's int8 scale by its own pass
+FQ_REDUCE = not os.environ.get("QD_NO_FQ_REDUCE")  # A/B switch: conv + finalize as separate calls
 LN_EPI = not os.environ.get("QD_NO_LN_EPI")  # A/B switch: to_out + residual and norm2 / norm3 as two launches
 
 

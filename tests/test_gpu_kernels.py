@@ -874,3 +874,30 @@ def test_linear_ln_equals_linear_then_layernorm(M, Kd, variant, bias, i8_out, de
         assert torch.equal(h[0], q0) and torch.equal(h[1], s0)
     else:
         assert torch.equal(h, k.layernorm(y0, 1e-5, gamma, beta))
+
+
+@pytest.mark.parametrize("n,hw,ci,co,add", [(8, 8, 1280, 1280, "res"), (8, 16, 1280, 1280, "res"), (8, 8, 2560, 1280, "cadd"),
+                                            (2, 16, 640, 640, "none"), (8, 32, 640, 640, "res"), (3, 8, 320, 640, "res")])
+@pytest.mark.parametrize("variant", [None, 4100, 6104, 2202, 1100])
+def test_conv2d_fq_equals_conv_then_finalize(n, hw, ci, co, add, variant, dev):
+    """The quantized conv + output fake-quant + residual / time-embedding add as one call
+    (qd_conv2d_fq: the split-K reduction finalizes the output where the plan splits): output and
+    amax bit-identical to conv2d_nhwc(amax) + fq_finalize under every forced tile / split."""
+    k = K()
+    g = torch.Generator().manual_seed(n * hw + ci + co)
+    x = torch.randn(n, hw, hw, ci, generator=g).half().to(dev)
+    w = (torch.randn(co, 3, 3, ci, generator=g) / (9 * ci) ** 0.5).half().to(dev)
+    b = torch.randn(co, generator=g).half().to(dev)
+    res = torch.randn(n, hw, hw, co, generator=g).half().to(dev) if add == "res" else None
+    cadd = torch.randn(n, co, generator=g).half().to(dev) if add == "cadd" else None
+    k.force_gemm(variant)
+    try:
+        a0 = torch.zeros(n * co, dtype=torch.float32, device=dev)
+        y0 = k.conv2d_nhwc(x, w, ci, 1, 1, bias=b, amax=a0)
+        x0 = k.fq_finalize(y0, a0, 8, residual=res, chan_add=cadd)
+        a1 = torch.zeros(n * co, dtype=torch.float32, device=dev)
+        x1 = k.conv2d_fq(x, w, ci, 8, a1, 1, 1, bias=b, residual=res, chan_add=cadd)
+    finally:
+        k.force_gemm(None)
+    assert torch.equal(a0, a1)
+    assert torch.equal(x0.view(torch.int16), x1.view(torch.int16))
