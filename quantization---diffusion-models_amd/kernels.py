@@ -602,12 +602,14 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 
 
 def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bias=None, amax_zeroed=False,
-              residual=None, chan_add=None):
+              residual=None, chan_add=None, fused_only=False):
     """conv2d_nhwc(..., amax=amax) then fq_finalize(y, amax, n_bits, residual, chan_add, out=y) - the
     quantized conv's output fake-quant and the block's residual / time-embedding add - as
     qd_conv2d_fq: when the conv's plan splits K at a level whose samples fit one reduction block
     (the 8x8 / 16x16 levels), the split-K reduction finalizes the output and the finalize launch
-    goes.  The kernel choice is conv2d_nhwc's for the same conv (same tuning key): bit-identical."""
+    goes.  The kernel choice is conv2d_nhwc's for the same conv (same tuning key): bit-identical.
+    fused_only: return None (nothing launched) unless the reduction finalizes the output - for a
+    caller whose alternative (a consumer applying the finalize on the fly) beats two launches."""
     _chk(x, "x")
     _chk(w_khwc, "weight")
     n, h, w, cip = x.shape
@@ -616,17 +618,29 @@ def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bi
     ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
     epi = (EPI_BIAS if bias is not None else 0) | EPI_AMAX | (EPI_AMAX_ZEROED if amax_zeroed else 0)
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
+    rps = ho * wo
+    fusable = rps % 32 == 0 and rps // 32 in (1, 2, 4, 8) and co % 32 == 0
+    if fused_only and (not fusable or cip % 64 or (key not in _TUNE and _OVERRIDE is None)):
+        return None
     if (key not in _TUNE and _OVERRIDE is None) or cip % 64:  # untuned shape: conv2d_nhwc tunes it
         y = conv2d_nhwc(x, w_khwc, ci, stride, pad, upsample2x, bias=bias, amax=amax, amax_zeroed=amax_zeroed)
         return fq_finalize(y, amax, n_bits, residual=residual, chan_add=chan_add, out=y)
+    M, Kd = n * ho * wo, kh * kw * cip
+    c = _TUNE.get(key)
+    force = (c[1] if c is not None else -1) if _OVERRIDE is None else _OVERRIDE
+    if fused_only:
+        _force(force)
+        try:
+            if _lib.load().qd_gemm_workspace(M, co, Kd, 0, 0, rps, epi) <= 0:
+                return None  # unsplit plan: no reduction to finalize in
+        finally:
+            _force(-1)
     _USED.add(key)
     if residual is not None:
         _chk(residual, "residual")
     out = _empty((n, ho, wo, co), torch.float16, x.device)
     ld = _cadd_ld(chan_add, n, co, "chan_add")
-    M, Kd = n * ho * wo, kh * kw * cip
-    c = _TUNE.get(key)
-    _force((c[1] if c is not None else -1) if _OVERRIDE is None else _OVERRIDE)
+    _force(force)
     try:
         ws, wsn = _gemm_ws(M, co, Kd, 0, ho * wo, epi, x.device)
         _lib.call("qd_conv2d_fq", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad, 1 if upsample2x else 0,

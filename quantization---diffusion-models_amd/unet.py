@@ -523,6 +523,13 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         else:
             amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
             pend_gn = pend and residual is not None and chan_add is None and ho * wo > 256
+            if FQ_REDUCE and defer and residual is None and chan_add is not None and ho * wo <= 256:
+                # conv1 (+ temb) at the small levels: where the plan splits K the reduction writes the
+                # finalized output, so the consuming GroupNorm reads it as is (no fq_in recompute)
+                xo = K.conv2d_fq(x, wk, ci, q, amax, stride, pad, upsample, bias=bias, amax_zeroed=zeroed,
+                                 chan_add=chan_add, fused_only=True)
+                if xo is not None:
+                    return xo, None
             if FQ_REDUCE and not (defer and residual is None) and not pend_gn:
                 # the output is finalized right away (a Pending at <= 256 pixels is: no GroupNorm
                 # statistics pass takes it): conv + finalize as one call, the split-K reduction
