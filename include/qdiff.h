@@ -183,11 +183,12 @@ int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n
  * K and a sample's Ho*Wo rows (<= 256, a multiple of 32) fit one reduction block, the split-K
  * reduction finalizes the output itself (column maxima in LDS, no atomics, no finalize launch);
  * otherwise the two launches run.  y = the final output, amax = the per-(n, co) maxima; bit-identical
- * to the two calls either way. */
+ * to the two calls either way.  xamax (optional, [N][Co] fp32): the final output's per-(n, co)
+ * max |y| - the per_channel input amax of the conv that consumes it (= qd_act_absmax of y). */
 int qd_conv2d_fq(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh, int kw,
                  int stride, int pad, int upsample2x, const void* bias, int n_bits, const void* residual,
-                 const void* chan_add, int chan_add_ld, void* y, int epi, float* amax, float* ws, long ws_elems,
-                 void* stream);
+                 const void* chan_add, int chan_add_ld, void* y, int epi, float* amax, float* xamax, float* ws,
+                 long ws_elems, void* stream);
 
 /* ---------------- int8-MFMA W8A8 mode ------------------------------------------------ */
 /* The reference's W8A8 is fake-quant (fp16 F.linear / F.conv2d on dequantized operands,

@@ -34,7 +34,7 @@ SIGNATURES = {
     "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
     "qd_linear_fwd": [P, I, I, I, P, I, P, P, I, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
     "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
-    "qd_conv2d_fq": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, I, P, P, I, P, I, P, P, ctypes.c_long, P],
+    "qd_conv2d_fq": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, I, P, P, I, P, I, P, P, P, ctypes.c_long, P],
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, I, P, P],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_groupnorm_xamax": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P, P],

@@ -102,6 +102,7 @@ struct GemmArgs {
   const f16* fq_cadd;
   int fq_cadd_ld;
   int fq_done;
+  float* fq_xamax;  // optional: the finalized output's per-(n, c) max |x| (its consumer conv's amax)
 };
 
 constexpr int BK = 64;
@@ -2353,7 +2354,19 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_fq(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (f16)((float)o[r] + (float)ca[r]);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cm[r] = fmaxf(rr ? cm[r] : 0.f, fabsf((float)o[r]));
     *reinterpret_cast<f16x4*>(p.y + m * p.ldy + n) = o;
+  }
+  if (p.fq_xamax) {  // (uniform) the consumer's amax of the final output, the same LDS reduction
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[rg][nl + r] = cm[r];
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      float m = 0.f;
+      for (int g = 0; g < 32; ++g) m = fmaxf(m, red[g][threadIdx.x]);
+      p.fq_xamax[(long)blockIdx.y * p.N + blockIdx.x * 32 + threadIdx.x] = m;
+    }
   }
 }
 
@@ -3148,6 +3161,7 @@ struct FqArgs {
   const void* residual;
   const void* cadd;
   int cadd_ld;
+  float* xamax;
 };
 
 static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh, int kw,
@@ -3198,6 +3212,7 @@ static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, cons
     p.res = (const f16*)fq->residual;
     p.fq_cadd = (const f16*)fq->cadd;
     p.fq_cadd_ld = fq->cadd_ld > 0 ? fq->cadd_ld : co;
+    p.fq_xamax = fq->xamax;
   }
   if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && !upsample2x) {
     // a pointwise conv IS a GEMM over the NHWC pixel rows (x [N*H*W][Ci_pad]): no tap decode
@@ -3209,8 +3224,11 @@ static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, cons
     run_gemm<AM_CONV_ANY>(p, QD_WFMT_F16, ws, ws_elems, S(stream));
   }
   QD_CHECK_LAUNCH();
-  if (fq && !p.fq_done)  // unsplit plan: the GEMM reduced the amax, the finalize is its own pass
-    return qd_fq_finalize(y, amax, n, Ho * Wo, co, fq->n_bits, fq->residual, fq->cadd, fq->cadd_ld, y, stream);
+  if (fq && !p.fq_done) {  // unsplit plan: the GEMM reduced the amax, the finalize is its own pass
+    const int rc2 = qd_fq_finalize(y, amax, n, Ho * Wo, co, fq->n_bits, fq->residual, fq->cadd, fq->cadd_ld, y, stream);
+    if (rc2 || !fq->xamax) return rc2;
+    return qd_act_absmax(y, QD_LAYOUT_NHWC, n, co, Ho, Wo, QD_GRAN_PER_CHANNEL, 0, fq->xamax, stream);
+  }
   return 0;
 }
 
@@ -3225,14 +3243,14 @@ extern "C" int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_
 extern "C" int qd_conv2d_fq(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh,
                             int kw, int stride, int pad, int upsample2x, const void* bias, int n_bits,
                             const void* residual, const void* chan_add, int chan_add_ld, void* y, int epi, float* amax,
-                            float* ws, long ws_elems, void* stream) {
+                            float* xamax, float* ws, long ws_elems, void* stream) {
   QD_REQUIRE((epi & QD_EPI_AMAX) && amax && !(epi & (QD_EPI_RESIDUAL | QD_EPI_AMAX_POST)),
              "qd_conv2d_fq: epi = QD_EPI_AMAX [| QD_EPI_AMAX_ZEROED | QD_EPI_BIAS], the residual is an argument");
   QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "qd_conv2d_fq: 2 <= n_bits <= 16");
   QD_REQUIRE(!residual || (reinterpret_cast<uintptr_t>(residual) & 15) == 0, "residual must be 16-B aligned");
   QD_REQUIRE(!chan_add || ((reinterpret_cast<uintptr_t>(chan_add) & 15) == 0 && (chan_add_ld <= 0 || chan_add_ld >= co)),
              "chan_add: 16-B aligned rows, ld >= Co");
-  const FqArgs fq{n_bits, residual, chan_add, chan_add_ld};
+  const FqArgs fq{n_bits, residual, chan_add, chan_add_ld, xamax};
   return conv_fwd(x, n, h, w, ci, ci_pad, wt, co, kh, kw, stride, pad, upsample2x, bias, nullptr, y, epi, amax, ws,
                   ws_elems, stream, &fq);
 }

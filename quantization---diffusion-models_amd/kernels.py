@@ -602,14 +602,16 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
 
 
 def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bias=None, amax_zeroed=False,
-              residual=None, chan_add=None, fused_only=False):
+              residual=None, chan_add=None, fused_only=False, xamax=None):
     """conv2d_nhwc(..., amax=amax) then fq_finalize(y, amax, n_bits, residual, chan_add, out=y) - the
     quantized conv's output fake-quant and the block's residual / time-embedding add - as
     qd_conv2d_fq: when the conv's plan splits K at a level whose samples fit one reduction block
     (the 8x8 / 16x16 levels), the split-K reduction finalizes the output and the finalize launch
     goes.  The kernel choice is conv2d_nhwc's for the same conv (same tuning key): bit-identical.
     fused_only: return None (nothing launched) unless the reduction finalizes the output - for a
-    caller whose alternative (a consumer applying the finalize on the fly) beats two launches."""
+    caller whose alternative (a consumer applying the finalize on the fly) beats two launches.
+    xamax ([N*Co] fp32): also the output's per-(n, co) max |x| (= act_absmax of it, the consuming
+    conv's input amax), reduced by the same reduction."""
     _chk(x, "x")
     _chk(w_khwc, "weight")
     n, h, w, cip = x.shape
@@ -624,7 +626,10 @@ def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bi
         return None
     if (key not in _TUNE and _OVERRIDE is None) or cip % 64:  # untuned shape: conv2d_nhwc tunes it
         y = conv2d_nhwc(x, w_khwc, ci, stride, pad, upsample2x, bias=bias, amax=amax, amax_zeroed=amax_zeroed)
-        return fq_finalize(y, amax, n_bits, residual=residual, chan_add=chan_add, out=y)
+        y = fq_finalize(y, amax, n_bits, residual=residual, chan_add=chan_add, out=y)
+        if xamax is not None:
+            _lib.call("qd_act_absmax", _p(y), NHWC, n, co, ho, wo, GRAN["per_channel"], 0, _p(xamax), _stream())
+        return y
     M, Kd = n * ho * wo, kh * kw * cip
     c = _TUNE.get(key)
     force = (c[1] if c is not None else -1) if _OVERRIDE is None else _OVERRIDE
@@ -644,7 +649,8 @@ def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bi
     try:
         ws, wsn = _gemm_ws(M, co, Kd, 0, ho * wo, epi, x.device)
         _lib.call("qd_conv2d_fq", _p(x), n, h, w, ci, cip, _p(w_khwc), co, kh, kw, stride, pad, 1 if upsample2x else 0,
-                  _p(bias), n_bits, _p(residual), _p(chan_add), ld, _p(out), epi, _p(amax), _p(ws), wsn, _stream())
+                  _p(bias), n_bits, _p(residual), _p(chan_add), ld, _p(out), epi, _p(amax), _p(xamax), _p(ws), wsn,
+                  _stream())
     finally:
         _force(-1)
     return out

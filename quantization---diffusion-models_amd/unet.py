@@ -367,7 +367,7 @@ class UNet2DConditionModel(nn.Module):
                     h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True, gn_out=True)
                 skips.append(h)
             if blk.downsamplers is not None:
-                h = run_conv(blk.downsamplers[0].conv, _get(h), gn=True)
+                h = run_conv(blk.downsamplers[0].conv, _get(h), gn=True, in_amax=_xamax(h))
                 skips.append(h)
         mb = self.mid_block
         h = resnet_fwd(mb.resnets[0], h, temb_silu, tp=tps.get(id(mb.resnets[0])), pend=True, gn_out=True)
@@ -382,7 +382,7 @@ class UNet2DConditionModel(nn.Module):
                 if blk.attentions is not None:
                     h = transformer_fwd(blk.attentions[i], h, ctx_kv, pend=True, gn_out=i + 1 < nres)
             if blk.upsamplers is not None:
-                h = run_conv(blk.upsamplers[0].conv, _get(h), upsample=True, gn=True)
+                h = run_conv(blk.upsamplers[0].conv, _get(h), upsample=True, gn=True, in_amax=_xamax(h))
         h = _get(h)
         q = conv_qbits(self.conv_out)
         h = K.groupnorm_nhwc(h, self.conv_norm_out.num_groups, self.conv_norm_out.eps,
@@ -395,10 +395,10 @@ class Pending:
     """A conv output y whose output fake-quant and residual add are still pending: the block
     output x = half(fq(y; amax, bits) + res).  A GroupNorm consumer materialises x in its
     statistics pass (K.groupnorm_fin); any other consumer calls get() (fq_finalize in place)."""
-    __slots__ = ("y", "amax", "bits", "res", "x")
+    __slots__ = ("y", "amax", "bits", "res", "x", "xamax")
 
     def __init__(self, y, amax, bits, res):
-        self.y, self.amax, self.bits, self.res, self.x = y, amax, bits, res, None
+        self.y, self.amax, self.bits, self.res, self.x, self.xamax = y, amax, bits, res, None, None
 
     def get(self):
         if self.x is None:
@@ -420,6 +420,11 @@ def _get(h):
     if isinstance(h, Pending):
         return h.get()
     return h.x if isinstance(h, GnReady) else h
+
+
+def _xamax(h):
+    """The per-(n, c) max |x| of a block output its producing reduction already reduced, or None."""
+    return h.xamax if isinstance(h, Pending) else None
 
 
 def _gn_i8(norm, x, silu):
@@ -534,11 +539,15 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
                 # the output is finalized right away (a Pending at <= 256 pixels is: no GroupNorm
                 # statistics pass takes it): conv + finalize as one call, the split-K reduction
                 # finalizing the output where the plan splits
+                pn_out = pend and residual is not None and chan_add is None
+                # a small-level block output: its consumer may be a sampler conv quantizing it per
+                # channel - the reduction hands over that amax too
+                xam = A.empty((n * wk.shape[0],), torch.float32, x.device) if pn_out and ho * wo <= 256 else None
                 xo = K.conv2d_fq(x, wk, ci, q, amax, stride, pad, upsample, bias=bias, amax_zeroed=zeroed,
-                                 residual=residual, chan_add=chan_add)
-                if pend and residual is not None and chan_add is None:
+                                 residual=residual, chan_add=chan_add, xamax=xam)
+                if pn_out:
                     pn = Pending(xo, amax, q, residual)
-                    pn.x = xo
+                    pn.x, pn.xamax = xo, xam
                     return pn
                 return xo
             y = K.conv2d_nhwc(x, wk, ci, stride, pad, upsample, bias=bias, amax=amax, amax_zeroed=zeroed)

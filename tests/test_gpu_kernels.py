@@ -896,8 +896,11 @@ def test_conv2d_fq_equals_conv_then_finalize(n, hw, ci, co, add, variant, dev):
         y0 = k.conv2d_nhwc(x, w, ci, 1, 1, bias=b, amax=a0)
         x0 = k.fq_finalize(y0, a0, 8, residual=res, chan_add=cadd)
         a1 = torch.zeros(n * co, dtype=torch.float32, device=dev)
-        x1 = k.conv2d_fq(x, w, ci, 8, a1, 1, 1, bias=b, residual=res, chan_add=cadd)
+        xam = torch.full((n * co,), -1.0, dtype=torch.float32, device=dev)
+        x1 = k.conv2d_fq(x, w, ci, 8, a1, 1, 1, bias=b, residual=res, chan_add=cadd, xamax=xam)
     finally:
         k.force_gemm(None)
     assert torch.equal(a0, a1)
     assert torch.equal(x0.view(torch.int16), x1.view(torch.int16))
+    # the consumer conv's per-channel input amax, reduced by the same launch: exactly act_absmax
+    assert torch.equal(xam, k.act_absmax(x0, "per_channel", k.NHWC))
