@@ -601,6 +601,26 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     return out
 
 
+def conv2d_fq_fuses(x, w_khwc, stride=1, pad=0, upsample2x=False, bias=None):
+    """True when conv2d_fq on these operands finalizes in the split-K reduction (its tuned plan
+    splits K and a sample's output rows fit one reduction block); nothing is launched."""
+    n, h, w, cip = x.shape
+    co, kh, kw, _ = w_khwc.shape
+    H, W = (2 * h, 2 * w) if upsample2x else (h, w)
+    ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    rps = ho * wo
+    epi = (EPI_BIAS if bias is not None else 0) | EPI_AMAX
+    key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi)
+    if rps % 32 or rps // 32 not in (1, 2, 4, 8) or co % 32 or cip % 64 or (key not in _TUNE and _OVERRIDE is None):
+        return False
+    c = _TUNE.get(key)
+    _force((c[1] if c is not None else -1) if _OVERRIDE is None else _OVERRIDE)
+    try:
+        return _lib.load().qd_gemm_workspace(n * rps, co, kh * kw * cip, 0, 0, rps, epi) > 0
+    finally:
+        _force(-1)
+
+
 def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bias=None, amax_zeroed=False,
               residual=None, chan_add=None, fused_only=False, xamax=None):
     """conv2d_nhwc(..., amax=amax) then fq_finalize(y, amax, n_bits, residual, chan_add, out=y) - the

@@ -541,8 +541,10 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
                 # finalizing the output where the plan splits
                 pn_out = pend and residual is not None and chan_add is None
                 # a small-level block output: its consumer may be a sampler conv quantizing it per
-                # channel - the reduction hands over that amax too
-                xam = A.empty((n * wk.shape[0],), torch.float32, x.device) if pn_out and ho * wo <= 256 else None
+                # channel - a reduction that finalizes it hands over that amax too (an unsplit plan
+                # would need a column-max pass of its own: left to the consumer, as before)
+                xam = A.empty((n * wk.shape[0],), torch.float32, x.device) \
+                    if pn_out and ho * wo <= 256 and K.conv2d_fq_fuses(x, wk, stride, pad, upsample, bias) else None
                 xo = K.conv2d_fq(x, wk, ci, q, amax, stride, pad, upsample, bias=bias, amax_zeroed=zeroed,
                                  residual=residual, chan_add=chan_add, xamax=xam)
                 if pn_out:
