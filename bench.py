@@ -57,7 +57,9 @@ def parse():
     ap.add_argument("--calib-batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the text encoder + VAE end-to-end timing")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core of sched_getaffinity")
+    ap.add_argument("--no-int8-mode", action="store_true",
+                    help="skip the int8-MFMA mode object of the default SD1.5 W8A8 line")
     a = ap.parse_args()
     if a.mode is None:
         a.mode = {"sd35": "w4a16", "sdxl": "w8a8"}.get(a.model, "w8a8-sq")
@@ -184,7 +186,7 @@ def _conv_choice(shape=(8, 64, 64, 320), kind="conv"):
                 if not ch:
                     return None
                 v = ch % 1000  # (+ 1000 * s: an explicit split-K count)
-                fam = ("k_conv_halo_i8" if 140 <= v <= 144 else "k_gemm_pp<I8>" if 130 <= v <= 134 else
+                fam = ("k_conv_halo_i8" if 140 <= v <= 149 else "k_gemm_pp<I8>" if 130 <= v <= 134 else
                        "k_gemm_dma<I8>")
                 return {"variant": ch, "family": fam}
             continue
@@ -400,25 +402,7 @@ def main():
         loop.set_inputs(lat, qdist.shard_context(full_ctx, rank, world))
         loop.step()
 
-    if world > 1:
-        qdist.share_gemm_table(warm_eager, rank, world)
-    for _ in range(args.warmup):
-        one_step()
-    log("warmup done")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = one_step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = t.item()
+    dt, out = timed_steps(args, one_step, warm_eager, rank, world, dev, log)
     images = B * world * args.steps
     value = images / dt
     if rank == 0:
@@ -428,9 +412,7 @@ def main():
         roof = dominant_kernel_roofline(dev, int8=int8)
         evals_per_s = value * args.denoise_steps  # UNet evals per image per step: 50 steps at CFG batch 2
         path_tflops = evals_per_s * 2 * UNET_GFLOP_PER_SAMPLE / 1e3
-        # north_star's target metric: images/s against the int8-blended bound of one GPU
-        # (int8-eligible GEMM FLOP at the int8 peak + attention FLOP at the fp16 peak)
-        t_min = SD15_I8_FLOP_PER_IMAGE / (PEAK_I8_TOPS * 1e12) + SD15_F16_FLOP_PER_IMAGE / (PEAK_F16_TFLOPS * 1e12)
+        t_min = int8_blended_tmin()
         wq = "W8A8" if args.mode.startswith("w8a8") else args.mode.upper()
         line = {
             "metric": f"images/sec SD1.5 {wq} {args.res}x{args.res} 50-step" + (" int8-MFMA" if int8 else ""),
@@ -458,13 +440,88 @@ def main():
         if not args.no_e2e:
             log("end to end (text encoder + VAE decode) ...")
             line["end_to_end"] = end_to_end(model, out[:B], prompts[:B], dt / args.steps)
+    if world == 1 and not int8 and args.mode.startswith("w8a8") and not args.no_int8_mode:
+        # north_star's target mode, measured in the same run: the same SD1.5 W8A8
+        # workload quantized with int8_mfma=True, the same steps / warmup protocol
+        line["int8_mode"] = int8_mode_line(args, dev, log, lat, full_ctx)
+    if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            line["cpu_baseline"] = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads or len(os.sched_getaffinity(0)))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def int8_blended_tmin():
+    """Seconds per SD1.5 512^2 image at north_star's int8-blended bound of one GPU: the
+    int8-eligible GEMM FLOP at the int8 peak + the attention FLOP at the fp16 peak."""
+    return SD15_I8_FLOP_PER_IMAGE / (PEAK_I8_TOPS * 1e12) + SD15_F16_FLOP_PER_IMAGE / (PEAK_F16_TFLOPS * 1e12)
+
+
+def timed_steps(args, one_step, warm_eager, rank, world, dev, log):
+    """The bench contract's timing: W untimed warm-up steps, then exactly K steps bracketed by a
+    barrier + device synchronize on both sides; the max over ranks.  Returns (seconds, last out)."""
+    import torch
+    import torch.distributed as dist
+    from qdiff import dist as qdist
+    if world > 1:
+        qdist.share_gemm_table(warm_eager, rank, world)
+    for _ in range(args.warmup):
+        one_step()
+    log("warmup done")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        out = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item(), out
+
+
+def int8_mode_line(args, dev, log, lat, full_ctx):
+    """The int8-MFMA W8A8 mode (quantize(..., int8_mfma=True)) on the headline's
+    workload and protocol (1 GPU): a second SD1.5 model built and calibrated like the first, its
+    own 50-step graph loop over the same latents and text embeddings, timed over the same K steps
+    after W warm-ups; with its int8-blended roofline fraction and the int8 dominant conv's
+    roofline (HIP events live, PMC HBM traffic from the committed rocprofv3 pass)."""
+    import torch
+    import argparse as _ap
+    a8 = _ap.Namespace(**vars(args))
+    a8.mode = args.mode + "-int8"
+    model = build_model(a8, dev)
+    log(f"int8-MFMA model built + quantized ({a8.mode})")
+    B = args.batch
+    loop = model.get_loop(B, args.res, args.res, args.denoise_steps, 7.5, use_graph=True)
+    from qdiff import dist as qdist
+    ctx = qdist.shard_context(full_ctx, 0, 1)
+
+    def one_step():
+        return loop.run(lat, ctx)
+
+    dt, out = timed_steps(a8, one_step, None, 0, 1, dev, log)
+    assert out is not None and torch.isfinite(out.float()).all(), "non-finite int8-mode latents"
+    value = B * args.steps / dt
+    log(f"int8 mode: timed {args.steps} steps: {dt:.3f}s")
+    t_min = int8_blended_tmin()
+    return {"metric": f"images/sec SD1.5 W8A8 {args.res}x{args.res} 50-step int8-MFMA", "value": round(value, 4),
+            "unit": "images/s", "ms_per_step": round(dt / args.steps * 1e3, 2), "steps": args.steps,
+            "warmup": args.warmup, "dtype": "i8 (int32 accumulate) + f16",
+            "config": f"same workload as the headline (SD1.5 {a8.mode}, {B} prompts, CFG batch {2 * B}, "
+                      f"{args.denoise_steps} DDIM steps, HIP graph per step), quantize(..., int8_mfma=True)",
+            "int8_blended_roofline": {"achieved": round(value, 4), "bound": round(1.0 / t_min, 2),
+                                      "unit": "images/s per GPU", "frac": round(value * t_min, 4),
+                                      "target_frac": 0.40},
+            "roofline": dominant_kernel_roofline(dev, int8=True)}
 
 
 def mmdit_dominant_roofline(model, dev, s, iters=10):
@@ -622,7 +679,7 @@ def main_sd35(args, model, rank, world, dev, log):
             line["weight_stream"] = weight_footprint(model)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            line["cpu_baseline"] = cpu_baseline_sd35(min(args.cpu_threads, len(os.sched_getaffinity(0))), cfg, s, sc,
+            line["cpu_baseline"] = cpu_baseline_sd35(args.cpu_threads or len(os.sched_getaffinity(0)), cfg, s, sc,
                                                      args.denoise_steps)
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -712,7 +769,7 @@ def main_sdxl(args, model, rank, world, dev, log):
         }
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            base = cpu_baseline(min(args.cpu_threads, len(os.sched_getaffinity(0))))
+            base = cpu_baseline(args.cpu_threads or len(os.sched_getaffinity(0)))
             # the SD1.5 C1 image's seconds scaled by the FLOP ratio of one SDXL image
             per_image = base["seconds_per_image"] * (2 * args.denoise_steps * SDXL_TFLOP_PER_SAMPLE * 1e12) / \
                 (2 * 10 * UNET_GFLOP_PER_SAMPLE * 1e9)

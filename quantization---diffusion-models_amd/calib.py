@@ -24,7 +24,10 @@ from . import kernels as K
 # (multi_row_sum): 16 rows into level 0, then level j += level j-1 whenever the row count is a
 # multiple of 16^j, the levels added 0 += 1 += 2 += 3 at the end (level width 16 while the call
 # count is <= 2^16).  The hook keeps the same four fp32 accumulators on device, so mean() has the
-# reference's bits, not just its value to within fp32 rounding (tests/test_calib_mean.py).
+# bits of the reference's mean_of_dict over CPU tensors (tests/test_calib_mean.py pins that CPU
+# reduction order).  The reference calibrates on CUDA (utils/calib_data.py:235), where torch.mean
+# reduces in the device's own order: parity with that run is to within fp32 rounding of the sum,
+# i.e. unpinned at the bit level.
 _LEVEL_BITS, _LEVELS, _MAX_CALLS = 4, 4, 1 << 16
 
 

@@ -2941,14 +2941,8 @@ static void launch_gemv(const GemmArgs& p, int fmt, int cpl, hipStream_t st) {
 }
 
 // M-fastest block order when the weight operand's bytes outweigh the activation operand's
-// (GemmArgs::mfast; wbytes / abytes: bytes per element of each, in the K the GemmArgs carry);
-// QD_NO_MFAST=1 keeps the split / N-fastest order everywhere (A/B knob)
+// (GemmArgs::mfast; wbytes / abytes: bytes per element of each, in the K the GemmArgs carry)
 static int block_order(const GemmArgs& p, bool linear, double wbytes, double abytes) {  // (convs: linear false)
-  static const bool off = [] {
-    const char* e = getenv("QD_NO_MFAST");
-    return e && atoi(e) != 0;
-  }();
-  if (off) return 0;
   return (double)p.N * p.K * wbytes > (double)p.M * (linear ? p.K : p.Cip) * abytes ? 1 : 0;
 }
 
@@ -3131,8 +3125,7 @@ static int linear_fwd(const void* x, int M, int K, int lda, const void* w, int w
   p.b_bytes = (unsigned)(wfmt == QD_WFMT_F16 ? (long)N * K * 2 : wfmt == QD_WFMT_I8 ? (long)N * K : (long)N * K / 2);
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
-  static const bool gemv_off = getenv("QD_NO_GEMV") != nullptr;  // A/B switch: tile GEMM for every M
-  const int cpl = gemv_off || ln ? 0 : gemv_cpl(p);
+  const int cpl = ln ? 0 : gemv_cpl(p);
   if (cpl) launch_gemv(p, wfmt, cpl, S(stream));
   else run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();
@@ -3247,6 +3240,8 @@ extern "C" int qd_conv2d_fq(const void* x, int n, int h, int w, int ci, int ci_p
   QD_REQUIRE((epi & QD_EPI_AMAX) && amax && !(epi & (QD_EPI_RESIDUAL | QD_EPI_AMAX_POST)),
              "qd_conv2d_fq: epi = QD_EPI_AMAX [| QD_EPI_AMAX_ZEROED | QD_EPI_BIAS], the residual is an argument");
   QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "qd_conv2d_fq: 2 <= n_bits <= 16");
+  // one add per output: the split-K reduction applies either the residual or the channel add
+  QD_REQUIRE(!(residual && chan_add), "qd_conv2d_fq: residual and chan_add are mutually exclusive");
   QD_REQUIRE(!residual || (reinterpret_cast<uintptr_t>(residual) & 15) == 0, "residual must be 16-B aligned");
   QD_REQUIRE(!chan_add || ((reinterpret_cast<uintptr_t>(chan_add) & 15) == 0 && (chan_add_ld <= 0 || chan_add_ld >= co)),
              "chan_add: 16-B aligned rows, ld >= Co");

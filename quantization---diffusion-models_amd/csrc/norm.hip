@@ -638,7 +638,7 @@ __global__ void __launch_bounds__(256) k_gn_fused(GnIn in, int hw, int c, int cg
 
 // groups per fused block: the fewest whole groups spanning whole octets (0: not fused)
 static int gn_fused_groups(int n, int hw, int c, int groups) {
-  if (hw > 256 || getenv("QD_GN_UNFUSED")) return 0;
+  if (hw > 256) return 0;
   const int cg = c / groups;
   for (int G = 1; G <= 16 && G * cg <= GNF_CW; ++G) {
     if (groups % G || (G * cg) % 8) continue;
@@ -1099,17 +1099,12 @@ static void ln_rows_geom(int c, int& lpr, int& per) {
       return;
     }
 }
-static bool ln_rows_env() {
-  static const bool off = getenv("QD_LN_ROWS_OFF") != nullptr;  // A/B switch: the one-row-per-wave kernels
-  return !off;
-}
-
 template <int MODE>
 static bool launch_ln_rows(const f16* x, long rows, int c, float eps, const f16* g, const f16* b, f16* y, int8_t* y8,
                            float* sa8, int rps, const float* amax, int qmax, f16* t_out, hipStream_t st) {
   int lpr, per;
   ln_rows_geom(c, lpr, per);
-  if (!lpr || !ln_rows_env()) return false;
+  if (!lpr) return false;
   const int rpw = 64 / lpr;
   int iters = 1;  // more rows per wave while the grid keeps >= 1024 blocks
   while (iters < 4 && (rows + 4L * rpw * iters * 2 - 1) / (4L * rpw * iters * 2) >= 1024) iters *= 2;

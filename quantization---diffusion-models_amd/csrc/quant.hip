@@ -863,8 +863,6 @@ __global__ void __launch_bounds__(256) k_quant_rows_g(const f16* __restrict__ x,
 }
 
 static bool launch_rows_g(const f16* x, long rows, int c, int ldx, int8_t* y, int ldy, float* sa, hipStream_t st) {
-  static const bool off = getenv("QD_QROWS_OLD") != nullptr;  // A/B switch: the one-row-per-wave kernel
-  if (off) return false;
   const int ch = c / 8;
   int lpr = 0, per = 0;
   for (int l = 8; l <= 64 && !lpr; l *= 2)

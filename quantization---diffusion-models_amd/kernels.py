@@ -586,8 +586,8 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
     _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
-        ty = torch.empty_like(out)
-        ta = torch.empty_like(amax) if amax is not None else None
+        ty = torch.empty((n, ho, wo, co), dtype=torch.float16, device=x.device)
+        ta = torch.empty(n * co, dtype=torch.float32, device=x.device) if epi & EPI_AMAX else None
         cands = _cands([(w_khwc, "f16", None, 0)])
         halo = kh == 3 and kw == 3 and stride == 1 and pad == 1 and cip % 64 == 0
         if halo:
@@ -597,8 +597,23 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
         c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
+    if out is _TUNE_ONLY:
+        return None
     launch(c if c is not None else (0, -1), out, amax, epi, False)
     return out
+
+
+_TUNE_ONLY = object()  # conv2d_nhwc(out=_TUNE_ONLY): tune the key on scratch buffers, launch nothing
+
+
+def _tune_conv_fq_key(x, w_khwc, ci, stride, pad, upsample2x, bias, key):
+    """Tune the (amax-epilogue) conv key of conv2d_fq now, on scratch buffers outside the step
+    arena, so the plan-dependent choices of conv2d_fq / conv2d_fq_fuses (and the buffers their
+    callers allocate) are the same on the first arena step as on every later step and capture."""
+    if key in _TUNE or _OVERRIDE is not None or not _TUNE_ON or torch.cuda.is_current_stream_capturing():
+        return
+    conv2d_nhwc(x, w_khwc, ci, stride, pad, upsample2x, bias=bias, out=_TUNE_ONLY,
+                amax=torch.empty(1, dtype=torch.float32, device=x.device))
 
 
 def conv2d_fq_fuses(x, w_khwc, stride=1, pad=0, upsample2x=False, bias=None):
@@ -611,7 +626,10 @@ def conv2d_fq_fuses(x, w_khwc, stride=1, pad=0, upsample2x=False, bias=None):
     rps = ho * wo
     epi = (EPI_BIAS if bias is not None else 0) | EPI_AMAX
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi)
-    if rps % 32 or rps // 32 not in (1, 2, 4, 8) or co % 32 or cip % 64 or (key not in _TUNE and _OVERRIDE is None):
+    if rps % 32 or rps // 32 not in (1, 2, 4, 8) or co % 32 or cip % 64:
+        return False
+    _tune_conv_fq_key(x, w_khwc, cip, stride, pad, upsample2x, bias, key)
+    if key not in _TUNE and _OVERRIDE is None:
         return False
     c = _TUNE.get(key)
     _force((c[1] if c is not None else -1) if _OVERRIDE is None else _OVERRIDE)
@@ -634,6 +652,8 @@ def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bi
     conv's input amax), reduced by the same reduction."""
     _chk(x, "x")
     _chk(w_khwc, "weight")
+    if residual is not None and chan_add is not None:
+        raise ValueError("conv2d_fq: residual and chan_add are mutually exclusive")
     n, h, w, cip = x.shape
     co, kh, kw, _ = w_khwc.shape
     H, W = (2 * h, 2 * w) if upsample2x else (h, w)
@@ -642,6 +662,8 @@ def conv2d_fq(x, w_khwc, ci, n_bits, amax, stride=1, pad=0, upsample2x=False, bi
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
     rps = ho * wo
     fusable = rps % 32 == 0 and rps // 32 in (1, 2, 4, 8) and co % 32 == 0
+    if fusable and cip % 64 == 0:
+        _tune_conv_fq_key(x, w_khwc, ci, stride, pad, upsample2x, bias, key)
     if fused_only and (not fusable or cip % 64 or (key not in _TUNE and _OVERRIDE is None)):
         return None
     if (key not in _TUNE and _OVERRIDE is None) or cip % 64:  # untuned shape: conv2d_nhwc tunes it

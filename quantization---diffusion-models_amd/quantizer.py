@@ -163,32 +163,6 @@ class AwqQuantizer:
                                              int8_mfma=i8)
                 setattr(parent, name, fake)
 
-    @torch.no_grad()
-    def pseudo_quantize_tensor(self, w, bitWidth=4):
-        """quantizer.py:163-198 (LLM path helper; kept for surface completeness, host torch)."""
-        org = w.shape
-        if self.group_size > 0:
-            assert org[-1] % self.group_size == 0
-            w = w.reshape(-1, self.group_size)
-        assert w.dim() == 2
-        assert torch.isnan(w).sum() == 0
-        if self.zero_point:
-            mx, mn = w.amax(dim=1, keepdim=True), w.amin(dim=1, keepdim=True)
-            max_int, min_int = 2 ** bitWidth - 1, 0
-            scales = (mx - mn).clamp(min=1e-5) / max_int
-            zeros = (-torch.round(mn / scales)).clamp_(min_int, max_int)
-            w = (torch.clamp(torch.round(w / scales) + zeros, min_int, max_int) - zeros) * scales
-            zeros = zeros.view(org[0], -1)
-        else:
-            mx = w.abs().amax(dim=1, keepdim=True).clamp(min=1e-5)
-            max_int, min_int = 2 ** (bitWidth - 1) - 1, -(2 ** (bitWidth - 1))
-            scales = mx / max_int
-            zeros = None
-            w = torch.clamp(torch.round(w / scales), min_int, max_int) * scales
-        assert torch.isnan(scales).sum() == 0
-        assert torch.isnan(w).sum() == 0
-        return w.reshape(org), scales.view(org[0], -1), zeros
-
 
 class SqQuantizer(AwqQuantizer):
     """SmoothQuant diffusion branch (quantizer_SQ.py:323-391, 395-431, 1025-1070)."""

@@ -21,7 +21,6 @@ implements the forward itself, MI355X-first:
 Architecture restated from diffusers' published UNet2DConditionModel (parity of the third-party
 architecture is UNPINNED: diffusers is not installed; see DESIGN.md and oracle/unet_ref.py).
 """
-import os
 from dataclasses import dataclass, field
 from typing import Optional, Sequence, Tuple, Union
 
@@ -437,17 +436,15 @@ def _gn_i8(norm, x, silu):
 
 
 # int8-MFMA mode: the GroupNorm statistics of conv outputs are reduced in the producing conv's
-# epilogue (GroupNorm = coefficient + apply launches); QD_NO_GN_PART=1: the statistics pass instead
-GN_PART = not os.environ.get("QD_NO_GN_PART")
+# epilogue (GroupNorm = coefficient + apply launches)
 
 
 # the GroupNorm-consumer finalize runs on the streaming (> 256 pixels) GroupNorm; smaller levels
 # keep finalize + the single-kernel GroupNorm (fewer launches there)
-GN_FIN = not os.environ.get("QD_NO_GN_FIN")  # A/B switch (scripts/ab_env.sh)
 
 
 def _gn_fin_ok(p):
-    return GN_FIN and isinstance(p, Pending) and p.x is None and p.y.shape[1] * p.y.shape[2] > 256
+    return isinstance(p, Pending) and p.x is None and p.y.shape[1] * p.y.shape[2] > 256
 
 
 def _f16(t):
@@ -528,14 +525,14 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         else:
             amax, zeroed = A.zeroed_f32(n * wk.shape[0], x.device)
             pend_gn = pend and residual is not None and chan_add is None and ho * wo > 256
-            if FQ_REDUCE and defer and residual is None and chan_add is not None and ho * wo <= 256:
+            if defer and residual is None and chan_add is not None and ho * wo <= 256:
                 # conv1 (+ temb) at the small levels: where the plan splits K the reduction writes the
                 # finalized output, so the consuming GroupNorm reads it as is (no fq_in recompute)
                 xo = K.conv2d_fq(x, wk, ci, q, amax, stride, pad, upsample, bias=bias, amax_zeroed=zeroed,
                                  chan_add=chan_add, fused_only=True)
                 if xo is not None:
                     return xo, None
-            if FQ_REDUCE and not (defer and residual is None) and not pend_gn:
+            if not (defer and residual is None) and not pend_gn:
                 # the output is finalized right away (a Pending at <= 256 pixels is: no GroupNorm
                 # statistics pass takes it): conv + finalize as one call, the split-K reduction
                 # finalizing the output where the plan splits
@@ -589,7 +586,7 @@ def _run_conv_i8(layer, i8, x, residual, chan_add, upsample, defer, in_amax=None
     hh = xq.shape[1] * (2 if upsample else 1)
     ww = xq.shape[2] * (2 if upsample else 1)
     k, s, p = layer.kernel_size[0], layer.stride[0], layer.padding[0]
-    if gn and GN_PART and (((hh + 2 * p - k) // s + 1) * ((ww + 2 * p - k) // s + 1)) % 64 == 0:
+    if gn and (((hh + 2 * p - k) // s + 1) * ((ww + 2 * p - k) // s + 1)) % 64 == 0:
         y, part = K.conv2d_i8(xq, sa, i8[0], i8[1], layer.in_channels, s, p, upsample, bias=layer.bias,
                               residual=residual, chan_add=chan_add, gn_stats=True)
         return GnReady(y, part)
@@ -734,7 +731,7 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False, gn_out=False):
         return _resnet_tail(res, h, temb_silu, tp, sc, pend)
     xr, sr = x, skip
     x, skip = _get(x), _get(skip)
-    if skip is not None and GN_PART and conv_i8(res.conv1) and isinstance(xr, GnReady) and isinstance(sr, GnReady) \
+    if skip is not None and conv_i8(res.conv1) and isinstance(xr, GnReady) and isinstance(sr, GnReady) \
             and conv_i8(res.conv_shortcut):
         # int8-MFMA mode, up block: norm1 over the skip concat from both producers' slot statistics
         # (no concat copy, no statistics pass); the shortcut's per-sample codes from the input maxima
@@ -745,7 +742,7 @@ def resnet_fwd(res, x, temb_silu, skip=None, tp=None, pend=False, gn_out=False):
         return _resnet_tail(res, h, temb_silu, tp, sc, pend, gn_out)
     if skip is not None and qs > 0:
         q1n = max(conv_qbits(res.conv1), 0)
-        if q1n > 0 and XAMAX_GN and x.shape[1] * x.shape[2] > 256:
+        if q1n > 0 and x.shape[1] * x.shape[2] > 256:
             # norm1 first: its statistics pass's channel extremes give the concat's exact per-(n, c)
             # maxima, so the shortcut's input quant is the apply pass alone (no column-max pass)
             h, xam = K.groupnorm_nhwc(x, res.norm1.num_groups, res.norm1.eps, _f16(res.norm1.weight),
@@ -784,7 +781,7 @@ def _resnet_tail(res, h, temb_silu, tp, sc, pend=False, gn_out=False):
     if conv_i8(res.conv2):
         h = K.groupnorm_nhwc_i8(h, res.norm2.num_groups, res.norm2.eps, _f16(res.norm2.weight), _f16(res.norm2.bias),
                                 silu=True, fq_in=spec)
-    elif GN_FIN and spec is not None and spec[0] is not None and h.shape[1] * h.shape[2] > 256:
+    elif spec is not None and spec[0] is not None and h.shape[1] * h.shape[2] > 256:
         # streaming levels: the statistics pass writes the finalized conv1 output to a scratch the
         # apply pass re-reads, instead of both passes recomputing the fake-quant + temb add
         amax, bits, cadd = spec
@@ -831,8 +828,8 @@ def transformer_fwd(tm, x, ctx_kv, pend=False, gn_out=False):
     # epilogue (post-residual) when proj_out quantizes per channel through the fp16 path
     q_out = 0 if tm.linear_proj or conv_i8(tm.proj_out) else conv_qbits(tm.proj_out)
     # int8-MFMA mode: the same epilogue amax gives proj_out's per-sample int8 scale
-    i8_out = I8_AMAX_FUSE and not tm.linear_proj and conv_i8(tm.proj_out) and lin_i8(tm.transformer_blocks[-1].ff.net[2])
-    want = AMAX_POST and (q_out > 0 or i8_out) and n * hh * ww >= AMAX_POST_MIN_ROWS and (hh * ww) % 64 == 0
+    i8_out = not tm.linear_proj and conv_i8(tm.proj_out) and lin_i8(tm.transformer_blocks[-1].ff.net[2])
+    want = (q_out > 0 or i8_out) and n * hh * ww >= AMAX_POST_MIN_ROWS and (hh * ww) % 64 == 0
     in_amax = None
     for bi, blk in enumerate(tm.transformer_blocks):
         last = bi == len(tm.transformer_blocks) - 1
@@ -928,7 +925,7 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
     i8_qkv = _qkv_operand_i8(a1) is not None
     if t_fq is not None:
         amax, bits, cadd = t_fq
-        if LN_FQ and amax is not None and bits > 0 and cadd is None and not (i8_qkv and big) and s % 4 == 0 \
+        if amax is not None and bits > 0 and cadd is None and not (i8_qkv and big) and s % 4 == 0 \
                 and c <= 2048:
             t, h = K.layernorm_fq(t, amax, bits, s, blk.norm1.eps, _f16(blk.norm1.weight), _f16(blk.norm1.bias))
         else:
@@ -975,7 +972,7 @@ def _out_ln(layer, x2d, t, norm, i8_next):
     big = t.shape[0] >= I8_MIN_ROWS
     i8h = bool(i8_next) and big
     g, b = _f16(norm.weight), _f16(norm.bias)
-    if LN_EPI and big and K.linear_ln_ok(t.shape[1]):
+    if big and K.linear_ln_ok(t.shape[1]):
         if lin_i8(layer) and layer.output_quant_name == "None":  # int8-MFMA linear (run_linear's i8 path)
             wq, sw = layer.i8_operand()
             xq, sa = K.quant_rows_i8(x2d)
@@ -994,12 +991,6 @@ def _out_ln(layer, x2d, t, norm, i8_next):
 # the post-residual amax epilogue runs unsplit (no split-K slabs): used where M is large enough
 # that the GEMM would not split anyway (the 64x64 and 32x32 levels of SD1.5 at CFG batch 8)
 AMAX_POST_MIN_ROWS = 8192
-XAMAX_GN = not os.environ.get("QD_NO_XAMAX_GN")  # A/B switch: the concat shortcut's column-max pass
-AMAX_POST = not os.environ.get("QD_NO_AMAX_POST")  # A/B switch (scripts/ab_env.sh): colmax pass instead
-LN_FQ = not os.environ.get("QD_NO_LN_FQ")  # A/B switch: proj_in finalize as its own pass before norm1
-I8_AMAX_FUSE = not os.environ.get("QD_NO_I8_AMAX_FUSE")  # A/B switch: proj_out's int8 scale by its own pass
-FQ_REDUCE = not os.environ.get("QD_NO_FQ_REDUCE")  # A/B switch: conv + finalize as separate calls
-LN_EPI = not os.environ.get("QD_NO_LN_EPI")  # A/B switch: to_out + residual and norm2 / norm3 as two launches
 
 
 def _fake_quant_gemm_operand(layer):

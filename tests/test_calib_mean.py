@@ -3,7 +3,9 @@ per-call channel maxima with mean_of_dict (/root/reference/models/StableDiffusio
 torch.mean of the stacked fp16 vectors) after Mean_Max_Activation_Hook recorded them
 (utils/calib_data.py:105-124).  tests/golden/make_golden.py ran both reference functions over 3, 24
 and 600 calls (600 = the reference's calibration: 12 pipeline calls x 50 steps), with magnitudes
-spread over ~2^14 so the fp32 sums round; calib.MeanMaxActivationHook must give the same fp16 bits."""
+spread over ~2^14 so the fp32 sums round; calib.MeanMaxActivationHook must give the same fp16 bits.
+The goldens ran on CPU tensors, so what is pinned is torch's CPU reduction order; the reference's
+own calibration runs on CUDA (utils/calib_data.py:235), whose torch.mean order is not pinned here."""
 import numpy as np
 import pytest
 import torch

@@ -511,3 +511,33 @@ def test_save_load_integer_formats(tmp_path, qc, i8):
     x = torch.randn(2, 4, cfg.sample_size, cfg.sample_size, generator=g).half()
     ctx = torch.randn(2, 77, cfg.cross_attention_dim, generator=g).half()
     assert torch.equal(_one_eval(model, x, 501, ctx), _one_eval(re, x, 501, ctx))
+
+
+def test_arena_plan_stable_with_empty_gemm_table():
+    """the buffers a step allocates must not depend on whether a conv key is
+    tuned yet.  With an EMPTY GEMM table, the capture's eager warm-up step tunes every shape, and
+    the split-K finalize decisions (conv2d_fq / conv2d_fq_fuses: the block-output xamax at the
+    16x16 / 8x8 levels) are taken from the tuned plan on that step already; the graph capture
+    (frozen arena) then follows the recorded plan, and replays equal the eager loop bit for bit.
+    SD1.5 widths at 128^2 (16x16 / 8x8 latents: cip % 64 == 0, K >= 2048, split candidates)."""
+    from qdiff import kernels as K
+    saved = dict(K._TUNE)
+    K._TUNE.clear()
+    try:
+        model = _model("synthetic:sd15", seed=3)
+        model.quantize(quant_config=dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True), quantUnet=True)
+        g = torch.Generator().manual_seed(5)
+        lat = torch.randn(2, 4, 16, 16, generator=g).half()
+        pe = torch.randn(2, 77, 768, generator=g).half()
+        ne = torch.randn(2, 77, 768, generator=g).half()
+        kw = dict(prompt_embeds=pe, negative_prompt_embeds=ne, lat=lat, height=128, width=128, num_inference_steps=3,
+                  output_type="latent")
+        graph = model.generate(use_graph=True, **kw).cpu()
+        assert any(k[0] == "conv" and k[2] <= 16 for k in K._TUNE), "no conv key was tuned"
+        eager = model.generate(use_graph=False, **kw).cpu()
+        graph2 = model.generate(use_graph=True, **kw).cpu()
+        assert torch.isfinite(graph.float()).all()
+        assert torch.equal(graph, graph2) and torch.equal(eager, graph)
+    finally:
+        K._TUNE.clear()
+        K._TUNE.update(saved)
