@@ -57,7 +57,8 @@ def parse():
     ap.add_argument("--calib-batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the text encoder + VAE end-to-end timing")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core of sched_getaffinity")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: every usable core (sched_getaffinity, capped by the cgroup CPU quota)")
     ap.add_argument("--no-int8-mode", action="store_true",
                     help="skip the int8-MFMA mode object of the default SD1.5 W8A8 line")
     a = ap.parse_args()
@@ -306,6 +307,37 @@ def pmc_traffic(variant=None, int8=False):
             "source": os.path.relpath(files[-1], ROOT)}
 
 
+def usable_cores():
+    """(cores, note): the host cores this process may run on - the sched_getaffinity set, capped by
+    the cgroup CPU quota when one is set (a GPU box shares its host: affinity lists every core of
+    the machine while the quota grants this job a slice; threads beyond the quota only time-slice,
+    and torch's CPU ops then run several times slower than on the quota's cores)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            quota = None
+    env = os.environ.get("OMP_NUM_THREADS")
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    note = f"sched_getaffinity {aff} cores, cgroup CPU quota {quota if quota is not None else 'none'}"
+    if quota is None and env and env.isdigit() and 0 < int(env) < aff:
+        # no quota visible: the box's stated per-job CPU share (OMP_NUM_THREADS) bounds the threads
+        cores = int(env)
+        note += f", OMP_NUM_THREADS {env} (the job's CPU share)"
+    return cores, note
+
+
 def cpu_baseline(threads):
     """the reference's CPU fake-quant path on config C1 (SD1.5 W8 RTN, 1 prompt,
     512x512, 10 DDIM steps with CFG = 10 UNet evaluations at batch 2) restated by the oracle
@@ -321,9 +353,13 @@ def cpu_baseline(threads):
         net = UNet2DConditionModel(SD15)
     shapes = {k: torch.empty(v.shape, dtype=torch.float16) for k, v in net.state_dict().items()}
     cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(SD15).items()}
+    note = None
+    if threads is None:
+        threads, note = usable_cores()
     r = CB.c1_baseline(cd, shapes, threads=threads)
     pc = r["per_class"]
     return {"value": round(1.0 / r["seconds_per_image"], 8), "unit": "images/s", "cores": r["threads"],
+            "cores_note": note or "--cpu-threads",
             "kind": "port", "cpu": r["cpu"], "config": "C1: SD1.5 W8 RTN fake-quant (A16), 1 prompt 512x512, "
                                                        "10 DDIM steps + CFG (10 UNet evals at batch 2)",
             "sample": (f"{r['distinct_shapes']} distinct op shapes / {r['ops_per_eval']} ops per UNet eval, each on a "
@@ -447,7 +483,7 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            line["cpu_baseline"] = cpu_baseline(args.cpu_threads or len(os.sched_getaffinity(0)))
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads or None)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
@@ -679,7 +715,7 @@ def main_sd35(args, model, rank, world, dev, log):
             line["weight_stream"] = weight_footprint(model)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            line["cpu_baseline"] = cpu_baseline_sd35(args.cpu_threads or len(os.sched_getaffinity(0)), cfg, s, sc,
+            line["cpu_baseline"] = cpu_baseline_sd35(args.cpu_threads or usable_cores()[0], cfg, s, sc,
                                                      args.denoise_steps)
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -769,7 +805,7 @@ def main_sdxl(args, model, rank, world, dev, log):
         }
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            base = cpu_baseline(args.cpu_threads or len(os.sched_getaffinity(0)))
+            base = cpu_baseline(args.cpu_threads or None)
             # the SD1.5 C1 image's seconds scaled by the FLOP ratio of one SDXL image
             per_image = base["seconds_per_image"] * (2 * args.denoise_steps * SDXL_TFLOP_PER_SAMPLE * 1e12) / \
                 (2 * 10 * UNET_GFLOP_PER_SAMPLE * 1e9)
