@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the text encoder + VAE end-to-end timing")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0: every usable core (sched_getaffinity, capped by the cgroup CPU quota)")
+    ap.add_argument("--epi-lds", action="store_true",
+                    help="measurement: every GEMM epilogue through the LDS C tile (qd_gemm_epi_lds, A/B runs)")
     ap.add_argument("--no-int8-mode", action="store_true",
                     help="skip the int8-MFMA mode object of the default SD1.5 W8A8 line")
     a = ap.parse_args()
@@ -410,6 +412,9 @@ def main():
             print(f"[bench +{time.time() - T0:.0f}s] {msg}", file=sys.stderr, flush=True)
 
     T0 = time.time()
+    if args.epi_lds:
+        from qdiff import _lib
+        _lib.call("qd_gemm_epi_lds", 1)
     model = build_model(args, dev)
     log(f"model built + quantized ({args.model} {args.mode})")
     if args.model == "sd35":

@@ -146,6 +146,9 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
  * weights; packed int4 with wscale_t: the BK-32 variants 110..117 and ping-pong 300..304; other
  * quantized formats keep the planner's register-staged choice). */
 int qd_gemm_force(int variant);
+/* Measurement knob: on != 0 routes every GEMM / conv epilogue through the LDS C tile (the default,
+ * 0, stores straight from the MFMA fragments wherever the epilogue allows; same output bits). */
+int qd_gemm_epi_lds(int on);
 
 /* Measurement knob (process-global): rows per thread of the streaming GroupNorm statistics /
  * apply passes (qd_groupnorm*, 0 = the built-in rule).  Changes the workspace size, so query

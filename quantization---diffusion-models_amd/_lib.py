@@ -66,6 +66,7 @@ SIGNATURES = {
     "qd_channel_absmax_accum": [P, I64, I, P, P, P, P],
     "qd_smooth_fold": [P, P, P, P, I, I, P, F, P, P, P],
     "qd_gemm_force": [I],
+    "qd_gemm_epi_lds": [I],
     "qd_gn_geom_force": [I, I],
     "qd_selftest_recip": [P, P],
     "qd_adaln_modulate": [P, I64, I, I, F, P, P, I, P, P],

@@ -103,6 +103,9 @@ struct GemmArgs {
   int fq_cadd_ld;
   int fq_done;
   float* fq_xamax;  // optional: the finalized output's per-(n, c) max |x| (its consumer conv's amax)
+  // epilogue form (measurement knob qd_gemm_epi_direct): 0 = stores straight from the MFMA fragments
+  // (permlane16 pairs -> 16-B stores) wherever the epilogue allows it; 1 = always through the LDS C tile
+  int epi_lds;
 };
 
 constexpr int BK = 64;
@@ -356,6 +359,7 @@ __device__ __forceinline__ float rowgroup_max(float v) {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ i32x8 f8_operand(f16x8 lo, f16x8 hi) {
@@ -414,7 +418,10 @@ constexpr int ln_lpr(int bn) {
 }
 constexpr int ln_per(int bn) { return ln_lpr(bn) ? bn / 8 / ln_lpr(bn) : 0; }
 
-template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH>
+// CONV: a conv kernel's epilogue (no GEGLU / GELU-tanh: those are linear-only, compiled out);
+// DIRECT: the direct-store path is compiled in (kernels whose epilogues always take the LDS path - the
+// int8 halo conv's GroupNorm slot statistics - leave it out: its registers would spill there)
+template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH, bool CONV = false, bool DIRECT = true>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM][TN], f16* smem, int m0, int n0,
                                               int wm0, int wn0, int split) {
   static_assert(SPLIT || epi_lds_halves(BM, BN) <= LDSH, "epilogue LDS exceeds the kernel's buffer");
@@ -442,8 +449,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
     const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
     const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
-    const bool geglu = (p.epi & QD_EPI_GEGLU) != 0;
-    const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+    const bool geglu = !CONV && (p.epi & QD_EPI_GEGLU) != 0;
+    const bool gtanh = !CONV && (p.epi & QD_EPI_GELU_TANH) != 0;
     // post-residual amax: the residual is added to the fragments (8-B loads per lane) before the
     // column maxes, and the coalesced pass below stores the tile as it stands
     const bool post = has_res && do_amax && (p.epi & QD_EPI_AMAX_POST) && !geglu && !gtanh;
@@ -473,7 +480,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // while the fragments go to LDS (a 2-deep load / add / store loop left the epilogue waiting on
     // HBM latency NR / 2 times)
     constexpr int CPR16 = BN / 8, NR = (BM * CPR16 + NT - 1) / NT;
-    const bool pre_res = has_res && !fres && !geglu;
+    // direct stores (no LDS C tile): the epilogues that need no row-complete / slot view of the tile
+    // (plain, bias, residual, pre-residual amax, GEGLU, GELU-tanh) store each lane's fragments
+    // themselves: fragments j, j + 1 (4 columns each, rows fr) are paired by one v_permlane16_swap per
+    // dword, after which lane (fr, fq) holds 8 consecutive columns 16 (fq & 1) + 8 (fq >> 1) of the
+    // pair - one 16-B store (or residual load) per lane and pair, 16 rows x 64 B per instruction.
+    // Same arithmetic per element as the LDS pass below, so the output bits are identical.
+    // (an odd TN's last fragment stores its 4 columns as one 8-B store per lane)
+    constexpr bool DIRECT_OK = DIRECT && TN >= 2 && TN <= 5 && TM * ((TN + 1) / 2) <= 20;  // (TN 8: spills)
+    const bool direct = DIRECT_OK && !p.epi_lds && !gn && !ln && !cadd && !post && (!geglu || TN % 4 == 0);
+    const bool pre_res = has_res && !fres && !geglu && !direct;
     // post-residual amax: the residual in the fragments' layout (4 consecutive columns of one row
     // per lane and fragment), all TM x TN 8-B loads issued before any is used
     constexpr bool PF_POST = TM * TN <= 20;  // (register budget: the 4 x 5 fragment tiles and smaller)
@@ -490,7 +506,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
         }
       }
     }
-    f16x8 rq[NR];
+    // (the direct path's residual fragments share this array: one private array fewer keeps the
+    // promote-alloca budget for the accumulators and operand staging)
+    constexpr int NRQ = NR > TM * (TN / 2 + (TN & 1)) ? NR : TM * (TN / 2 + (TN & 1));
+    f16x8 rq[NRQ];
     if (pre_res) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -498,6 +517,166 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
         const int row = e / CPR16, n = n0 + (e - row * CPR16) * 8;
         const bool ok = (BM * CPR16 % NT == 0 || e < BM * CPR16) && m0 + row < p.M && n < p.N;
         rq[i] = bload(rrs, ok ? ((unsigned)(m0 + row) * (unsigned)p.ldy + (unsigned)n) * 2u : OOB);
+      }
+    }
+    // column-max commit of fragment column group j (cm: this lane's 4 column maxima over its rows)
+    auto amax_commit = [&](int j, float (&cm)[4]) {
+      const int nl = wn0 + j * 16 + fq * 4;
+      const int n = n0 + nl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
+      const int row0 = m0 + wm0;
+      if (blk_amax) {
+        if (fr == 0) *reinterpret_cast<f32x4*>(cmx + (wm0 / WM) * BN + nl) = (f32x4){cm[0], cm[1], cm[2], cm[3]};
+      } else if (fr == 0 && n < p.N && row0 < p.M) {
+        float* a = p.amax + (long)(row0 / p.rows_per_sample) * p.N + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
+      }
+    };
+    if constexpr (DIRECT_OK) {
+      if (direct) {
+        constexpr int NJ = TN / 2;
+        const int cpart = 16 * (fq & 1) + 8 * (fq >> 1);
+        const bool gg = geglu;
+        // output columns of pair jp: GEGLU pairs OUTPUT fragments (2 gemm fragments each: hidden | gate)
+        const int ocol0 = gg ? ((n0 + wn0) >> 1) : n0 + wn0;
+        const int oN = gg ? (p.N >> 1) : p.N;
+        const int npair = gg ? NJ / 2 : NJ;
+        constexpr bool TAIL = TN & 1;  // (never with GEGLU: TN % 4 == 0 there)
+        // residual fragments of row block i are loaded two row blocks ahead (all TM x NJ at once would
+        // hold 64 VGPRs beside the 256 x 128 tile's 128 accumulators and spill)
+        constexpr int NJT = NJ + (TAIL ? 1 : 0);  // rq[i * NJT + jp]: pair jp of row block i (jp == NJ: the tail)
+        auto load_res = [&](int i) {
+          {
+            const int m = m0 + wm0 + i * 16 + fr;
+#pragma unroll
+            for (int jp = 0; jp < NJ; ++jp) {
+              const int n = ocol0 + 32 * jp + cpart;
+              rq[i * NJT + jp] = bload(rrs, (jp < npair && m < p.M && n < oN) ? ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u : OOB);
+            }
+            if constexpr (TAIL) {
+              const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
+              const f16x4 t = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(
+                  rrs, (m < p.M && n < p.N) ? (int)(((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u) : (int)OOB, 0, 0));
+              rq[i * NJT + NJ] = (f16x8){t[0], t[1], t[2], t[3], (f16)0, (f16)0, (f16)0, (f16)0};
+            }
+          }
+        };
+        // prefetch distance in row blocks (the 256 x 128 tiles' 32 fragments leave room for one)
+        constexpr int PFD = TM * TN >= 32 ? 1 : 2;
+        if (has_res) {
+#pragma unroll
+          for (int i = 0; i < PFD && i < TM; ++i) load_res(i);
+        }
+        // the bias per fragment column (h = half(acc + bias), the LDS pass's f32 add), then this lane's
+        // column maxima of h per column group (no per-row arrays: register pressure)
+        f16x4 bq[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn0 + j * 16 + fq * 4;
+          bq[j] = (has_bias && n < p.N) ? *reinterpret_cast<const f16x4*>(p.bias + n) : f16x4{};
+        }
+        auto frag16 = [&](int i, int j) {
+          f16x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[j][r]);
+          return h;
+        };
+        if (do_amax && !gg) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 16 + fq * 4;
+            float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              const bool ok = m0 + wm0 + i * 16 + fr < p.M && n < p.N;
+              const f16x4 h = frag16(i, j);
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (ok) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+            }
+            amax_commit(j, cm);
+          }
+        }
+        // GEGLU output fragment: half(h * half(gelu(g))) of gemm fragments j | j + 1
+        auto geglu_frag = [&](int i, int j) {
+          const f16x4 hv = frag16(i, j), gv = frag16(i, j + 1);
+          f16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 g2 = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+            o[r] = (f16)((float)hv[r] * (float)(f16)g2.x);
+            o[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)g2.y);
+          }
+          return o;
+        };
+        auto plain_frag = [&](int i, int j) {
+          f16x4 o = frag16(i, j);
+          if (gtanh) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (f16)gelu_tanh_f((float)o[r]);
+          }
+          return o;
+        };
+        // pair (a | b) -> 16-B store (+ residual) at output column n of row m
+        auto store_pair = [&](int i, int jp, f16x4 fa, f16x4 fb, int m, bool row_ok) {
+          u32x4 w;
+          {
+            const u32x2 a = __builtin_bit_cast(u32x2, fa), b = __builtin_bit_cast(u32x2, fb);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+            w = (u32x4){s0[0], s1[0], s0[1], s1[1]};
+          }
+          const int n = ocol0 + 32 * jp + cpart;
+          if (has_res) {
+            f16x8 v = __builtin_bit_cast(f16x8, w);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + jp][r]);
+            w = __builtin_bit_cast(u32x4, v);
+          }
+          const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
+          __builtin_amdgcn_raw_buffer_store_b128(w, yrs, (row_ok && n < oN) ? (int)off : (int)OOB, 0, 0);
+        };
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          if (has_res && i + PFD < TM) load_res(i + PFD);
+          const int m = m0 + wm0 + i * 16 + fr;
+          const bool row_ok = m < p.M;
+          if constexpr (TN % 4 == 0) {
+            if (gg) {
+#pragma unroll
+              for (int jp = 0; jp < TN / 4; ++jp) store_pair(i, jp, geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2), m, row_ok);
+              continue;
+            }
+          }
+#pragma unroll
+          for (int jp = 0; jp < NJ; ++jp) store_pair(i, jp, plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1), m, row_ok);
+          if constexpr (TAIL) {
+            f16x4 v = plain_frag(i, TN - 1);
+            if (has_res) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + NJ][r]);
+            }
+            const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
+            const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs,
+                                                  (row_ok && n < p.N) ? (int)off : (int)OOB, 0, 0);
+          }
+          // one row block at a time: the scheduler may not pull later blocks' conversions / swaps up
+          // (their temporaries beside the live accumulators spill)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (do_amax && !gg && blk_amax) {
+          __syncthreads();
+          for (int c = threadIdx.x; c < BN; c += NT) {
+            float mm = cmx[c];
+#pragma unroll
+            for (int w = 1; w < WGM; ++w) mm = fmaxf(mm, cmx[w * BN + c]);
+            if (n0 + c < p.N && m0 < p.M) atomic_max_pos(p.amax + (long)(m0 / p.rows_per_sample) * p.N + n0 + c, mm);
+          }
+        }
+        return;
       }
     }
     {
@@ -538,20 +717,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           }
           *reinterpret_cast<f16x4*>(ct + ml * LP + nl) = h;
         }
-        if (do_amax && !geglu) {
-          // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cm[r] = rowgroup_max(cm[r]);
-          const int row0 = m0 + wm0;
-          if (blk_amax) {
-            // rows past M contribute 0 (cm starts at 0, `ok` excludes them)
-            if (fr == 0) *reinterpret_cast<f32x4*>(cmx + (wm0 / WM) * BN + nl) = (f32x4){cm[0], cm[1], cm[2], cm[3]};
-          } else if (fr == 0 && col_ok && row0 < p.M) {
-            float* a = p.amax + (long)(row0 / p.rows_per_sample) * p.N + n;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) atomic_max_pos(a + r, cm[r]);
-          }
-        }
+        // rows of this wave tile lie in one sample (rows_per_sample % WM == 0, host check); rows past
+        // M contribute 0 (cm starts at 0, `ok` excludes them)
+        if (do_amax && !geglu) amax_commit(j, cm);
       }
     }
     __syncthreads();
@@ -838,7 +1006,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN, 256, TM, TN, SPLIT, 2 * (ASZ + BSZ)>(p, acc, smem, m0, n0, wm0, wn0, split);
+  gemm_epilogue<BM, BN, 256, TM, TN, SPLIT, 2 * (ASZ + BSZ), AMODE != AM_LINEAR>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // ---- LDS-DMA variant ----------------------------------------------------------------------
@@ -1320,7 +1488,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
       for (int j = 0; j < TN; ++j) acc[i][j] *= s;
     }
   }
-  gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
+  gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, AMODE != AM_LINEAR>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // ---- ping-pong GEMM (256 x BN tile, 8 waves, BK 32, 4-stage LDS-DMA ring) ----------------
@@ -1716,8 +1884,8 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
-  else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
+  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true, LDSZ, true>(p, acc, smem, m0, n0, wm0, wn0, split);
+  else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ, true>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // ---- split-phase halo conv (variants 202 / 203) -------------------------------------------
@@ -1892,8 +2060,8 @@ __global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
-  else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ>(p, acc, smem, m0, n0, wm0, wn0, split);
+  if (p.splits > 1) gemm_epilogue<BM, BN, NT, TM, TN, true, LDSZ, true>(p, acc, smem, m0, n0, wm0, wn0, split);
+  else gemm_epilogue<BM, BN, NT, TM, TN, false, LDSZ, true>(p, acc, smem, m0, n0, wm0, wn0, split);
 }
 
 // ---- int8 halo conv (int8-MFMA mode, qd_gemm_force 140 / 141) -------------------------------
@@ -2164,10 +2332,10 @@ __global__ void __launch_bounds__(2 * BM, BM == 256 ? 1 : 2) k_conv_halo_i8(Gemm
   }
   if (p.splits > 1) {
     i8_scale<TM, TN, true>(p, iacc, acc, m0, n0, wm0, wn0);
-    gemm_epilogue<BM, BN, NT, TM, TN, true, LDSB / 2>(p, acc, esm, m0, n0, wm0, wn0, split);
+    gemm_epilogue<BM, BN, NT, TM, TN, true, LDSB / 2, true, false>(p, acc, esm, m0, n0, wm0, wn0, split);
   } else {
     i8_scale<TM, TN, false>(p, iacc, acc, m0, n0, wm0, wn0);
-    gemm_epilogue<BM, BN, NT, TM, TN, false, LDSB / 2>(p, acc, esm, m0, n0, wm0, wn0, split);
+    gemm_epilogue<BM, BN, NT, TM, TN, false, LDSB / 2, true, false>(p, acc, esm, m0, n0, wm0, wn0, split);
   }
 }
 
@@ -2481,6 +2649,173 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_gn(GemmArgs p) {
   }
 }
 
+// ---- int8 GEGLU projection + per-token int8 codes of its output (int8-MFMA mode) -------------
+// diffusers FeedForward's GEGLU (ff.net.0: proj -> hidden * gelu(gate)) followed by ff.net.2's
+// per-token input quantization as ONE launch on a row-complete tile: a block owns BM = 64 token
+// rows and ALL N = 2H interleaved projection rows, so the row max of the GEGLU output - the
+// per-token scale - is found in-block and the fp16 GEGLU output never reaches HBM (the two-launch
+// path writes it and the row quantizer reads it back: 2 x 84 MB per 64x64-level call at CFG 8).
+//   * A (the block's 64 x K codes, K = 64 KS) stays in registers: wave (wm, wn) of the 2 x 4 wave
+//     grid holds rows 32 wm .. +31 as TM = 2 x KS fragments of v_mfma_i32_16x16x64_i8;
+//   * the projection streams through a 3-slot LDS-DMA ring in chunks of 128 rows = 4 interleave
+//     blocks [hidden 16 | gate 16] = 64 GEGLU outputs, as KS K-step slabs of 128 x 64 B (BDma,
+//     BKT 32: the int8 "half view"); wave wn takes block wn: fragment j = 0 hidden, 1 gate, C^T
+//     layout as k_gemm_dma's int8 tiles; the fp32 weight scales and the bias sit in LDS;
+//   * per chunk: h, g = half(((float)acc sa[m]) sw[n] + bias) and half(h half(gelu(g))) -
+//     gemm_epilogue's GEGLU arithmetic - kept as fp16 in registers (NCH x 8 values per lane);
+//   * after the last chunk: the row max over each lane's values, its lane groups (shuffles) and
+//     the 4 waves sharing the rows (LDS), s = fq_scale(max, 127), codes q_i8 - k_quant_rows_g's
+//     arithmetic - staged through LDS into 16-B row stores.
+// Bit-identical to linear_i8(..., geglu=True) followed by quant_rows_i8 (tests/test_gpu_int8.py).
+__device__ __forceinline__ int8_t q_i8g(float x, float s, double rs) {  // (quant.hip q_i8)
+  const f16 t = (f16)(float)((double)x * rs);
+  return (int8_t)__builtin_rintf((float)t);
+}
+
+template <int KS, int NCH>
+__global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __restrict__ y8, int ldy8,
+                                                     float* __restrict__ sa8) {
+  constexpr int BM = 64, NT = 512, CH = 128, TM = 2, SLAB = CH * 32, CHUNK = KS * SLAB;
+  constexpr int NOUT = NCH * 64;               // GEGLU outputs per row
+  constexpr int CP = NOUT + 16;                // code-tile row pitch (bytes): 16 rows x 4 B conflict-free
+  constexpr int RING = 3 * CHUNK;              // halves
+  static_assert(BM * CP <= RING * 2, "code tile fits the ring");
+  constexpr int ASZ = KS * BM * 32;             // the A tile: KS slabs of 64 rows x 64 B
+  __shared__ __attribute__((aligned(16))) f16 smem[RING + ASZ + NCH * CH * 3 + 2 * 4 * BM];
+  f16* const As = smem + RING;
+  float* const swl = reinterpret_cast<float*>(smem + RING + ASZ);             // [N] fp32 weight scales
+  f16* const bl16 = smem + RING + ASZ + NCH * CH * 2;                          // [N] bias
+  float* const rmx = reinterpret_cast<float*>(smem + RING + ASZ + NCH * CH * 3);  // [4][BM] row maxima
+  const int m0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+
+  // weight scales and bias of all N rows into LDS (plain loads, drained before any DMA)
+  for (int n = threadIdx.x; n < NCH * CH; n += NT) {
+    swl[n] = p.sw[n];
+    bl16[n] = p.bias ? p.bias[n] : (f16)0.f;
+  }
+  // the block's A tile into LDS (64-B slab rows, the ring's swizzle): 16-B piece e = (row, ks, chunk);
+  // in registers it would hold 40 VGPRs beside the 80 of the packed GEGLU outputs (spills)
+  const __amdgpu_buffer_rsrc_t ars = rsrc(p.a, p.a_bytes);
+  for (int e = threadIdx.x; e < BM * KS * 4; e += NT) {
+    const int row = e / (KS * 4), rem = e - row * (KS * 4), ks = rem >> 2, ch = rem & 3;
+    const int m = m0 + row;
+    const f16x8 v = bload(ars, m < p.M ? (unsigned)m * (unsigned)p.lda * 2u + (unsigned)(ks * 64 + ch * 16) : OOB);
+    *reinterpret_cast<f16x8*>(As + ks * BM * 32 + swz_t<32>(row, ch)) = v;
+  }
+  float sam[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) sam[i] = p.sa[min(m0 + wm * 32 + i * 16 + fr, p.M - 1)];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  BDma<CH, NT, 32> bl;
+  auto issue_chunk = [&](int c, f16* dst) {
+    bl.init(p, c * CH, wid);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bl.issue(p, ks * 32, dst + ks * SLAB, wid);
+  };
+  issue_chunk(0, smem);
+  issue_chunk(1, smem + CHUNK);
+
+  // (packed: two fp16 per VGPR - unpacked the 40 x 4 values alone would take 160 registers)
+  u32x2 vals[NCH][TM];
+  f16x2v m2[TM];  // running packed |value| maxima of each row block (exact)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) m2[i] = (f16x2v){(f16)0.f, (f16)0.f};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    // own DMA of chunk c landed (chunk c + 1 may stay in flight), then the block barrier: every
+    // wave's share landed and chunk c - 1's slot is free for chunk c + 2
+    if (c + 1 < NCH) wait_vm<KS>();
+    else wait_vm<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 2 < NCH) issue_chunk(c + 2, smem + ((c + 2) % 3) * CHUNK);
+    const f16* Bs = smem + (c % 3) * CHUNK;
+    i32x4 iacc[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) iacc[i][j] = (i32x4){0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      f16x8 bf[2], af[TM];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + ks * SLAB + swz_t<32>(wn * 32 + j * 16 + fr, fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + ks * BM * 32 + swz_t<32>(wm * 32 + i * 16 + fr, fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          iacc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, bf[j]),
+                                                             __builtin_bit_cast(i32x4, af[i]), iacc[i][j], 0, 0, 0);
+    }
+    // GEGLU of the chunk: rows n = c CH + 32 wn + 16 j + 4 fq + r
+    const int nl = c * CH + wn * 32 + fq * 4;
+    const f32x4 sw0 = *reinterpret_cast<const f32x4*>(swl + nl), sw1 = *reinterpret_cast<const f32x4*>(swl + nl + 16);
+    const f16x4 b0 = *reinterpret_cast<const f16x4*>(bl16 + nl), b1 = *reinterpret_cast<const f16x4*>(bl16 + nl + 16);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_barrier(0);  // one row block's GELU temporaries at a time
+      f16x4 hv, gv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[r] = (f16)((((float)iacc[i][0][r] * sam[i]) * sw0[r]) + (float)b0[r]);
+        gv[r] = (f16)((((float)iacc[i][1][r] * sam[i]) * sw1[r]) + (float)b1[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f32x2 g2 = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+        const f16x2v o = {(f16)((float)hv[r] * (float)(f16)g2.x), (f16)((float)hv[r + 1] * (float)(f16)g2.y)};
+        vals[c][i][r >> 1] = __builtin_bit_cast(unsigned, o);
+        m2[i] = __builtin_elementwise_max(m2[i], __builtin_elementwise_abs(o));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // row maxima: the lane's values, its 4 lane groups (fq), the 4 waves wn sharing the rows
+  float mx[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float m = fmaxf((float)m2[i][0], (float)m2[i][1]);
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    mx[i] = m;
+    if (fq == 0) rmx[wn * BM + wm * 32 + i * 16 + fr] = m;
+  }
+  __syncthreads();  // (also: every wave's last ring reads are done - the code tile reuses the ring)
+  char* const ct = reinterpret_cast<char*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rl = wm * 32 + i * 16 + fr;
+    const float m = fmaxf(fmaxf(rmx[rl], rmx[BM + rl]), fmaxf(rmx[2 * BM + rl], rmx[3 * BM + rl]));
+    const float s = fq_scale(m, 127);
+    const double rs = rcp_exact(s);
+    if (wn == 0 && fq == 0 && m0 + rl < p.M) sa8[m0 + rl] = s;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      __builtin_amdgcn_sched_barrier(0);  // (hoisted, the unpacked values of every chunk spill)
+      unsigned w = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        w |= (unsigned)(uint8_t)q_i8g((float)__builtin_bit_cast(f16x2v, vals[c][i][r >> 1])[r & 1], s, rs) << (8 * r);
+      *reinterpret_cast<unsigned*>(ct + rl * CP + c * 64 + wn * 16 + fq * 4) = w;
+    }
+  }
+  __syncthreads();
+  constexpr int C16 = NOUT / 16;
+  for (int e = threadIdx.x; e < BM * C16; e += NT) {
+    const int row = e / C16, cc = e - row * C16;
+    if (m0 + row < p.M)
+      *reinterpret_cast<uint4*>(y8 + (long)(m0 + row) * ldy8 + cc * 16) = *reinterpret_cast<const uint4*>(ct + row * CP + cc * 16);
+  }
+}
+
 // ---- tile / split selection (host) ----------------------------------------------------------
 // kind 0: register-staged k_gemm (any weight format); kind 1: LDS-DMA k_gemm_dma (F16 weights)
 struct Plan {
@@ -2518,6 +2853,11 @@ static constexpr DmaVar kDmaC[] = {
     // per CU, so one block's epilogue (residual, y, LayerNorm) runs beside the other's K loop
     {64, 320, 1, 4, 3, 0, 1.00, 32},   // 18
 };
+static int g_epi_lds = 0;  // measurement knob (qd_gemm_epi_lds): 1 = every epilogue through the LDS C tile
+extern "C" int qd_gemm_epi_lds(int on) {
+  g_epi_lds = on ? 1 : 0;
+  return 0;
+}
 static int g_force = -1;  // tuning knob (qd_gemm_force): -1 auto, 0..3 register tiles, 100 + i DMA variant i
 static int g_split = 0;   // with a forced DMA / ping-pong / halo variant: exact split-K count (0 = the fit rule)
 
@@ -3093,6 +3433,7 @@ static int linear_fwd(const void* x, int M, int K, int lda, const void* w, int w
                       const LnArgs* ln) {
   QD_REQUIRE(!(epi & QD_EPI_LN), "QD_EPI_LN is set by qd_linear_ln");
   GemmArgs p{};
+  p.epi_lds = g_epi_lds;
   p.a = (const f16*)x;
   p.lda = lda;
   p.b = w;
@@ -3161,6 +3502,7 @@ static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, cons
                     int stride, int pad, int upsample2x, const void* bias, const void* residual, void* y, int epi,
                     float* amax, float* ws, long ws_elems, void* stream, const FqArgs* fq) {
   GemmArgs p{};
+  p.epi_lds = g_epi_lds;
   const int H = upsample2x ? 2 * h : h, W = upsample2x ? 2 * w : w;
   const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   p.a = (const f16*)x;
@@ -3483,6 +3825,7 @@ static int linear_i8(const void* x, const float* sa, int M, int K, int lda, cons
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
              "x and w must be 16-B aligned");
   GemmArgs p{};
+  p.epi_lds = g_epi_lds;
   p.a = (const f16*)x;
   p.lda = lda / 2;
   p.b = w;
@@ -3525,6 +3868,43 @@ extern "C" int qd_linear_i8(const void* x, const float* sa, int M, int K, int ld
                    stream, nullptr);
 }
 
+// int8 GEGLU projection + per-token codes of its output (k_geglu_i8q): x [M, K] codes (lda), sa [M],
+// w [N][K] codes with rows interleaved in 16-row [hidden | gate] blocks (as qd_linear_i8's GEGLU
+// epilogue), sw [N] fp32, bias [N] fp16 -> y8 [M, N / 2] codes (ldy8) + sa8 [M]: bit-identical to
+// qd_linear_i8(..., QD_EPI_GEGLU) followed by qd_quant_rows_i8.  Shapes: K = 320, N = 2560 (SD1.5's
+// 64x64-level feed-forward); qd_linear_i8_geglu_q_ok tells.
+extern "C" int qd_linear_i8_geglu_q_ok(int K, int N) { return K == 320 && N == 2560 ? 1 : 0; }
+
+extern "C" int qd_linear_i8_geglu_q(const void* x, const float* sa, int M, int K, int lda, const void* w,
+                                    const float* sw, const void* bias, int N, int8_t* y8, int ldy8, float* sa8,
+                                    void* stream) {
+  QD_REQUIRE(qd_linear_i8_geglu_q_ok(K, N), "qd_linear_i8_geglu_q: K = 320, N = 2560 only");
+  QD_REQUIRE(x && sa && w && sw && y8 && sa8, "null pointer");
+  QD_REQUIRE(lda >= K && lda % 16 == 0 && ldy8 >= N / 2 && ldy8 % 16 == 0, "lda / ldy8: >= the row, multiples of 16");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(y8) & 15) == 0 && (reinterpret_cast<uintptr_t>(sw) & 15) == 0,
+             "x, w, y8, sw must be 16-B aligned");
+  QD_REQUIRE(!bias || (reinterpret_cast<uintptr_t>(bias) & 7) == 0, "bias must be 8-B aligned");
+  QD_REQUIRE((double)M * lda < 2147483648.0, "activation exceeds the 2 GiB buffer-addressing range");
+  if (M <= 0) return 0;
+  GemmArgs p{};
+  p.a = (const f16*)x;
+  p.lda = lda / 2;
+  p.b = w;
+  p.bias = (const f16*)bias;
+  p.M = M;
+  p.N = N;
+  p.K = K / 2;
+  p.sa = sa;
+  p.sw = sw;
+  p.i8 = 1;
+  p.a_bytes = (unsigned)((long)(M - 1) * lda + K);
+  p.b_bytes = (unsigned)((long)N * K);
+  k_geglu_i8q<5, 20><<<(M + 63) / 64, 512, 0, S(stream)>>>(p, y8, ldy8, sa8);
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int qd_linear_i8_ln(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
                                const void* bias, const void* residual, void* y, int N, int ldy, int epi,
                                const void* ln_gamma, const void* ln_beta, float ln_eps, void* ln_y, int8_t* ln_y8,
@@ -3541,6 +3921,7 @@ extern "C" int qd_conv2d_i8(const void* x, const float* sa, int n, int h, int w,
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(wt) & 15) == 0,
              "x and w must be 16-B aligned");
   GemmArgs p{};
+  p.epi_lds = g_epi_lds;
   const int H = upsample2x ? 2 * h : h, W = upsample2x ? 2 * w : w;
   const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   p.a = (const f16*)x;
@@ -3631,6 +4012,7 @@ extern "C" int qd_linear_fp8(const void* x, const float* sa, int M, int K, int l
              "operands exceed the 2 GiB buffer-addressing range");
   if (M == 0) return 0;
   GemmArgs p{};
+  p.epi_lds = g_epi_lds;
   p.a = (const f16*)x;
   p.lda = lda / 2;
   p.b = w;
