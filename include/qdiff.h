@@ -221,6 +221,17 @@ int qd_quant_samples_i8_amax(const void* x, int n, long per_sample, const float*
 int qd_linear_i8(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
                  const void* bias, const void* residual, void* y, int N, int ldy, int epi, float* amax,
                  int rows_per_sample, float* ws, long ws_elems, void* stream);
+/* int8-MFMA mode, diffusers FeedForward at the SD1.5 64x64 level: the GEGLU projection (w [N][K] codes
+ * with rows interleaved in 16-row [hidden | gate] blocks, fp32 per-row scales sw, fp16 bias) of
+ * per-token codes x / sa, GEGLU, and the per-token int8 codes y8 [M, N / 2] (ldy8) + fp32 scales
+ * sa8 [M] of its output - ff.net.2's input - in ONE launch; the fp16 GEGLU output never reaches
+ * memory.  Bit-identical to qd_linear_i8(..., QD_EPI_GEGLU) followed by qd_quant_rows_i8.  Replaces
+ * ff.net.0 + ff.net.2's input quantization (reference: diffusers GEGLU around quantize/
+ * fake_quant.py:223's F.linear).  Shapes: qd_linear_i8_geglu_q_ok(K, N) (K 320, N 2560). */
+int qd_linear_i8_geglu_q_ok(int K, int N);
+int qd_linear_i8_geglu_q(const void* x, const float* sa, int M, int K, int lda, const void* w, const float* sw,
+                         const void* bias, int N, int8_t* y8, int ldy8, float* sa8, void* stream);
+
 /* Row-complete LayerNorm epilogue (diffusers BasicTransformerBlock: attn.to_out + residual ->
  * norm2 / norm3): y = the qd_linear_fwd / qd_linear_i8 output with QD_EPI_RESIDUAL (epi must
  * hold it; no amax / GEGLU / GELU-tanh), AND LayerNorm(y) over each row (gamma / beta fp16 [N],

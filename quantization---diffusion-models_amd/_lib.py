@@ -83,6 +83,8 @@ SIGNATURES = {
     "qd_linear_i8": [P, P, I, I, I, P, P, P, P, P, I, I, I, P, I, P, ctypes.c_long, P],
     "qd_linear_ln": [P, I, I, I, P, I, P, P, I, P, P, P, I, I, I, P, P, F, P, P, P, P, ctypes.c_long, P],
     "qd_linear_i8_ln": [P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, P, P, P, P],
+    "qd_linear_i8_geglu_q_ok": [I, I],
+    "qd_linear_i8_geglu_q": [P, P, I, I, I, P, P, P, I, P, I, P, P],
     "qd_linear_ln_ok": [I],
     "qd_conv2d_i8": [P, P, I, I, I, I, I, P, P, I, I, I, I, I, I, P, P, P, I, P, P, I, P, P, ctypes.c_long, P],
     "qd_groupnorm_part": [P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, P, P, P, P],

@@ -106,6 +106,10 @@ struct GemmArgs {
   // epilogue form (measurement knob qd_gemm_epi_direct): 0 = stores straight from the MFMA fragments
   // (permlane16 pairs -> 16-B stores) wherever the epilogue allows it; 1 = always through the LDS C tile
   int epi_lds;
+  // persistent int8 LDS-DMA linears (qd_gemm_force 160+ / 170+): the launch's block count; each block
+  // runs logical tiles bid, bid + grid, ... and stages the next tile's first K steps under the
+  // current tile's epilogue whenever that epilogue stores straight from the fragments (no LDS)
+  int pgrid;
 };
 
 constexpr int BK = 64;
@@ -421,6 +425,24 @@ constexpr int ln_per(int bn) { return ln_lpr(bn) ? bn / 8 / ln_lpr(bn) : 0; }
 // CONV: a conv kernel's epilogue (no GEGLU / GELU-tanh: those are linear-only, compiled out);
 // DIRECT: the direct-store path is compiled in (kernels whose epilogues always take the LDS path - the
 // int8 halo conv's GroupNorm slot statistics - leave it out: its registers would spill there)
+// whether gemm_epilogue stores straight from the fragments (see there): the tile shapes whose pair
+// loop fits the register budget (TN 8: spills), and the epilogues that need no row-complete / slot
+// view of the tile (plain, bias, residual, pre-residual amax, GEGLU at TN % 4 == 0, GELU-tanh)
+template <int TM, int TN, bool DIRECT>
+constexpr bool epi_direct_ok() { return DIRECT && TN >= 2 && TN <= 5 && TM * ((TN + 1) / 2) <= 20; }
+template <int BN, int TM, int TN, bool CONV, bool DIRECT>
+__device__ __forceinline__ bool epi_direct(const GemmArgs& p) {
+  const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
+  const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
+  const bool geglu = !CONV && (p.epi & QD_EPI_GEGLU) != 0;
+  const bool gtanh = !CONV && (p.epi & QD_EPI_GELU_TANH) != 0;
+  const bool post = has_res && do_amax && (p.epi & QD_EPI_AMAX_POST) && !geglu && !gtanh;
+  const bool gn = (p.epi & QD_EPI_GNSTATS) && p.gnp && !geglu && !gtanh;
+  const bool ln = BN == 320 && (p.epi & QD_EPI_LN) && !geglu && !gtanh;
+  const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd && !geglu && !gtanh;
+  return epi_direct_ok<TM, TN, DIRECT>() && !p.epi_lds && !gn && !ln && !cadd && !post && (!geglu || TN % 4 == 0);
+}
+
 template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH, bool CONV = false, bool DIRECT = true>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM][TN], f16* smem, int m0, int n0,
                                               int wm0, int wn0, int split) {
@@ -487,8 +509,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // pair - one 16-B store (or residual load) per lane and pair, 16 rows x 64 B per instruction.
     // Same arithmetic per element as the LDS pass below, so the output bits are identical.
     // (an odd TN's last fragment stores its 4 columns as one 8-B store per lane)
-    constexpr bool DIRECT_OK = DIRECT && TN >= 2 && TN <= 5 && TM * ((TN + 1) / 2) <= 20;  // (TN 8: spills)
-    const bool direct = DIRECT_OK && !p.epi_lds && !gn && !ln && !cadd && !post && (!geglu || TN % 4 == 0);
+    constexpr bool DIRECT_OK = epi_direct_ok<TM, TN, DIRECT>();
+    const bool direct = epi_direct<BN, TM, TN, CONV, DIRECT>(p);
     const bool pre_res = has_res && !fres && !geglu && !direct;
     // post-residual amax: the residual in the fragments' layout (4 consecutive columns of one row
     // per lane and fragment), all TM x TN 8-B loads issued before any is used
@@ -636,7 +658,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
             w = __builtin_bit_cast(u32x4, v);
           }
           const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
+#ifdef QD_ABLATE_EPI_STORES  // diagnostic build: the direct epilogue's stores dropped (values kept live)
+          asm volatile("" ::"v"(w), "v"(off));
+#else
           __builtin_amdgcn_raw_buffer_store_b128(w, yrs, (row_ok && n < oN) ? (int)off : (int)OOB, 0, 0);
+#endif
         };
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -1294,10 +1320,22 @@ constexpr int dma_waves_per_eu_w4(int bm, int bn, int st, int nt, int bkt) {
                    : 1;
 }
 
+// PERSIST (int8 linears, lock-step pipeline, unsplit): a grid of p.pgrid blocks; block b runs the
+// logical tiles b, b + grid, ... (XCD-remapped like the one-tile grid).  After a tile's K loop the
+// first ST-1 K steps of the block's next tile are issued into the (now free) stages BEFORE the tile's
+// epilogue when that epilogue touches no LDS (direct stores, no column amax), so the next tile's
+// L2 -> LDS traffic runs under this tile's scaling, conversions and output stores; the next tile's
+// first K step then waits for every outstanding memory op (its DMA is older than the stores).  The
+// register cap is half the one-tile kernel's occupancy (the tile loop keeps the next tile's DMA
+// state and the loop-invariant lane coordinates live through the epilogue: at the one-tile cap the
+// 128 x 160 tile spills ~50 VGPRs).
 template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false,
-          bool F8 = false, bool W4 = false>
-__global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, BN, ST, 64 * WGM * WGN, BKT)
-                                                     : dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
+          bool F8 = false, bool W4 = false, bool PERSIST = false>
+__global__ void __launch_bounds__(64 * WGM * WGN,
+                                  W4        ? dma_waves_per_eu_w4(BM, BN, ST, 64 * WGM * WGN, BKT)
+                                  : PERSIST ? (dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT) / 2 > 0
+                                                   ? dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT) / 2 : 1)
+                                            : dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT))
     k_gemm_dma(GemmArgs p) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -1312,6 +1350,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
                 "fp8: one 128-code group per 128-B LDS row, no split-K, the scale row in one DMA piece");
   static_assert(!W4 || (!I8 && !F8 && PIPE == 0 && AMODE == AM_LINEAR && BN <= 512),
                 "int4: lock-step pipeline, linear A operand, one scale piece");
+  static_assert(!PERSIST || (I8 && PIPE == 0 && AMODE == AM_LINEAR && !SPLIT), "persistent: int8 linears, unsplit");
   using AL = ADma<BM, NT, AMODE, BKT>;
   using BL = std::conditional_t<W4, BDma4<BN, NT, BKT>, BDma<BN, NT, BKT>>;
   __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
@@ -1319,14 +1358,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
   const int ntile = nbm * nbn;
   const int nwg = ntile * p.splits;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  auto xmap = [&](int b) {  // (logical) block index -> XCD-contiguous tile index
+    const int xcd = b & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  };
+  int lt = blockIdx.x;
   int bm, bn, split;
-  tile_of(p, wg, nbm, nbn, bm, bn, split);
-  const int m0 = bm * BM, n0 = bn * BN;
-  const int kbeg = split * p.kps;
-  const int kend = min(p.K, kbeg + p.kps);
+  tile_of(p, xmap(lt), nbm, nbn, bm, bn, split);
+  int m0 = bm * BM, n0 = bn * BN;
+  int kbeg = split * p.kps;
+  int kend = min(p.K, kbeg + p.kps);
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1353,6 +1395,21 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
 
   f32x4 acc[TM][TN];
   i32x4 iacc[I8 ? TM : 1][I8 ? TN : 1];
+  // the first ST-1 K steps of the tile whose K range starts at kb (nks steps)
+  auto prologue = [&](int kb, int nks) {
+#pragma unroll
+    for (int s = 0; s < ST - 1; ++s) {
+      if (s < nks) {
+        al.issue(p, kb + s * BKT, smem + s * SSZ, wid);
+        bl.issue(p, kb + s * BKT, smem + s * SSZ + ASZ, wid);
+        issue_scale(kb + s * BKT, smem + s * SSZ);
+      }
+    }
+  };
+  int nk = (kend - kbeg + BKT - 1) / BKT;
+  prologue(kbeg, nk);
+  bool drain = false;  // (PERSIST) a later tile: its first K step waits for every outstanding op
+  for (;;) {
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1360,26 +1417,20 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
       acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       if constexpr (I8) iacc[i][j] = (i32x4){0, 0, 0, 0};
     }
-
-  const int nk = (kend - kbeg + BKT - 1) / BKT;
-#pragma unroll
-  for (int s = 0; s < ST - 1; ++s) {
-    if (s < nk) {
-      al.issue(p, kbeg + s * BKT, smem + s * SSZ, wid);
-      bl.issue(p, kbeg + s * BKT, smem + s * SSZ + ASZ, wid);
-      issue_scale(kbeg + s * BKT, smem + s * SSZ);
-    }
-  }
   unsigned m64 = 0, m54 = 0;
   if constexpr (W4) w4_magics(m64, m54);
+  // (PERSIST: the fragment addresses are re-derived per tile from an opaque copy of the lane
+  // coordinates - hoisted out of the tile loop they stay live through every epilogue and spill)
+  int frl = fr, fql = fq;
+  if constexpr (PERSIST) asm volatile("" : "+v"(frl), "+v"(fql));
   auto read_frags = [&](const f16* As, int ks, f16x8 (&af)[TM], f16x8 (&bf)[TN]) {
     const f16* Bs = As + ASZ;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BKT>(wm0 + i * 16 + fr, ks * 4 + fq));
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<BKT>(wm0 + i * 16 + frl, ks * 4 + fql));
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      if constexpr (W4) bf[j] = w4_frag<BKT>(Bs, wn0 + j * 16 + fr, ks, fq, BDma4<BN, NT, BKT>::CODE_H, m64, m54);
-      else bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BKT>(wn0 + j * 16 + fr, ks * 4 + fq));
+      if constexpr (W4) bf[j] = w4_frag<BKT>(Bs, wn0 + j * 16 + frl, ks, fql, BDma4<BN, NT, BKT>::CODE_H, m64, m54);
+      else bf[j] = *reinterpret_cast<const f16x8*>(Bs + swz_t<BKT>(wn0 + j * 16 + frl, ks * 4 + fql));
     }
   };
   auto mfmas = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
@@ -1411,7 +1462,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
   if constexpr (PIPE == 0) {
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      sync(min(ST - 2, nk - 1 - kt));
+      if (PERSIST && kt == 0 && drain) {
+        wait_vm<0>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      } else {
+        sync(min(ST - 2, nk - 1 - kt));
+      }
       if (kt + ST - 1 < nk) {
         int nx = cur + ST - 1;
         if (nx >= ST) nx -= ST;
@@ -1488,7 +1546,46 @@ __global__ void __launch_bounds__(64 * WGM * WGN, W4 ? dma_waves_per_eu_w4(BM, B
       for (int j = 0; j < TN; ++j) acc[i][j] *= s;
     }
   }
-  gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, AMODE != AM_LINEAR>(p, acc, smem, m0, n0, wm0, wn0, split);
+  if constexpr (PERSIST) {
+    const int ln = lt + (int)gridDim.x;
+    const bool more = ln < nwg;
+    int m0n = 0, n0n = 0, kbn = 0, ken = 0, bmn = 0, bnn = 0, spn = 0;
+    if (more) {
+      tile_of(p, xmap(ln), nbm, nbn, bmn, bnn, spn);
+      m0n = bmn * BM;
+      n0n = bnn * BN;
+      kbn = spn * p.kps;
+      ken = min(p.K, kbn + p.kps);
+    }
+    const int nkn = (ken - kbn + BKT - 1) / BKT;
+    // the epilogue below stores from the fragments and keeps no column maxima in LDS
+    const bool early = more && epi_direct<BN, TM, TN, false, true>(p) && !((p.epi & QD_EPI_AMAX) && p.amax);
+    if (early) {
+      al.init(p, m0n, kbn, wid);
+      bl.init(p, n0n, wid);
+      prologue(kbn, nkn);
+    }
+    gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, false>(p, acc, smem, m0, n0, wm0, wn0, split);
+    if (!more) break;
+    if (!early) {
+      __syncthreads();  // the epilogue's LDS C tile / column maxima are read
+      al.init(p, m0n, kbn, wid);
+      bl.init(p, n0n, wid);
+      prologue(kbn, nkn);
+    }
+    lt = ln;
+    m0 = m0n;
+    n0 = n0n;
+    split = spn;
+    kbeg = kbn;
+    kend = ken;
+    nk = nkn;
+    drain = true;
+  } else {
+    gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, AMODE != AM_LINEAR>(p, acc, smem, m0, n0, wm0, wn0, split);
+    break;
+  }
+  }
 }
 
 // ---- ping-pong GEMM (256 x BN tile, 8 waves, BK 32, 4-stage LDS-DMA ring) ----------------
@@ -2672,15 +2769,18 @@ __device__ __forceinline__ int8_t q_i8g(float x, float s, double rs) {  // (quan
   return (int8_t)__builtin_rintf((float)t);
 }
 
-template <int KS, int NCH>
-__global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __restrict__ y8, int ldy8,
-                                                     float* __restrict__ sa8) {
-  constexpr int BM = 64, NT = 512, CH = 128, TM = 2, SLAB = CH * 32, CHUNK = KS * SLAB;
+// WGM = 1: 4 waves (one per SIMD, the whole 512-register file: the packed GEGLU outputs of the 64
+// rows, NCH x 16 VGPRs); WGM = 2: 8 waves, two per SIMD (32 rows each, NCH x 8 VGPRs of outputs).
+// Wave (wm, wn) takes rows 64 / WGM * wm .. and interleave block wn of each chunk.
+template <int KS, int NCH, int WGM>
+__global__ void __launch_bounds__(256 * WGM, 1) k_geglu_i8q(GemmArgs p, int8_t* __restrict__ y8, int ldy8,
+                                                           float* __restrict__ sa8) {
+  constexpr int BM = 64, NT = 256 * WGM, CH = 128, TM = 4 / WGM, SLAB = CH * 32, CHUNK = KS * SLAB;
   constexpr int NOUT = NCH * 64;               // GEGLU outputs per row
   constexpr int CP = NOUT + 16;                // code-tile row pitch (bytes): 16 rows x 4 B conflict-free
   constexpr int RING = 3 * CHUNK;              // halves
+  constexpr int ASZ = KS * BM * 32;            // the A tile: KS slabs of 64 rows x 64 B
   static_assert(BM * CP <= RING * 2, "code tile fits the ring");
-  constexpr int ASZ = KS * BM * 32;             // the A tile: KS slabs of 64 rows x 64 B
   __shared__ __attribute__((aligned(16))) f16 smem[RING + ASZ + NCH * CH * 3 + 2 * 4 * BM];
   f16* const As = smem + RING;
   float* const swl = reinterpret_cast<float*>(smem + RING + ASZ);             // [N] fp32 weight scales
@@ -2689,15 +2789,13 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
   const int m0 = blockIdx.x * BM;
   const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid >> 2, wn = wid & 3, r0 = wm * 16 * TM;
 
-  // weight scales and bias of all N rows into LDS (plain loads, drained before any DMA)
   for (int n = threadIdx.x; n < NCH * CH; n += NT) {
     swl[n] = p.sw[n];
     bl16[n] = p.bias ? p.bias[n] : (f16)0.f;
   }
-  // the block's A tile into LDS (64-B slab rows, the ring's swizzle): 16-B piece e = (row, ks, chunk);
-  // in registers it would hold 40 VGPRs beside the 80 of the packed GEGLU outputs (spills)
+  // the block's A tile into LDS (64-B slab rows, the ring's swizzle)
   const __amdgpu_buffer_rsrc_t ars = rsrc(p.a, p.a_bytes);
   for (int e = threadIdx.x; e < BM * KS * 4; e += NT) {
     const int row = e / (KS * 4), rem = e - row * (KS * 4), ks = rem >> 2, ch = rem & 3;
@@ -2707,7 +2805,7 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
   }
   float sam[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) sam[i] = p.sa[min(m0 + wm * 32 + i * 16 + fr, p.M - 1)];
+  for (int i = 0; i < TM; ++i) sam[i] = p.sa[min(m0 + r0 + i * 16 + fr, p.M - 1)];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -2717,19 +2815,17 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) bl.issue(p, ks * 32, dst + ks * SLAB, wid);
   };
+  constexpr int PER = BDma<CH, NT, 32>::L;  // DMA instructions per wave and K slab
   issue_chunk(0, smem);
   issue_chunk(1, smem + CHUNK);
 
-  // (packed: two fp16 per VGPR - unpacked the 40 x 4 values alone would take 160 registers)
-  u32x2 vals[NCH][TM];
-  f16x2v m2[TM];  // running packed |value| maxima of each row block (exact)
+  unsigned vlo[NCH][TM], vhi[NCH][TM];  // packed fp16 GEGLU outputs: columns 4fq + {0, 1} | {2, 3}
+  f16x2v m2[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) m2[i] = (f16x2v){(f16)0.f, (f16)0.f};
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    // own DMA of chunk c landed (chunk c + 1 may stay in flight), then the block barrier: every
-    // wave's share landed and chunk c - 1's slot is free for chunk c + 2
-    if (c + 1 < NCH) wait_vm<KS>();
+    if (c + 1 < NCH) wait_vm<KS * PER>();
     else wait_vm<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -2747,7 +2843,7 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
 #pragma unroll
       for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const f16x8*>(Bs + ks * SLAB + swz_t<32>(wn * 32 + j * 16 + fr, fq));
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + ks * BM * 32 + swz_t<32>(wm * 32 + i * 16 + fr, fq));
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + ks * BM * 32 + swz_t<32>(r0 + i * 16 + fr, fq));
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -2755,13 +2851,11 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
           iacc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, bf[j]),
                                                              __builtin_bit_cast(i32x4, af[i]), iacc[i][j], 0, 0, 0);
     }
-    // GEGLU of the chunk: rows n = c CH + 32 wn + 16 j + 4 fq + r
     const int nl = c * CH + wn * 32 + fq * 4;
     const f32x4 sw0 = *reinterpret_cast<const f32x4*>(swl + nl), sw1 = *reinterpret_cast<const f32x4*>(swl + nl + 16);
     const f16x4 b0 = *reinterpret_cast<const f16x4*>(bl16 + nl), b1 = *reinterpret_cast<const f16x4*>(bl16 + nl + 16);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      __builtin_amdgcn_sched_barrier(0);  // one row block's GELU temporaries at a time
       f16x4 hv, gv;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -2772,38 +2866,39 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
       for (int r = 0; r < 4; r += 2) {
         const f32x2 g2 = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
         const f16x2v o = {(f16)((float)hv[r] * (float)(f16)g2.x), (f16)((float)hv[r + 1] * (float)(f16)g2.y)};
-        vals[c][i][r >> 1] = __builtin_bit_cast(unsigned, o);
+        if (r == 0) vlo[c][i] = __builtin_bit_cast(unsigned, o);
+        else vhi[c][i] = __builtin_bit_cast(unsigned, o);
         m2[i] = __builtin_elementwise_max(m2[i], __builtin_elementwise_abs(o));
       }
+      // pin the chunk's outputs here: left alone the compiler sinks this pure VALU math past the
+      // later chunks' barriers and keeps every chunk's accumulators alive (hundreds of registers)
+      asm volatile("" : "+v"(vlo[c][i]), "+v"(vhi[c][i]));
     }
-    __builtin_amdgcn_sched_barrier(0);
   }
-  // row maxima: the lane's values, its 4 lane groups (fq), the 4 waves wn sharing the rows
-  float mx[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     float m = fmaxf((float)m2[i][0], (float)m2[i][1]);
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
-    mx[i] = m;
-    if (fq == 0) rmx[wn * BM + wm * 32 + i * 16 + fr] = m;
+    if (fq == 0) rmx[wn * BM + r0 + i * 16 + fr] = m;
   }
   __syncthreads();  // (also: every wave's last ring reads are done - the code tile reuses the ring)
   char* const ct = reinterpret_cast<char*>(smem);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int rl = wm * 32 + i * 16 + fr;
+    const int rl = r0 + i * 16 + fr;
     const float m = fmaxf(fmaxf(rmx[rl], rmx[BM + rl]), fmaxf(rmx[2 * BM + rl], rmx[3 * BM + rl]));
     const float s = fq_scale(m, 127);
     const double rs = rcp_exact(s);
     if (wn == 0 && fq == 0 && m0 + rl < p.M) sa8[m0 + rl] = s;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      __builtin_amdgcn_sched_barrier(0);  // (hoisted, the unpacked values of every chunk spill)
       unsigned w = 0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        w |= (unsigned)(uint8_t)q_i8g((float)__builtin_bit_cast(f16x2v, vals[c][i][r >> 1])[r & 1], s, rs) << (8 * r);
+      for (int r = 0; r < 4; ++r) {
+        const f16x2v pr = __builtin_bit_cast(f16x2v, r < 2 ? vlo[c][i] : vhi[c][i]);
+        w |= (unsigned)(uint8_t)q_i8g((float)pr[r & 1], s, rs) << (8 * r);
+      }
       *reinterpret_cast<unsigned*>(ct + rl * CP + c * 64 + wn * 16 + fq * 4) = w;
     }
   }
@@ -2820,6 +2915,7 @@ __global__ void __launch_bounds__(512, 1) k_geglu_i8q(GemmArgs p, int8_t* __rest
 // kind 0: register-staged k_gemm (any weight format); kind 1: LDS-DMA k_gemm_dma (F16 weights)
 struct Plan {
   int kind, bm, bn, var, splits, kps;
+  int pdiv = 0;  // persistent int8 DMA linears: tiles per block (grid = tiles / pdiv)
 };
 
 // LDS-DMA variants: tile, wave grid, LDS stages
@@ -2877,9 +2973,11 @@ extern "C" int qd_gemm_force(int variant) {
   const int v = variant >= 1000 ? variant % 1000 : variant, sp = variant >= 1000 ? variant / 1000 : 0;
   QD_REQUIRE(v == -1 || (v >= 0 && v < 4) ||
                  (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 203) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
-                 (v >= 130 && v <= 134) || (v >= 140 && v <= 149),
+                 (v >= 130 && v <= 134) || (v >= 140 && v <= 151) || (v >= 160 && v <= 167) || (v >= 170 && v <= 177),
              "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..117, fp8: 120..123), 200-203 halo conv, "
-             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-149); + 1000 * s: split-K count s (1 = unsplit)");
+             "300-304 ping-pong (int8: 130-134, int8 halo conv 140-149, fused GEGLU codes 150 / 151, persistent "
+             "int8 DMA linears 160-167 / 170-177: variants 10-17 with 2 / 4 tiles per block); + 1000 * s: "
+             "split-K count s (1 = unsplit)");
   QD_REQUIRE(sp <= 32, "qd_gemm_force: split count above 32");
   g_force = v;
   g_split = sp;
@@ -3605,6 +3703,13 @@ template <int V, int AMODE, bool SPLIT>
 static void launch_i8_v(const GemmArgs& p, hipStream_t st) {
   constexpr DmaVar d = kDmaC[V];
   static_assert(d.bkt == 32 && d.pipe == 0, "int8 variants use the 64-B row layout");
+  if constexpr (AMODE == AM_LINEAR && !SPLIT && V >= 10 && V <= 17 && V != 12 && V != 13) {
+    if (p.pgrid > 0) {
+      k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, false, true, false, false, true>
+          <<<p.pgrid, 64 * d.wgm * d.wgn, 0, st>>>(p);
+      return;
+    }
+  }
   const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
   k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT, true><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
 }
@@ -3698,11 +3803,20 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   }
   int var = N % 160 == 0 ? 10 : 11;
   if (g_force >= 110 && g_force <= 117) var = g_force - 100;
+  int pdiv = 0;
+  if (g_force >= 160 && g_force <= 177 && g_force % 10 <= 7) {
+    var = 10 + g_force % 10;
+    pdiv = g_force < 170 ? 2 : 4;
+  }
   if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
   if (gn && rows_per_sample % kDmaC[var].bm != 0) var = rows_per_sample % 128 == 0 ? 11 : 15;  // tile in one sample
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];
   Plan pl{1, d.bm, d.bn, var, 1, Kh};
+  if (pdiv && var != 12 && var != 13) {  // persistent: unsplit
+    pl.pdiv = pdiv;
+    return pl;
+  }
   const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
   const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
   const int per_cu = std::max(1, std::min(by_lds, by_waves));
@@ -3748,6 +3862,12 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   p.splits = pl.splits;
   p.kps = pl.kps;
   p.mfast = AMODE == AM_LINEAR ? 0 : block_order(p, false, 1.0, 1.0);  // int8 codes on both sides (half view)
+  p.pgrid = 0;
+  if (AMODE == AM_LINEAR && pl.kind == 1 && pl.splits == 1 && pl.pdiv) {
+    const long tiles = (long)((p.M + pl.bm - 1) / pl.bm) * ((p.N + pl.bn - 1) / pl.bn);
+    const long g = (tiles + pl.pdiv - 1) / pl.pdiv;
+    p.pgrid = (int)std::min(tiles, (g + 7) / 8 * 8);  // (a multiple of 8: logical tiles keep their XCD)
+  }
   auto halo = [&]() {  // the kernel reads p.splits itself (int32 slabs when split)
     if (pl.var == 2) launch_halo_i8<160, 4>(p, st);
     else if (pl.var == 3) launch_halo_i8<160, 5>(p, st);
@@ -3900,7 +4020,10 @@ extern "C" int qd_linear_i8_geglu_q(const void* x, const float* sa, int M, int K
   p.i8 = 1;
   p.a_bytes = (unsigned)((long)(M - 1) * lda + K);
   p.b_bytes = (unsigned)((long)N * K);
-  k_geglu_i8q<5, 20><<<(M + 63) / 64, 512, 0, S(stream)>>>(p, y8, ldy8, sa8);
+  // 8 waves, two per SIMD (the default, 150); 151: 4 waves with the whole register file (slower:
+  // 110 vs 83 us at M 32768, profiles/r05h_geglu_q_bench.log - one wave per SIMD hides nothing)
+  if (g_force == 151) k_geglu_i8q<5, 20, 1><<<(M + 63) / 64, 256, 0, S(stream)>>>(p, y8, ldy8, sa8);
+  else k_geglu_i8q<5, 20, 2><<<(M + 63) / 64, 512, 0, S(stream)>>>(p, y8, ldy8, sa8);
   QD_CHECK_LAUNCH();
   return 0;
 }

@@ -412,20 +412,28 @@ __global__ void __launch_bounds__(256) k_gn_apply(GnIn in, int hw, int c, int ro
                                                   const float* __restrict__ amax_n = nullptr,
                                                   int8_t* __restrict__ y8 = nullptr, float* __restrict__ sa8 = nullptr) {
   const int chunk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (chunk * 8 >= c) return;
-  const int ch = chunk * 8;
   const long n = blockIdx.y;
   float s8 = 0.f;
   double r8 = 0.0;
   if constexpr (I8) {
-    // amax_n[n][g] (qmax carries the group count here): max over the sample's groups
-    const float* ag = amax_n + n * qmax;
-    float m = 0.f;
-    for (int gi = 0; gi < qmax; ++gi) m = fmaxf(m, ag[gi]);
-    s8 = fq_scale(m, 127);
+    // amax_n[n][g] (qmax carries the group count here, <= 64): max over the sample's groups - one
+    // load per lane of the block's first wave (always full: blocks hold >= 64 threads) and a wave
+    // reduction (max is exact), handed to the block through LDS, instead of qmax loads per thread
+    // (a partial last wave's shuffles would read inactive lanes)
+    __shared__ float smx;
+    const int flat = threadIdx.y * blockDim.x + threadIdx.x;
+    if (flat < 64) {
+      float m = flat < qmax ? amax_n[n * qmax + flat] : 0.f;
+      m = wave_max(m);
+      if (flat == 0) smx = m;
+    }
+    __syncthreads();
+    s8 = fq_scale(smx, 127);
     r8 = rcp_exact(s8);
     if (chunk == 0 && blockIdx.z == 0 && threadIdx.y == 0) sa8[n] = s8;
   }
+  if (chunk * 8 >= c) return;
+  const int ch = chunk * 8;
   const int r0 = blockIdx.z * rows_per_block, r1 = min(hw, r0 + rows_per_block);
   float2 k[8];
   float sq[8];
@@ -716,6 +724,7 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
     return 0;
   }
   if (y8) {  // (the qmax argument carries the group count of amax_n[n][group])
+    QD_REQUIRE(groups <= 64, "int8 output: at most 64 groups (one per lane of the apply pass's reduction)");
     if (xf && silu) k_gn_apply<1, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
     else if (xf) k_gn_apply<1, 0, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
     else if (silu) k_gn_apply<0, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, sa8);
@@ -844,6 +853,7 @@ extern "C" int qd_groupnorm_part(const float* part, const void* x, const float* 
                                             (const f16*)gamma, (const f16*)beta, silu, y8 != nullptr, coef, amax,
                                             amax_n, reinterpret_cast<const float4*>(part2), xamax);
   const dim3 ga(g.gx, n, g.z), ba(g.bx, g.by);
+  QD_REQUIRE(!y8 || groups <= 64, "int8 output: at most 64 groups (one per lane of the apply pass's reduction)");
   if (y8) {  // (the qmax argument carries the group count of amax_n[n][group])
     if (silu) k_gn_apply<0, 1, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, scales);
     else k_gn_apply<0, 0, false, true><<<ga, ba, 0, st>>>(in, hw, c, g.rpb, coef, groups, amax, nullptr, amax_n, y8, scales);

@@ -706,6 +706,9 @@ I8_VARIANTS = (110, 111, 112, 113, 114, 115, 116, 117,  # qd_gemm_force ids: LDS
 # 3x3 conv, activation halo staged once per 64-code chunk: 256-pixel tiles (BN 160 / 128; 142-144 deeper
 # weight rings), 145-147 128-pixel tiles with two blocks per CU, 148 / 149 one 8x8 image per tile
 I8_HALO_VARIANTS = (140, 141, 142, 143, 144, 145, 146, 147, 148, 149)
+# persistent LDS-DMA linears (unsplit): variants 10, 11, 14-17 with 2 (160 + v) / 4 (170 + v) tiles per
+# block, the next tile's first K steps staged under the current tile's epilogue
+I8_PERSIST_VARIANTS = (160, 161, 164, 165, 166, 167, 170, 171, 174, 175, 176, 177)
 
 
 def quant_rows_i8(x2d, out=None, scales=None):
@@ -868,12 +871,50 @@ def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, row
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        c = _choose(key, list(I8_VARIANTS) + ([] if epi & (EPI_GEGLU | EPI_AMAX_POST) else _i8_split_cands(M, N, Kd)),
+        c = _choose(key, list(I8_VARIANTS) + list(I8_PERSIST_VARIANTS) +
+                    ([] if epi & (EPI_GEGLU | EPI_AMAX_POST) else _i8_split_cands(M, N, Kd)),
                     lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
     launch(c if c is not None else -1, out, amax, epi, False)
     return out
+
+
+_GEGLU_Q_OK = {}
+
+
+def linear_i8_geglu_q_ok(k, n):
+    """True when linear_i8_geglu_q takes K = k input codes and N = n interleaved projection rows."""
+    if (k, n) not in _GEGLU_Q_OK:
+        _GEGLU_Q_OK[(k, n)] = bool(_lib.load().qd_linear_i8_geglu_q_ok(k, n))
+    return _GEGLU_Q_OK[(k, n)]
+
+
+def linear_i8_geglu_q(xq, sa, wq, sw, bias=None):
+    """(codes, scales) = quant_rows_i8(linear_i8(xq, sa, wq, sw, bias=bias, geglu=True)) in ONE launch
+    (qd_linear_i8_geglu_q): the int8 GEGLU projection and the per-token int8 codes of its output,
+    the fp16 GEGLU output never materialised.  wq [N, K] int8 rows interleaved as geglu_interleave_rows,
+    sw [N] fp32, bias [N] fp16; linear_i8_geglu_q_ok(K, N) must hold."""
+    if xq.dtype != torch.int8 or wq.dtype != torch.int8 or not xq.is_cuda:
+        raise ValueError("int8 GEMM operands must be int8 HIP tensors")
+    if xq.dim() != 2 or xq.stride(1) != 1 or not wq.is_contiguous():
+        raise ValueError("xq must be 2-D with unit column stride, wq contiguous")
+    M, Kd = xq.shape
+    N = wq.shape[0]
+    if not linear_i8_geglu_q_ok(Kd, N):
+        raise ValueError(f"linear_i8_geglu_q: no fused kernel for K {Kd}, N {N}")
+    _chk(sw, "sw", torch.float32)
+    if bias is not None:
+        _chk(bias, "bias")
+    y8 = _empty((M, N // 2), torch.int8, xq.device)
+    sa8 = _empty((M,), torch.float32, xq.device)
+    _force(_OVERRIDE if _OVERRIDE is not None else -1)  # (150 / 151: the two wave layouts; benchmarks)
+    try:
+        _lib.call("qd_linear_i8_geglu_q", _p(xq), _p(sa), M, Kd, xq.stride(0), _p(wq), _p(sw), _p(bias), N, _p(y8),
+                  N // 2, _p(sa8), _stream())
+    finally:
+        _force(-1)
+    return y8, sa8
 
 
 def conv2d_i8(xq, sa, wq, sw, ci, stride=1, pad=0, upsample2x=False, bias=None, residual=None, out=None, amax=None,

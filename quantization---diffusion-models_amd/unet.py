@@ -943,13 +943,20 @@ def block_fwd(blk, t, n, s, ctx_kv, want_amax=False, t_fq=None):
     o = K.attention(q, k, v, a2.heads)
     pj = blk.ff.net[0].proj
     t, h = _out_ln(a2.to_out[0], o.view(-1, c), t, blk.norm3, lin_i8(pj) and pj.output_quant_name == "None")
-    g = ff_geglu(blk.ff.net[0].proj, h)
     fo = blk.ff.net[2]
-    if want_amax and lin_i8(fo) and fo.output_quant_name == "None" and g.shape[0] >= I8_MIN_ROWS:
+    if isinstance(h, tuple) and lin_i8(fo) and fo.output_quant_name == "None" and h[0].shape[0] >= I8_MIN_ROWS \
+            and K.linear_i8_geglu_q_ok(h[0].shape[1], pj.out_features):
+        # int8-MFMA mode at the 64x64 level: GEGLU + the per-token codes of its output in one launch
+        wq, sw, b = _geglu_operand_i8(pj, pj.i8_operand())
+        g = K.linear_i8_geglu_q(h[0], h[1], wq, sw, bias=b)
+    else:
+        g = ff_geglu(blk.ff.net[0].proj, h)
+    rows = g[0].shape[0] if isinstance(g, tuple) else g.shape[0]
+    if want_amax and lin_i8(fo) and fo.output_quant_name == "None" and rows >= I8_MIN_ROWS:
         # int8-MFMA mode: per-token codes of the GEGLU output, the block output's per-(n, c) amax
         # after the residual add reduced in the GEMM epilogue (proj_out's per-sample scale)
         i8 = fo.i8_operand()
-        xq, sa = K.quant_rows_i8(g)
+        xq, sa = g if isinstance(g, tuple) else K.quant_rows_i8(g)
         amax, zeroed = A.zeroed_f32(n * c, t.device)
         out = K.linear_i8(xq, sa, i8[0], i8[1], bias=fo.bias, residual=t, amax=amax, rows_per_sample=s,
                           amax_zeroed=zeroed, amax_post=True)

@@ -40,9 +40,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--pmc", action="store_true")
+    ap.add_argument("--pmc-n", type=int, default=320,
+                    help="--pmc: N of the M 32768 K 320 int8 linear (2560: the plain wide-N shape, no residual)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
+    if a.pmc and a.pmc_n != 320:
+        x = torch.randn(32768, 320, generator=g).half().to(dev)
+        w = (torch.randn(a.pmc_n, 320, generator=g) / 320 ** 0.5).half().to(dev)
+        xq, sa = K.quant_rows_i8(x)
+        wq, sw16, _ = K.weight_quant(w, 320, 8, want_dq=False)
+        sw = sw16.float().view(-1).contiguous()
+        b = torch.randn(a.pmc_n, generator=g).half().to(dev)
+        for _ in range(5):
+            K.linear_i8(xq, sa, wq, sw, bias=b)
+        torch.cuda.synchronize()
+        print("choice", [v for kk, v in K.gemm_choices(used_only=True).items()])
+        return
     if a.pmc:
         x, w, r, xq, sa, wq, sw = operands(32768, 320, dev, g)
         for _ in range(5):

@@ -118,11 +118,20 @@ def main():
                     help="keep the committed table, tune only the shapes it lacks (new epilogue keys)")
     ap.add_argument("--drop-epi", type=int, default=0,
                     help="with --add: first drop the entries whose epilogue flags intersect this mask")
+    ap.add_argument("--retune-i8-linear", action="store_true",
+                    help="keep the committed table, re-tune only the int8 linears (SD1.5, both modes run)")
     ap.add_argument("--retune-i4", action="store_true",
                     help="keep the committed table, re-tune only the linears whose operands include packed int4")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    if a.retune_i4:
+    if a.retune_i8_linear:
+        K.load_table(OUT)
+        dropped = {k: K._TUNE.pop(k) for k in [k for k in K.gemm_choices() if k[0] == "linear_i8"]}
+        log(f"committed table without its {len(dropped)} int8 linears")
+        run_sd15(dev)
+        for key, ch in dropped.items():  # shapes this run does not meet keep their committed choice
+            K._TUNE.setdefault(key, ch)
+    elif a.retune_i4:
         K.load_table(OUT)
         for key in [k for k in K.gemm_choices() if k[0] == "linear" and "i4" in k[-1]]:
             del K._TUNE[key]

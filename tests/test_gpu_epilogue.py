@@ -47,7 +47,7 @@ def _variants(fam):
     if fam == "f16":
         return [None] + list(K.REG_VARIANTS) + list(K.DMA_VARIANTS)
     if fam == "i8":
-        return [None] + list(K.I8_VARIANTS)
+        return [None] + list(K.I8_VARIANTS) + list(K.I8_PERSIST_VARIANTS)
     return [None] + [v for v in K.W4_VARIANTS if v < 300]
 
 

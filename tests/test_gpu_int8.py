@@ -21,6 +21,9 @@ def K():
 I8_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 130, 131, 132, 133, 134]
 # explicit split-K counts (variant + 1000 * s; the int32 slabs make every split bit-identical)
 I8_SPLIT_FORCE = [1110, 3110, 4111, 2115, 6133, 8111]
+# persistent LDS-DMA linears (kernels.I8_PERSIST_VARIANTS: 2 / 4 tiles per block, the next tile's DMA
+# under the current tile's direct-store epilogue)
+I8_PERSIST_FORCE = [160, 161, 164, 165, 166, 167, 170, 171, 174, 175, 176, 177]
 
 
 def _bits(a):
@@ -54,7 +57,7 @@ def test_sample_codes(dev):
 
 @pytest.mark.parametrize("M,N,Kd", [(64, 64, 64), (200, 320, 320), (616, 640, 768), (4096, 2560, 320),
                                     (8, 1280, 1280), (1000, 64, 128), (256, 1280, 5120), (77, 320, 2560)])
-@pytest.mark.parametrize("variant", I8_FORCE + I8_SPLIT_FORCE)
+@pytest.mark.parametrize("variant", I8_FORCE + I8_SPLIT_FORCE + I8_PERSIST_FORCE)
 def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
     k = K()
     rng = np.random.default_rng(M + N + Kd)
@@ -74,7 +77,7 @@ def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
     assert np.array_equal(_bits(y), _bits(ref)), np.abs(y.astype(np.float32) - ref.astype(np.float32)).max()
 
 
-@pytest.mark.parametrize("variant", [None, 110, 130, 131, 133])
+@pytest.mark.parametrize("variant", [None, 110, 130, 131, 133, 160, 166, 167, 177])
 def test_linear_i8_geglu_and_amax(variant, dev):
     k = K()
     k.force_gemm(variant)
@@ -104,7 +107,7 @@ def _geglu_amax(k, dev):
     assert torch.equal(amax.cpu(), y.float().abs().view(2, 256, -1).amax(1).reshape(-1).cpu())
 
 
-@pytest.mark.parametrize("variant", I8_FORCE + I8_SPLIT_FORCE)
+@pytest.mark.parametrize("variant", I8_FORCE + I8_SPLIT_FORCE + [160, 170, 175])
 def test_linear_i8_post_residual_amax_and_fused_scale(variant, dev):
     """the int8 proj_out scale fusion (unet.block_fwd: the last ff.net.2 GEMM reduces the
     block output's per-(n, c) amax after its residual add, qd_linear_i8 post-residual amax) and
@@ -598,3 +601,36 @@ def test_quant_rows_i8_grouped_and_wide(rows, c, dev):
     q, s = k.quant_rows_i8(torch.from_numpy(x).to(dev))
     qr, sr = R.quant_rows_i8(x)
     assert np.array_equal(q.cpu().numpy(), qr) and np.array_equal(s.cpu().numpy(), sr)
+
+
+@pytest.mark.parametrize("M", [32768, 1000, 64, 1])
+@pytest.mark.parametrize("variant", [None, 150, 151])
+def test_linear_i8_geglu_q_equals_geglu_then_row_codes(M, variant, dev):
+    """The fused int8 GEGLU + per-token codes launch (qd_linear_i8_geglu_q, the SD1.5 64x64 level's
+    K 320 -> 2 x 1280 projection) is bit-identical to linear_i8(geglu=True) followed by quant_rows_i8
+    (both pinned to oracle/int8_ref.py above): codes and scales, ragged M, both wave layouts."""
+    k = K()
+    Kd, N = 320, 2560
+    assert k.linear_i8_geglu_q_ok(Kd, N)
+    rng = np.random.default_rng(M + 17)
+    x = (rng.standard_normal((M, Kd)) * 2).astype(np.float16)
+    w = (rng.standard_normal((N, Kd)) / Kd ** 0.5).astype(np.float16)
+    b = rng.standard_normal(N).astype(np.float16)
+    if M > 8:
+        x[3] *= 50   # an outlier token (its scale is far from the others')
+        x[5] = 0     # an all-zero token
+    xq, sa = R.quant_rows_i8(x)
+    wq, sw = R.weight_rows_i8(w)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    perm = k.geglu_interleave_rows(N, dev)
+    wqi, swi, bi = t(wq)[perm].contiguous(), t(sw)[perm].contiguous(), t(b)[perm].contiguous()
+    g = k.linear_i8(t(xq), t(sa), wqi, swi, bias=bi, geglu=True)
+    q_ref, s_ref = k.quant_rows_i8(g)
+    k.force_gemm(variant)
+    try:
+        q, s = k.linear_i8_geglu_q(t(xq), t(sa), wqi, swi, bias=bi)
+    finally:
+        k.force_gemm(None)
+    torch.cuda.synchronize()
+    assert torch.equal(s.cpu(), s_ref.cpu())
+    assert torch.equal(q.cpu(), q_ref.cpu())
