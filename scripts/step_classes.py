@@ -4,10 +4,10 @@ usage: python scripts/step_classes.py gpurun_out/prof_X/run_kernel_trace.csv [ma
 import csv
 import sys
 
-CLASSES = [("GEMM/conv", ("k_gemm", "k_conv_halo", "k_gemv")), ("split-K reduce", ("k_splitk",)),
+CLASSES = [("GEMM/conv", ("k_gemm", "k_conv_halo", "k_gemv", "k_geglu_i8q")), ("split-K reduce", ("k_splitk",)),
            ("attention", ("k_attn",)), ("GroupNorm", ("k_gn_",)), ("LayerNorm", ("k_layernorm", "k_ln_rows", "k_fq_layernorm")),
            ("finalize", ("k_finalize",)), ("colmax + apply", ("k_colmax", "k_apply", "k_act_")),
-           ("int8 act quant", ("k_quant_rows_i8", "k_quant_rows_g", "k_sample_")), ("scheduler / embed", ("k_cfg", "k_timestep")),
+           ("int8 act quant", ("k_quant_rows_i8", "k_quant_rows_g", "k_sample_", "k_cat_apply_i8")), ("scheduler / embed", ("k_cfg", "k_timestep")),
            ("elementwise", ("k_silu", "k_add", "k_concat", "k_geglu", "k_zero", "k_nchw", "k_nhwc"))]
 
 path = sys.argv[1]
