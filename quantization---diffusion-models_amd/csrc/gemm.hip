@@ -110,6 +110,8 @@ struct GemmArgs {
   // runs logical tiles bid, bid + grid, ... and stages the next tile's first K steps under the
   // current tile's epilogue whenever that epilogue stores straight from the fragments (no LDS)
   int pgrid;
+  // A-stationary int8 linears (k_gemm_as_i8): N-tile ranges per A panel
+  int as_nsplit;
 };
 
 constexpr int BK = 64;
@@ -958,6 +960,213 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
   }
 }
 
+// The direct-store epilogue in two phases for the persistent DMA kernels: direct_outputs forms every
+// 16-B store word of the wave tile (bias, GELU-tanh / GEGLU, permlane16 pairing, residual add - the
+// same per-element arithmetic as gemm_epilogue's direct path, so the same bits) with every load it
+// needs (bias, residual) issued AND consumed first; direct_stores then only stores.  Between the two
+// the kernel issues the next tile's DMA: no load younger than that DMA is waited for (a counted
+// vmcnt on an ordinary load would wait for the older DMA too), so the DMA runs under the stores.
+template <int TM, int TN>
+__device__ __forceinline__ void direct_outputs(const GemmArgs& p, const f32x4 (&acc)[TM][TN], int m0, int n0, int wm0,
+                                               int wn0, u32x4 (&wo)[TM][TN / 2 + (TN & 1)]) {
+  constexpr int NJ = TN / 2, NJT = NJ + (TN & 1);
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
+  const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
+  const bool gg = (p.epi & QD_EPI_GEGLU) != 0;
+  const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+  const int cpart = 16 * (fq & 1) + 8 * (fq >> 1);
+  const int ocol0 = gg ? ((n0 + wn0) >> 1) : n0 + wn0;
+  const int oN = gg ? (p.N >> 1) : p.N;
+  const int npair = gg ? NJ / 2 : NJ;
+  const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
+  const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res ? p.res : p.y, has_res ? ybytes : 0u);
+  f16x8 rq[TM][NJT];
+  if (has_res) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm0 + i * 16 + fr;
+#pragma unroll
+      for (int jp = 0; jp < NJ; ++jp) {
+        const int n = ocol0 + 32 * jp + cpart;
+        rq[i][jp] = bload(rrs, (jp < npair && m < p.M && n < oN) ? ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u : OOB);
+      }
+      if constexpr ((TN & 1) != 0) {
+        const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
+        const f16x4 t = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(
+            rrs, (m < p.M && n < p.N) ? (int)(((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u) : (int)OOB, 0, 0));
+        rq[i][NJ] = (f16x8){t[0], t[1], t[2], t[3], (f16)0, (f16)0, (f16)0, (f16)0};
+      }
+    }
+  }
+  f16x4 bq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + j * 16 + fq * 4;
+    bq[j] = (has_bias && n < p.N) ? *reinterpret_cast<const f16x4*>(p.bias + n) : f16x4{};
+  }
+  auto frag16 = [&](int i, int j) {
+    f16x4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[j][r]);
+    return h;
+  };
+  auto geglu_frag = [&](int i, int j) {
+    const f16x4 hv = frag16(i, j), gv = frag16(i, j + 1);
+    f16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      const f32x2 g2 = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+      o[r] = (f16)((float)hv[r] * (float)(f16)g2.x);
+      o[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)g2.y);
+    }
+    return o;
+  };
+  auto plain_frag = [&](int i, int j) {
+    f16x4 o = frag16(i, j);
+    if (gtanh) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (f16)gelu_tanh_f((float)o[r]);
+    }
+    return o;
+  };
+  auto pair = [&](int i, int jp, f16x4 fa, f16x4 fb) {
+    const u32x2 a = __builtin_bit_cast(u32x2, fa), b = __builtin_bit_cast(u32x2, fb);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+    u32x4 w = (u32x4){s0[0], s1[0], s0[1], s1[1]};
+    if (has_res) {
+      f16x8 v = __builtin_bit_cast(f16x8, w);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i][jp][r]);
+      w = __builtin_bit_cast(u32x4, v);
+    }
+    return w;
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    if constexpr (TN % 4 == 0) {
+      if (gg) {
+#pragma unroll
+        for (int jp = 0; jp < TN / 4; ++jp) wo[i][jp] = pair(i, jp, geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2));
+#pragma unroll
+        for (int jp = TN / 4; jp < NJT; ++jp) wo[i][jp] = (u32x4){0u, 0u, 0u, 0u};
+        continue;
+      }
+    }
+#pragma unroll
+    for (int jp = 0; jp < NJ; ++jp) wo[i][jp] = pair(i, jp, plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1));
+    if constexpr ((TN & 1) != 0) {
+      f16x4 v = plain_frag(i, TN - 1);
+      if (has_res) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (f16)((float)v[r] + (float)rq[i][NJ][r]);
+      }
+      const u32x2 t = __builtin_bit_cast(u32x2, v);
+      wo[i][NJ] = (u32x4){t.x, t.y, 0u, 0u};
+    }
+  }
+}
+
+// direct_outputs without a residual, the bias fragments already loaded (the A-stationary kernel
+// loads them ahead of its DMA): the same per-element arithmetic
+template <int TM, int TN>
+__device__ __forceinline__ void direct_outputs_pre(const GemmArgs& p, const f32x4 (&acc)[TM][TN], const f16x4 (&bq)[TN],
+                                                   int m0, int n0, int wm0, int wn0,
+                                                   u32x4 (&wo)[TM][TN / 2 + (TN & 1)]) {
+  constexpr int NJ = TN / 2, NJT = NJ + (TN & 1);
+  const bool gg = (p.epi & QD_EPI_GEGLU) != 0;
+  const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+  auto frag16 = [&](int i, int j) {
+    f16x4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[j][r]);
+    return h;
+  };
+  auto geglu_frag = [&](int i, int j) {
+    const f16x4 hv = frag16(i, j), gv = frag16(i, j + 1);
+    f16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      const f32x2 g2 = gelu2_f((f32x2){(float)gv[r], (float)gv[r + 1]});
+      o[r] = (f16)((float)hv[r] * (float)(f16)g2.x);
+      o[r + 1] = (f16)((float)hv[r + 1] * (float)(f16)g2.y);
+    }
+    return o;
+  };
+  auto plain_frag = [&](int i, int j) {
+    f16x4 o = frag16(i, j);
+    if (gtanh) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (f16)gelu_tanh_f((float)o[r]);
+    }
+    return o;
+  };
+  auto pair = [&](f16x4 fa, f16x4 fb) {
+    const u32x2 a = __builtin_bit_cast(u32x2, fa), b = __builtin_bit_cast(u32x2, fb);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+    return (u32x4){s0[0], s1[0], s0[1], s1[1]};
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    if constexpr (TN % 4 == 0) {
+      if (gg) {
+#pragma unroll
+        for (int jp = 0; jp < TN / 4; ++jp) wo[i][jp] = pair(geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2));
+#pragma unroll
+        for (int jp = TN / 4; jp < NJT; ++jp) wo[i][jp] = (u32x4){0u, 0u, 0u, 0u};
+        continue;
+      }
+    }
+#pragma unroll
+    for (int jp = 0; jp < NJ; ++jp) wo[i][jp] = pair(plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1));
+    if constexpr ((TN & 1) != 0) {
+      const u32x2 t = __builtin_bit_cast(u32x2, plain_frag(i, TN - 1));
+      wo[i][NJ] = (u32x4){t.x, t.y, 0u, 0u};
+    }
+  }
+}
+
+// the stores of direct_outputs' words; returns the number of store instructions this wave issued
+template <int TM, int TN>
+__device__ __forceinline__ int direct_stores(const GemmArgs& p, const u32x4 (&wo)[TM][TN / 2 + (TN & 1)], int m0, int n0,
+                                             int wm0, int wn0) {
+  constexpr int NJ = TN / 2;
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool gg = (p.epi & QD_EPI_GEGLU) != 0;
+  const int cpart = 16 * (fq & 1) + 8 * (fq >> 1);
+  const int ocol0 = gg ? ((n0 + wn0) >> 1) : n0 + wn0;
+  const int oN = gg ? (p.N >> 1) : p.N;
+  const int npair = gg ? NJ / 2 : NJ;
+  const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
+  const __amdgpu_buffer_rsrc_t yrs = rsrc(p.y, ybytes);
+  int nst = 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm0 + i * 16 + fr;
+    const bool row_ok = m < p.M;
+#pragma unroll
+    for (int jp = 0; jp < NJ; ++jp) {
+      if (jp >= npair) continue;  // (wave-uniform: GEGLU halves the pairs)
+      const int n = ocol0 + 32 * jp + cpart;
+      const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
+      __builtin_amdgcn_raw_buffer_store_b128(wo[i][jp], yrs, (row_ok && n < oN) ? (int)off : (int)OOB, 0, 0);
+      ++nst;
+    }
+    if constexpr ((TN & 1) != 0) {
+      const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
+      const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
+      __builtin_amdgcn_raw_buffer_store_b64((u32x2){wo[i][NJ][0], wo[i][NJ][1]}, yrs,
+                                            (row_ok && n < p.N) ? (int)off : (int)OOB, 0, 0);
+      ++nst;
+    }
+  }
+  return nst;
+}
+
 // ---- kernel -----------------------------------------------------------------------------
 template <int BM, int BN, int AMODE, int BFMT, bool SPLIT>
 __global__ void __launch_bounds__(256, 2) k_gemm(GemmArgs p) {
@@ -1277,6 +1486,8 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     QD_VM_CASE(7) QD_VM_CASE(8) QD_VM_CASE(9) QD_VM_CASE(10) QD_VM_CASE(11) QD_VM_CASE(12)
     QD_VM_CASE(13) QD_VM_CASE(14) QD_VM_CASE(15) QD_VM_CASE(16) QD_VM_CASE(17) QD_VM_CASE(18)
     QD_VM_CASE(19) QD_VM_CASE(20) QD_VM_CASE(21) QD_VM_CASE(22) QD_VM_CASE(23) QD_VM_CASE(24)
+    QD_VM_CASE(25) QD_VM_CASE(26) QD_VM_CASE(27) QD_VM_CASE(28) QD_VM_CASE(29) QD_VM_CASE(30)
+    QD_VM_CASE(31) QD_VM_CASE(32)
     default: wait_vm<0>(); break;
   }
 }
@@ -1320,7 +1531,8 @@ constexpr int dma_waves_per_eu_w4(int bm, int bn, int st, int nt, int bkt) {
                    : 1;
 }
 
-// PERSIST (int8 linears, lock-step pipeline, unsplit): a grid of p.pgrid blocks; block b runs the
+// PERSIST (int8 linears, lock-step pipeline, unsplit; the template also builds for fp16 weights, whose
+// persistent tiles measured no faster on any SD shape - profiles/r05q_sweep_f16.log): a grid of p.pgrid blocks; block b runs the
 // logical tiles b, b + grid, ... (XCD-remapped like the one-tile grid).  After a tile's K loop the
 // first ST-1 K steps of the block's next tile are issued into the (now free) stages BEFORE the tile's
 // epilogue when that epilogue touches no LDS (direct stores, no column amax), so the next tile's
@@ -1350,7 +1562,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
                 "fp8: one 128-code group per 128-B LDS row, no split-K, the scale row in one DMA piece");
   static_assert(!W4 || (!I8 && !F8 && PIPE == 0 && AMODE == AM_LINEAR && BN <= 512),
                 "int4: lock-step pipeline, linear A operand, one scale piece");
-  static_assert(!PERSIST || (I8 && PIPE == 0 && AMODE == AM_LINEAR && !SPLIT), "persistent: int8 linears, unsplit");
+  static_assert(!PERSIST || (!F8 && !W4 && PIPE == 0 && AMODE == AM_LINEAR && !SPLIT),
+                "persistent: int8 / fp16 linears, lock-step pipeline, unsplit");
   using AL = ADma<BM, NT, AMODE, BKT>;
   using BL = std::conditional_t<W4, BDma4<BN, NT, BKT>, BDma<BN, NT, BKT>>;
   __shared__ __attribute__((aligned(16))) f16 smem[LDSZ];
@@ -1408,7 +1621,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
   };
   int nk = (kend - kbeg + BKT - 1) / BKT;
   prologue(kbeg, nk);
-  bool drain = false;  // (PERSIST) a later tile: its first K step waits for every outstanding op
+  bool drain = false;  // (PERSIST) a later tile: its first K step waits for its stage past the stores
+  int nst = 0;         // (PERSIST) store instructions the previous tile's epilogue issued after the DMA
   for (;;) {
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1463,7 +1677,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (PERSIST && kt == 0 && drain) {
-        wait_vm<0>();
+        // younger than this tile's first stage: its next ST-2 stages and the previous tile's stores
+        // (counted in issue order with the DMA; nst = 0 after an LDS-tile epilogue)
+        wait_vm_rt(min(ST - 2, nk - 1) * per + nst);
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -1558,14 +1774,21 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
       ken = min(p.K, kbn + p.kps);
     }
     const int nkn = (ken - kbn + BKT - 1) / BKT;
-    // the epilogue below stores from the fragments and keeps no column maxima in LDS
+    // a direct-store epilogue with no column maxima: every output word is formed (its loads
+    // consumed) before the next tile's DMA is issued, then only stored
     const bool early = more && epi_direct<BN, TM, TN, false, true>(p) && !((p.epi & QD_EPI_AMAX) && p.amax);
-    if (early) {
-      al.init(p, m0n, kbn, wid);
-      bl.init(p, n0n, wid);
-      prologue(kbn, nkn);
+    nst = 0;
+    if constexpr (epi_direct_ok<TM, TN, true>()) {
+      if (early) {
+        u32x4 wo[TM][TN / 2 + (TN & 1)];
+        direct_outputs<TM, TN>(p, acc, m0, n0, wm0, wn0, wo);
+        al.init(p, m0n, kbn, wid);
+        bl.init(p, n0n, wid);
+        prologue(kbn, nkn);
+        nst = direct_stores<TM, TN>(p, wo, m0, n0, wm0, wn0);
+      }
     }
-    gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, false>(p, acc, smem, m0, n0, wm0, wn0, split);
+    if (!early) gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, false>(p, acc, smem, m0, n0, wm0, wn0, split);
     if (!more) break;
     if (!early) {
       __syncthreads();  // the epilogue's LDS C tile / column maxima are read
@@ -1586,6 +1809,139 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
     break;
   }
   }
+}
+
+// ---- A-stationary int8 linear (qd_gemm_force 190-192; round 5) ------------------------------
+// For short K (K = KC codes, 320 or 640) and wide N the one-tile kernels restream the A rows once per
+// N tile: at M 32768 N 2560 K 320 a CU moves 1.2 MB of operands at the ~25 GB/s per CU its LDS-DMA
+// ring sustains inside a GEMM.  Here a block (8 waves, WGM x WGN, wave tile 64 x BN/WGN)
+// keeps its BM x KC A panel in LDS for all of its N tiles (loaded once) and streams only the weight
+// rows through a RING-deep ring that runs continuously across the tiles - W step g = (tile g / NK,
+// k-step g % NK) - so a tile's epilogue runs while the next tile's first stages land.  Per CU at that
+// shape: 80 KB of A + 400 KB of W.  The epilogue is the two-phase direct store (direct_outputs /
+// direct_stores: plain, bias, GEGLU at TN 4); its scale / bias loads are issued at the top of the
+// tile's last step, before that step's DMA, so waiting for them never waits for younger DMA; the
+// stores are counted into the next waits (vmcnt counts loads, stores and LDS-DMA in issue order).
+// Every step issues the same DMA (past the last step: a dummy piece into a scratch slot), so every
+// count is exact.  Exact int32 sums, the i8_scale / epilogue arithmetic: the same bits as every
+// other int8 variant.
+template <int BM, int BN, int KC, int RING>
+__global__ void __launch_bounds__(512, 1) k_gemm_as_i8(GemmArgs p) {
+  constexpr int NT = 512, NW = 8, WGM = BM / 64, WGN = NW / WGM;
+  constexpr int WN = BN / WGN, TM = 4, TN = WN / 16, NK = KC / 64;
+  constexpr int ASZ = BM * 32, BSZ = BN * 32;  // halves per A / W stage (64-B rows)
+  static_assert(BM % 64 == 0 && NW % WGM == 0 && WN % 16 == 0 && KC % 64 == 0 && RING >= 3, "A-stationary tile");
+  static_assert(epi_direct_ok<TM, TN, true>(), "A-stationary: direct-store epilogue tiles only");
+  static_assert(NK >= RING - 1, "one store batch pending at a time");
+  using AL = ADma<BM, NT, AM_LINEAR, 32>;
+  using BL = BDma<BN, NT, 32>;
+  static_assert((BN / 16) % NW == 0, "the same number of 16-row W pieces per wave and step");
+  constexpr int PW = BN / 16 / NW;  // W pieces per wave and step
+  __shared__ __attribute__((aligned(16))) f16 smem[NK * ASZ + (RING + 1) * BSZ];
+  f16* const apanel = smem;
+  f16* const ring = smem + NK * ASZ;
+  f16* const scratch = ring + RING * BSZ;  // the dummy pieces past the last step
+
+  const int npanel = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int nsplit = p.as_nsplit;
+  const int nwg = npanel * nsplit;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int panel = wg / nsplit, part = wg - panel * nsplit;
+  const int tper = (ntn + nsplit - 1) / nsplit;
+  const int t0 = part * tper, ntile = min(ntn, t0 + tper) - t0;
+  if (ntile <= 0) return;  // (block-uniform)
+  const int m0 = panel * BM;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * 64, wn0 = (wid % WGN) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  AL al;
+  al.init(p, m0, 0, wid);
+#pragma unroll
+  for (int s = 0; s < NK; ++s) al.issue(p, s * 32, apanel + s * ASZ, wid);
+  BL bl;
+  int btile = -1;
+  const int T = ntile * NK;
+  // W step g -> ring slot g % RING (steps >= T: a dummy piece into the scratch slot)
+  auto issue_w = [&](int g) {
+    const int gg = g < T ? g : T - 1;
+    const int j = gg / NK, s = gg - j * NK;
+    if (j != btile) {
+      bl.init(p, (t0 + j) * BN, wid);
+      btile = j;
+    }
+    bl.issue(p, s * 32, g < T ? ring + (g % RING) * BSZ : scratch, wid);
+  };
+#pragma unroll
+  for (int g = 0; g < RING - 1; ++g) issue_w(g);
+
+  i32x4 iacc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) iacc[i][j] = (i32x4){0, 0, 0, 0};
+  int nst = 0, store_after = -1;  // store instructions of the last epilogue, issued after W step store_after
+  const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
+  for (int g = 0; g < T; ++g) {
+    const int j = g / NK, s = g - j * NK;
+    const int n0 = (t0 + j) * BN;
+    // own pieces of step g landed; younger: the next RING-2 steps' pieces (+ the stores issued after
+    // step store_after, when g <= store_after)
+    wait_vm_rt((RING - 2) * PW + (g <= store_after ? nst : 0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    float sa[TM];
+    f32x4 sw[TN];
+    f16x4 bq[TN];
+    if (s == NK - 1) {  // the epilogue's operands, before this step's DMA (waiting for them then
+                        // waits for older pieces only)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) sa[i] = p.sa[min(m0 + wm0 + i * 16 + fr, p.M - 1)];
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) {
+        const int n = n0 + wn0 + jj * 16 + fq * 4;
+        sw[jj] = n < p.N ? *reinterpret_cast<const f32x4*>(p.sw + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        bq[jj] = (has_bias && n < p.N) ? *reinterpret_cast<const f16x4*>(p.bias + n) : f16x4{};
+      }
+      asm volatile("" ::: "memory");
+    }
+    issue_w(g + RING - 1);
+    {
+      const f16* As = apanel + s * ASZ;
+      const f16* Bs = ring + (g % RING) * BSZ;
+      f16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f16x8*>(As + swz_t<32>(wm0 + i * 16 + fr, fq));
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) bf[jj] = *reinterpret_cast<const f16x8*>(Bs + swz_t<32>(wn0 + jj * 16 + fr, fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj)
+          iacc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, bf[jj]),
+                                                              __builtin_bit_cast(i32x4, af[i]), iacc[i][jj], 0, 0, 0);
+    }
+    if (s == NK - 1) {
+      f32x4 acc[TM][TN];
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][jj][r] = ((float)iacc[i][jj][r] * sa[i]) * sw[jj][r];
+          iacc[i][jj] = (i32x4){0, 0, 0, 0};
+        }
+      u32x4 wo[TM][TN / 2 + (TN & 1)];
+      direct_outputs_pre<TM, TN>(p, acc, bq, m0, n0, wm0, wn0, wo);
+      nst = direct_stores<TM, TN>(p, wo, m0, n0, wm0, wn0);
+      store_after = g + RING - 1;
+    }
+  }
+  wait_vm<0>();  // (the dummy pieces land in this block's LDS before it exits)
 }
 
 // ---- ping-pong GEMM (256 x BN tile, 8 waves, BK 32, 4-stage LDS-DMA ring) ----------------
@@ -2973,10 +3329,12 @@ extern "C" int qd_gemm_force(int variant) {
   const int v = variant >= 1000 ? variant % 1000 : variant, sp = variant >= 1000 ? variant / 1000 : 0;
   QD_REQUIRE(v == -1 || (v >= 0 && v < 4) ||
                  (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 203) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
-                 (v >= 130 && v <= 134) || (v >= 140 && v <= 151) || (v >= 160 && v <= 167) || (v >= 170 && v <= 177),
+                 (v >= 130 && v <= 134) || (v >= 140 && v <= 151) || (v >= 160 && v <= 167) || (v >= 170 && v <= 177) ||
+                 (v >= 190 && v <= 192),
              "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..117, fp8: 120..123), 200-203 halo conv, "
              "300-304 ping-pong (int8: 130-134, int8 halo conv 140-149, fused GEGLU codes 150 / 151, persistent "
-             "int8 DMA linears 160-167 / 170-177: variants 10-17 with 2 / 4 tiles per block); + 1000 * s: "
+             "int8 DMA linears 160-167 / 170-177: variants 10-17 with 2 / 4 tiles per block, A-stationary int8 "
+             "linears 190-192); + 1000 * s: "
              "split-K count s (1 = unsplit)");
   QD_REQUIRE(sp <= 32, "qd_gemm_force: split count above 32");
   g_force = v;
@@ -3751,8 +4109,28 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // gn: GroupNorm-statistics / per-(sample, column) add epilogue - lock-step DMA tiles that lie in
 // one sample (rows_per_sample % BM == 0), or the halo conv; split-K plans reduce through
 // k_splitk_reduce_gn (64-row blocks)
+// A-stationary int8 linears (k_gemm_as_i8, qd_gemm_force 190 + c): tile BM x BN, K = KC codes
+struct AsCfg {
+  int bm, bn, kc, ring;
+};
+static constexpr AsCfg kAsC[] = {{256, 128, 320, 4}, {128, 256, 640, 3}, {128, 128, 640, 4}};
+
+// the LDS-DMA variant an UNSPLIT int8 GEMM runs for the requested one: amax epilogues need every
+// wave's rows in one sample, GroupNorm-statistics / channel-add epilogues every block's
+static int i8_unsplit_var(int var, int rows_per_sample, bool amax, bool gn) {
+  if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
+  if (gn && rows_per_sample % kDmaC[var].bm != 0) var = rows_per_sample % 128 == 0 ? 11 : 15;  // tile in one sample
+  return var;
+}
+
 static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool geglu, bool post = false,
                     bool gn = false) {
+  if (g_force >= 190 && g_force <= 192) {
+    // plain / bias / GEGLU (TN 4 tiles) epilogues, unsplit; the residual / LDS-form checks are in run_i8
+    const AsCfg& c = kAsC[g_force - 190];
+    const int tn = c.bn / (8 / (c.bm / 64)) / 16;
+    if (Kh * 2 == c.kc && !amax && !post && !gn && (!geglu || tn % 4 == 0)) return Plan{4, c.bm, c.bn, g_force - 190, 1, Kh};
+  }
   if (g_force >= 140 && g_force <= 149 && !geglu && Kh % 288 == 0) {
     // int8 halo conv (applicability checked at launch): 140 BN 160 / 141 BN 128 (3-slot weight
     // ring), 142 / 143 / 144 BN 160 with 4 / 5 / 6 slots (256-pixel tiles); 145 / 146 / 147:
@@ -3808,8 +4186,13 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
     var = 10 + g_force % 10;
     pdiv = g_force < 170 ? 2 : 4;
   }
-  if (amax && rows_per_sample % (kDmaC[var].bm / kDmaC[var].wgm) != 0) var = 11;
-  if (gn && rows_per_sample % kDmaC[var].bm != 0) var = rows_per_sample % 128 == 0 ? 11 : 15;  // tile in one sample
+  int fsp;
+  // a split-K plan reduces the amax / GroupNorm statistics / channel add in its reduction kernel (64-row
+  // blocks), so only an unsplit tile needs whole-sample rows: with an explicit split the requested tile
+  // stands (the 8x8 level's GroupNorm convs otherwise all collapse to 64-row tiles, each re-reading the
+  // whole weight once per 64 rows)
+  const bool fsplit = g_force >= 110 && !geglu && !post && !pdiv && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp) && fsp > 1;
+  if (!fsplit) var = i8_unsplit_var(var, rows_per_sample, amax, gn);
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];
   Plan pl{1, d.bm, d.bn, var, 1, Kh};
@@ -3820,7 +4203,6 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
   const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
   const int per_cu = std::max(1, std::min(by_lds, by_waves));
-  int fsp;
   if (g_force >= 110 && !geglu && !post && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp)) {
     pl.splits = fsp;
     pl.kps = Kh / fsp;
@@ -3849,6 +4231,12 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   const bool post = (p.epi & QD_EPI_AMAX_POST) != 0, gn = epi_gn(p.epi);
   Plan pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post,
                     gn);
+  if (pl.kind == 4 && (AMODE != AM_LINEAR || ((p.epi & QD_EPI_RESIDUAL) && p.res) || p.epi_lds)) {
+    const int f = g_force;  // A-stationary tile not applicable (residual, the LDS-form knob, a conv)
+    g_force = -1;
+    pl = plan_i8(p.M, p.N, p.K, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, (p.epi & QD_EPI_GEGLU) != 0, post, gn);
+    g_force = f;
+  }
   if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 32, pl.bm))) {  // int8 halo conv not applicable
     const int f = g_force;
     g_force = -1;
@@ -3858,6 +4246,11 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
   if (pl.splits > 1 && (!ws || ws_elems < split_ws_elems(pl, p.M, p.N))) {
     pl.splits = 1;
     pl.kps = pl.kind == 2 ? p.K / 288 : p.K;
+    if (pl.kind == 1) {  // unsplit after all: the tile must hold whole-sample rows again
+      pl.var = i8_unsplit_var(pl.var, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0, gn);
+      pl.bm = kDmaC[pl.var].bm;
+      pl.bn = kDmaC[pl.var].bn;
+    }
   }
   p.splits = pl.splits;
   p.kps = pl.kps;
@@ -3880,6 +4273,17 @@ static void run_i8(GemmArgs& p, float* ws, long ws_elems, hipStream_t st) {
     else if (pl.bn == 160) launch_halo_i8<160, 3>(p, st);
     else launch_halo_i8<128, 3>(p, st);
   };
+  if constexpr (AMODE == AM_LINEAR) {
+    if (pl.kind == 4) {
+      const int npanel = (p.M + pl.bm - 1) / pl.bm, ntn = (p.N + pl.bn - 1) / pl.bn;
+      p.as_nsplit = std::max(1, std::min(ntn, (256 + npanel / 2) / npanel));  // one block per CU
+      const int grid = npanel * p.as_nsplit;
+      if (pl.var == 0) k_gemm_as_i8<256, 128, 320, 4><<<grid, 512, 0, st>>>(p);
+      else if (pl.var == 1) k_gemm_as_i8<128, 256, 640, 3><<<grid, 512, 0, st>>>(p);
+      else k_gemm_as_i8<128, 128, 640, 4><<<grid, 512, 0, st>>>(p);
+      return;
+    }
+  }
   if (pl.splits == 1) {
     if (pl.kind == 2) halo();
     else if (pl.kind == 3) launch_pp_i8<AMODE, false>(p, pl.bn, st);

@@ -709,6 +709,10 @@ I8_HALO_VARIANTS = (140, 141, 142, 143, 144, 145, 146, 147, 148, 149)
 # persistent LDS-DMA linears (unsplit): variants 10, 11, 14-17 with 2 (160 + v) / 4 (170 + v) tiles per
 # block, the next tile's first K steps staged under the current tile's epilogue
 I8_PERSIST_VARIANTS = (160, 161, 164, 165, 166, 167, 170, 171, 174, 175, 176, 177)
+# A-stationary linears (K 320 / 640 codes; plain / bias / GEGLU; qd_gemm_force only, not tuner
+# candidates: no faster on any SD shape): the block's A panel stays in LDS over all of its
+# N tiles, the weights stream through one continuous ring (k_gemm_as_i8)
+I8_AS_VARIANTS = (190, 191, 192)
 
 
 def quant_rows_i8(x2d, out=None, scales=None):

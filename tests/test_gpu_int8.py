@@ -198,7 +198,7 @@ GN_CASES = [(320, 320, 3, 1, 64, False, False, True), (320, 320, 3, 1, 64, False
             (1280, 1280, 3, 1, 8, False, True, False), (320, 320, 1, 1, 64, False, True, False),
             (640, 640, 3, 2, 32, False, False, False), (640, 320, 3, 1, 32, True, True, False)]
 GN_FORCE = [None, 110, 111, 112, 113, 114, 115, 116, 117, 140, 141, 142, 145, 146, 147, 148, 149, 3110, 4111, 2142,
-            2145, 5148, 6111]
+            2145, 5148, 6111, 2117, 3116, 4113, 2112]  # (explicit splits keep their tile: the reduction makes the statistics)
 
 
 @pytest.mark.parametrize("cin,cout,ksz,stride,hw,ups,res,cadd", GN_CASES)
@@ -634,3 +634,37 @@ def test_linear_i8_geglu_q_equals_geglu_then_row_codes(M, variant, dev):
     torch.cuda.synchronize()
     assert torch.equal(s.cpu(), s_ref.cpu())
     assert torch.equal(q.cpu(), q_ref.cpu())
+
+
+@pytest.mark.parametrize("M,N,Kd", [(32768, 960, 320), (1000, 2560, 320), (64, 320, 320), (8192, 1920, 640),
+                                    (300, 5120, 640), (777, 1280, 640)])
+@pytest.mark.parametrize("variant", [190, 191, 192])
+@pytest.mark.parametrize("epi", ["plain", "bias", "geglu"])
+def test_linear_i8_astationary_bit_exact(M, N, Kd, variant, epi, dev):
+    """k_gemm_as_i8 (the A panel held in LDS over a block's N tiles, one continuous weight ring): the
+    same bits as the one-tile LDS-DMA variant (110) - ragged M, partial last N tiles, one-tile
+    blocks; variants whose K differs fall back to the planner (still compared)."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N + Kd + variant)
+    x = torch.randn(M, Kd, generator=g).half().to(dev)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).half().to(dev)
+    b = torch.randn(N, generator=g).half().to(dev)
+    xq, sa = k.quant_rows_i8(x)
+    wq, sw16, _ = k.weight_quant(w, Kd, 8, want_dq=False)
+    sw = sw16.float().view(-1).contiguous()
+    if epi == "geglu":
+        perm = k.geglu_interleave_rows(N, dev)
+        wq, sw, b = wq[perm].contiguous(), sw[perm].contiguous(), b[perm].contiguous()
+
+    def run(v):
+        k.force_gemm(v)
+        try:
+            return k.linear_i8(xq, sa, wq, sw, bias=None if epi == "plain" else b, geglu=epi == "geglu").clone()
+        finally:
+            k.force_gemm(None)
+    ref, y = run(110), run(variant)
+    assert torch.equal(y.view(torch.int16), ref.view(torch.int16))
+    if M <= 1000 and epi != "geglu":
+        xr, sar = xq.cpu().numpy(), sa.cpu().numpy()
+        o = R.linear_i8(xr, sar, wq.cpu().numpy(), sw.cpu().numpy(), None if epi == "plain" else b.cpu().numpy(), None)
+        assert np.array_equal(_bits(y.cpu().numpy()), _bits(o))
