@@ -3421,7 +3421,11 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
   } else if (g_force >= 100 && g_force < 118 &&  // (118: the LayerNorm epilogue's tile, ln_var only)
              (!quant_w || (w4 && w4g % kDmaC[g_force - 100].bkt == 0 && kDmaC[g_force - 100].pipe == 0))) {
     const DmaVar& d = kDmaC[g_force - 100];
-    const bool ok = (!amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
+    // an explicit split reduces the amax in its reduction kernel: only an unsplit tile needs every
+    // wave's rows in one sample
+    int fs0 = 0;
+    const bool fsplit = !geglu && !post && K % 64 == 0 && forced_split(K / 64, 4, fs0) && fs0 > 1;
+    const bool ok = (fsplit || !amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
     if (ok) {
       best = {1, d.bm, d.bn, g_force - 100, 1, K};
       // split K (whole 64-deep steps, >= 8 per split) while the blocks fit one resident round
@@ -3783,6 +3787,17 @@ static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t
     if (pl.splits > 1) {  // no room for slabs: best unsplit plan
       pl.splits = 1;
       pl.kps = p.K;
+      if (pl.kind == 1 && (p.epi & QD_EPI_AMAX) && p.rows_per_sample % (kDmaC[pl.var].bm / kDmaC[pl.var].wgm) != 0) {
+        const int f = g_force, sp = g_split;  // the explicitly split tile needs whole-sample wave rows unsplit
+        g_force = -1;
+        g_split = 0;
+        pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, true, (p.epi & QD_EPI_GEGLU) != 0, post,
+                       w4g);
+        g_force = f;
+        g_split = sp;
+        pl.splits = 1;
+        pl.kps = p.K;
+      }
     }
   }
   p.splits = pl.splits;

@@ -354,7 +354,8 @@ def _split_cands(M, N, K, ops, halo=False):
 
 # int8 (int32 partial slabs: every split count gives the same bits) - explicit split counts for
 # the int8 GEMMs whose tiles cannot fill the GPU; K in int8 codes
-I8_SPLIT_VARIANTS = (110, 111, 115, 133)
+I8_SPLIT_VARIANTS = (110, 111, 113, 115, 117, 133)  # (113 / 117: 256-row tiles - half the weight re-reads
+                                                   # of the 128-row ones at the 8x8 level's 512 rows)
 
 
 def _i8_split_cands(M, N, K, halo=False):

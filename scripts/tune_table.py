@@ -118,6 +118,8 @@ def main():
                     help="keep the committed table, tune only the shapes it lacks (new epilogue keys)")
     ap.add_argument("--drop-epi", type=int, default=0,
                     help="with --add: first drop the entries whose epilogue flags intersect this mask")
+    ap.add_argument("--drop-conv-hw", type=int, default=0,
+                    help="with --add: also drop the fp16 / int8 conv entries whose input side is <= this")
     ap.add_argument("--retune-i8-linear", action="store_true",
                     help="keep the committed table, re-tune only the int8 linears (SD1.5, both modes run)")
     ap.add_argument("--retune-i4", action="store_true",
@@ -145,6 +147,9 @@ def main():
         if a.drop_epi:
             for key in [k for k in K.gemm_choices() if k[0] in ("conv_i8", "linear_i8") and
                         (k[11] if k[0] == "conv_i8" else k[5]) & a.drop_epi]:
+                dropped[key] = K._TUNE.pop(key)
+        if a.drop_conv_hw:
+            for key in [k for k in K.gemm_choices() if k[0] in ("conv", "conv_i8") and k[2] <= a.drop_conv_hw]:
                 dropped[key] = K._TUNE.pop(key)
         log(f"committed table ({n0} shapes)")
         for name in a.models.split(","):

@@ -604,7 +604,9 @@ def test_linear_post_residual_amax(variant, fmt, forced_gemm, dev):
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3] + list(range(100, 116)) + [200, 201, 202, 203, 300, 301, 302, 303, 304]
                          # + 1000 * s: an explicit split-K count s (1 = unsplit) for the DMA / ping-pong / halo plans
-                         + [1100, 2104, 3109, 4105, 6114, 8115, 1301, 2301, 4301, 1202, 2202, 3203, 5203])
+                         + [1100, 2104, 3109, 4105, 6114, 8115, 1301, 2301, 4301, 1202, 2202, 3203, 5203]
+                         # explicit splits of tiles whose wave rows exceed a sample (the reduction makes the amax)
+                         + [2103, 3113, 2117])
 def test_gemm_variants_conv_and_linear(variant, forced_gemm, dev):
     """Every kernel family / tile (register-staged and LDS-DMA) on ragged shapes: rows past M,
     conv halo, stride 2, fused 2x upsample, the 4-channel conv_in (any-Ci decode), K tails,
