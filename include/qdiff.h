@@ -144,7 +144,10 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
  * following qd_linear_fwd / qd_conv2d_fwd.  -1 = planner's choice (default); 0..3 = the
  * register-staged tiles 128x160, 128x128, 128x64, 64x64; 100 + i = LDS-DMA variant i (F16
  * weights; packed int4 with wscale_t: the BK-32 variants 110..117 and ping-pong 300..304; other
- * quantized formats keep the planner's register-staged choice). */
+ * quantized formats keep the planner's register-staged choice).  int8 (qd_linear_i8 / qd_conv2d_i8):
+ * 110..117 LDS-DMA, 130..134 ping-pong, 140..149 halo conv, 150 / 151 the fused GEGLU + codes kernel,
+ * 160..167 / 170..177 persistent LDS-DMA linears (2 / 4 tiles per block), 190..192 A-stationary
+ * linears.  + 1000 * s: explicit split-K count s (1 = unsplit).  Every int8 choice gives the same bits. */
 int qd_gemm_force(int variant);
 /* Measurement knob: on != 0 routes every GEMM / conv epilogue through the LDS C tile (the default,
  * 0, stores straight from the MFMA fragments wherever the epilogue allows; same output bits). */

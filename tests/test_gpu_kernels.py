@@ -869,7 +869,13 @@ def test_linear_ln_equals_linear_then_layernorm(M, Kd, variant, bias, i8_out, de
         y, h = k.linear_ln(x, w, r, gamma, beta, 1e-5, bias=b, i8_out=i8_out)
     finally:
         k.force_gemm(None)
-    y0 = k.linear(x, w, "f16", bias=b, residual=r)
+    # the reference linear unsplit (forced: 1100 = LDS-DMA tile, split count 1): every unsplit fp16
+    # tile sums K in the same order, a tuned split-K choice for the shape would not
+    k.force_gemm(1100)
+    try:
+        y0 = k.linear(x, w, "f16", bias=b, residual=r)
+    finally:
+        k.force_gemm(None)
     assert torch.equal(y, y0)
     if i8_out:
         q0, s0 = k.layernorm_i8(y0, 1e-5, gamma, beta)
