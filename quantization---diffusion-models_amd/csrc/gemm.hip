@@ -595,16 +595,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
         }
         // the bias per fragment column (h = half(acc + bias), the LDS pass's f32 add), then this lane's
         // column maxima of h per column group (no per-row arrays: register pressure)
-        f16x4 bq[TN];
+        // (the bias widened to f32 once per column group, not once per row block: the per-row-block
+        // sched_barrier below keeps the compiler from hoisting the conversions itself)
+        f32x4 bq[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wn0 + j * 16 + fq * 4;
-          bq[j] = (has_bias && n < p.N) ? *reinterpret_cast<const f16x4*>(p.bias + n) : f16x4{};
+          const f16x4 b = (has_bias && n < p.N) ? *reinterpret_cast<const f16x4*>(p.bias + n) : f16x4{};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bq[j][r] = (float)b[r];
         }
         auto frag16 = [&](int i, int j) {
           f16x4 h;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + (float)bq[j][r]);
+          for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + bq[j][r]);
           return h;
         };
         if (do_amax && !gg) {
@@ -643,8 +647,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           }
           return o;
         };
-        // pair (a | b) -> 16-B store (+ residual) at output column n of row m
-        auto store_pair = [&](int i, int jp, f16x4 fa, f16x4 fb, int m, bool row_ok) {
+        // pair (a | b) -> 16-B store (+ residual: RES, a compile-time copy of has_res - the row loop is
+        // instantiated for both, so no per-element select) at output column n of row m
+        auto store_pair = [&](auto res_c, int i, int jp, f16x4 fa, f16x4 fb, int m, bool row_ok) {
+          constexpr bool RES = decltype(res_c)::value;
           u32x4 w;
           {
             const u32x2 a = __builtin_bit_cast(u32x2, fa), b = __builtin_bit_cast(u32x2, fb);
@@ -653,7 +659,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
             w = (u32x4){s0[0], s1[0], s0[1], s1[1]};
           }
           const int n = ocol0 + 32 * jp + cpart;
-          if (has_res) {
+          if constexpr (RES) {
             f16x8 v = __builtin_bit_cast(f16x8, w);
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + jp][r]);
@@ -666,35 +672,41 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           __builtin_amdgcn_raw_buffer_store_b128(w, yrs, (row_ok && n < oN) ? (int)off : (int)OOB, 0, 0);
 #endif
         };
+        auto rows = [&](auto res_c) {
+          constexpr bool RES = decltype(res_c)::value;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if (has_res && i + PFD < TM) load_res(i + PFD);
-          const int m = m0 + wm0 + i * 16 + fr;
-          const bool row_ok = m < p.M;
-          if constexpr (TN % 4 == 0) {
-            if (gg) {
+          for (int i = 0; i < TM; ++i) {
+            if (RES && i + PFD < TM) load_res(i + PFD);
+            const int m = m0 + wm0 + i * 16 + fr;
+            const bool row_ok = m < p.M;
+            if constexpr (TN % 4 == 0) {
+              if (gg) {
 #pragma unroll
-              for (int jp = 0; jp < TN / 4; ++jp) store_pair(i, jp, geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2), m, row_ok);
-              continue;
+                for (int jp = 0; jp < TN / 4; ++jp)
+                  store_pair(res_c, i, jp, geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2), m, row_ok);
+                continue;
+              }
             }
-          }
 #pragma unroll
-          for (int jp = 0; jp < NJ; ++jp) store_pair(i, jp, plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1), m, row_ok);
-          if constexpr (TAIL) {
-            f16x4 v = plain_frag(i, TN - 1);
-            if (has_res) {
+            for (int jp = 0; jp < NJ; ++jp) store_pair(res_c, i, jp, plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1), m, row_ok);
+            if constexpr (TAIL) {
+              f16x4 v = plain_frag(i, TN - 1);
+              if constexpr (RES) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + NJ][r]);
+                for (int r = 0; r < 4; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + NJ][r]);
+              }
+              const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
+              const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs,
+                                                    (row_ok && n < p.N) ? (int)off : (int)OOB, 0, 0);
             }
-            const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
-            const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs,
-                                                  (row_ok && n < p.N) ? (int)off : (int)OOB, 0, 0);
+            // one row block at a time: the scheduler may not pull later blocks' conversions / swaps up
+            // (their temporaries beside the live accumulators spill)
+            __builtin_amdgcn_sched_barrier(0);
           }
-          // one row block at a time: the scheduler may not pull later blocks' conversions / swaps up
-          // (their temporaries beside the live accumulators spill)
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        };
+        if (has_res) rows(std::true_type{});
+        else rows(std::false_type{});
         if (do_amax && !gg && blk_amax) {
           __syncthreads();
           for (int c = threadIdx.x; c < BN; c += NT) {
