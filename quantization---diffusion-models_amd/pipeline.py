@@ -9,6 +9,7 @@ per-step scheduler constants and a device step counter that the fused CFG+DDIM k
 increments, so one captured graph is replayed ``num_inference_steps`` times with no host work
 between steps.
 """
+import gc
 import zlib
 
 import torch
@@ -110,9 +111,20 @@ class DenoiseLoop:
             self.step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
+        # A dead Python cycle that still owns a graph, stream or event (an earlier pipeline, say)
+        # must not be finalised inside the capture: its destructor's HIP calls are illegal while
+        # a stream is capturing and abort the process.  Collect now, and keep the collector off
+        # until the capture has ended.
+        gc.collect()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.step(frozen=True)   # no allocation may happen inside the capture
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g):
+                self.step(frozen=True)   # no allocation may happen inside the capture
+        finally:
+            if gc_on:
+                gc.enable()
         self.graph = g
 
     @torch.no_grad()
