@@ -2827,7 +2827,9 @@ static bool halo_ok(const GemmArgs& p, int bn, int chunk = 64, int bm = 256) {
 // groups of RPT rows; RPT small enough that the launch has >= ~512 blocks - the slab read is
 // latency-bound, not bandwidth-bound, at the small M that splits K); slabs summed in split order
 // (deterministic: every RPT gives identical results); the RPT rows of a thread are loaded
-// together per split.  amax: one atomic per column per 4*RPT rows (rows_per_sample % 16 == 0).
+// together per split.  amax: one atomic per column per 4*RPT rows (rows_per_sample % 16 == 0),
+// of h = half(sum + bias), or - QD_EPI_AMAX_POST - of the final half(h + residual) (the post-residual
+// amax of an explicitly split plan: the GEMM's own epilogue then only writes the slabs).
 template <int RPT>
 __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   __shared__ float red[4][256];
@@ -2839,6 +2841,7 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
   const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
   const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+  const bool post = do_amax && has_res && (p.epi & QD_EPI_AMAX_POST);
   f16x4 bq = {};
   if (has_bias && col_ok) bq = *reinterpret_cast<const f16x4*>(p.bias + n);
   float cm[4] = {0.f, 0.f, 0.f, 0.f};
@@ -2889,7 +2892,7 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         h[r] = (f16)(s[rr][r] + (float)bq[r]);
-        cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
+        if (!post) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
       }
       if (gtanh) {
 #pragma unroll
@@ -2899,6 +2902,10 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs p) {
         const f16x4 rq = *reinterpret_cast<const f16x4*>(p.res + (long)m * p.ldy + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) h[r] = (f16)((float)h[r] + (float)rq[r]);
+      }
+      if (post) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cm[r] = fmaxf(cm[r], fabsf((float)h[r]));
       }
       *reinterpret_cast<f16x4*>(p.y + (long)m * p.ldy + n) = h;
     }
@@ -3436,7 +3443,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
     // an explicit split reduces the amax in its reduction kernel: only an unsplit tile needs every
     // wave's rows in one sample
     int fs0 = 0;
-    const bool fsplit = !geglu && !post && K % 64 == 0 && forced_split(K / 64, 4, fs0) && fs0 > 1;
+    const bool fsplit = !geglu && K % 64 == 0 && forced_split(K / 64, 4, fs0) && fs0 > 1;
     const bool ok = (fsplit || !amax || rows_per_sample % (d.bm / d.wgm) == 0) && (!geglu || d.bn % 32 == 0);
     if (ok) {
       best = {1, d.bm, d.bn, g_force - 100, 1, K};
@@ -3445,7 +3452,7 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
       const int per_cu = std::max(1, std::min(by_lds, by_waves));
       int fsp;
-      if (!geglu && !post && K % 64 == 0 && forced_split(K / 64, 4, fsp)) {
+      if (!geglu && K % 64 == 0 && forced_split(K / 64, 4, fsp)) {
         best.splits = fsp;
         best.kps = K / fsp;
       } else {
@@ -4132,7 +4139,9 @@ static void launch_i8(const GemmArgs& p, int var, hipStream_t st) {
 // variant: qd_gemm_force 110..117 (DMA variants 10-17, the 64-B-row family), else a default by
 // N; K (in the half view) splits into runs of whole 32-slot steps while the blocks fit one round
 // post: post-residual amax epilogue - the lock-step DMA tiles only (the ping-pong epilogue
-// reduces before its residual add; split-K slabs would run it in the reduce kernel)
+// reduces before its residual add); split only on an explicit split count (a tuner candidate:
+// k_splitk_reduce takes the post-residual amax), never by the heuristic below, so tuned unsplit
+// entries keep their plan
 // gn: GroupNorm-statistics / per-(sample, column) add epilogue - lock-step DMA tiles that lie in
 // one sample (rows_per_sample % BM == 0), or the halo conv; split-K plans reduce through
 // k_splitk_reduce_gn (64-row blocks)
@@ -4218,7 +4227,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   // blocks), so only an unsplit tile needs whole-sample rows: with an explicit split the requested tile
   // stands (the 8x8 level's GroupNorm convs otherwise all collapse to 64-row tiles, each re-reading the
   // whole weight once per 64 rows)
-  const bool fsplit = g_force >= 110 && !geglu && !post && !pdiv && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp) && fsp > 1;
+  const bool fsplit = g_force >= 110 && !geglu && !pdiv && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp) && fsp > 1;
   if (!fsplit) var = i8_unsplit_var(var, rows_per_sample, amax, gn);
   if (geglu && kDmaC[var].bn % 32 != 0) var = 11;
   const DmaVar& d = kDmaC[var];
@@ -4230,7 +4239,7 @@ static Plan plan_i8(int M, int N, int Kh, int rows_per_sample, bool amax, bool g
   const long tiles_mn = (long)((M + d.bm - 1) / d.bm) * ((N + d.bn - 1) / d.bn);
   const int by_lds = 163840 / (2 * dma_lds_halves(d.bm, d.bn, d.st, d.bkt)), by_waves = 2048 / (64 * d.wgm * d.wgn);
   const int per_cu = std::max(1, std::min(by_lds, by_waves));
-  if (g_force >= 110 && !geglu && !post && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp)) {
+  if (g_force >= 110 && !geglu && Kh % 32 == 0 && forced_split(Kh / 32, 8, fsp)) {
     pl.splits = fsp;
     pl.kps = Kh / fsp;
     return pl;

@@ -298,6 +298,9 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
   const int groups = c / cg;
   const int ni = blockIdx.x / groups, g0 = (blockIdx.x % groups) * cg;
   const int t = threadIdx.x;
+  // the affine parameters of the thread's first channel, loaded before the partials pass (their
+  // latency hides under it instead of following the group statistics)
+  const float gm0 = t < cg ? (float)gamma[g0 + t] : 0.f, bt0 = t < cg ? (float)beta[g0 + t] : 0.f;
   if (t == 0) nflag = 0;
   for (int j = t; j < cg; j += 256) {
     cmin[j] = 0x7fffffff;
@@ -351,11 +354,12 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     stat[1] = 1.0f / sqrtf(var + eps);
   }
   __syncthreads();
+  float gmx = 0.f;  // the thread's max over its channels' output amax (amax_n below)
   for (int j = t; j < cg; j += 256) {
     const int ch = g0 + j;
     const long i = (long)ni * c + ch;
-    const float sc = stat[1] * (float)gamma[ch];
-    const float2 k = make_float2(sc, fmaf(-sc, stat[0], (float)beta[ch]));
+    const float sc = stat[1] * (j == t ? gm0 : (float)gamma[ch]);
+    const float2 k = make_float2(sc, fmaf(-sc, stat[0], j == t ? bt0 : (float)beta[ch]));
     coef[i] = k;
     if (!quant) continue;
     const int ia = cmin[j], ib = cmax[j];
@@ -366,8 +370,10 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const float top = fabsf(gn_out(sc >= 0.f ? mx : mn, k, silu));  // largest z
     if (!silu) {
       amax[i] = fmaxf(lo, hi);
+      gmx = fmaxf(gmx, fmaxf(lo, hi));
     } else if (top >= SILU_NEG_BOUND) {
       amax[i] = top;
+      gmx = fmaxf(gmx, top);
     } else {
       flagged[atomicAdd(&nflag, 1)] = j;
     }
@@ -384,15 +390,19 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     m = wave_max(m);
     if ((t & 63) == 0) fmx[t >> 6] = m;
     __syncthreads();
-    if (t == 0) amax[i] = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));
+    if (t == 0) {
+      const float a = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));
+      amax[i] = a;
+      gmx = fmaxf(gmx, a);
+    }
     __syncthreads();
   }
   if (amax_n) {
-    // int8 output: this (n, group)'s max over its channels into amax_n[n][group]; the apply pass
-    // takes the max over the groups (no same-address atomics: they serialise across blocks)
-    float m = 0.f;
-    for (int j = t; j < cg; j += 256) m = fmaxf(m, amax[(long)ni * c + g0 + j]);
-    m = wave_max(m);
+    // int8 output: this (n, group)'s max over its channels into amax_n[n][group] - from the
+    // registers that wrote amax above (the scanned channels' values sit with thread 0), not a
+    // re-read of amax; the apply pass takes the max over the groups (no same-address atomics:
+    // they serialise across blocks)
+    float m = wave_max(gmx);
     if ((t & 63) == 0) fmx[t >> 6] = m;
     __syncthreads();
     if (t == 0) amax_n[blockIdx.x] = fmaxf(fmaxf(fmx[0], fmx[1]), fmaxf(fmx[2], fmx[3]));

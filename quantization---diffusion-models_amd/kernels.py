@@ -877,7 +877,7 @@ def linear_i8(xq, sa, wq, sw, bias=None, residual=None, out=None, amax=None, row
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
         c = _choose(key, list(I8_VARIANTS) + list(I8_PERSIST_VARIANTS) +
-                    ([] if epi & (EPI_GEGLU | EPI_AMAX_POST) else _i8_split_cands(M, N, Kd)),
+                    ([] if epi & EPI_GEGLU else _i8_split_cands(M, N, Kd)),
                     lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)

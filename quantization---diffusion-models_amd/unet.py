@@ -829,7 +829,8 @@ def transformer_fwd(tm, x, ctx_kv, pend=False, gn_out=False):
     q_out = 0 if tm.linear_proj or conv_i8(tm.proj_out) else conv_qbits(tm.proj_out)
     # int8-MFMA mode: the same epilogue amax gives proj_out's per-sample int8 scale
     i8_out = not tm.linear_proj and conv_i8(tm.proj_out) and lin_i8(tm.transformer_blocks[-1].ff.net[2])
-    want = (q_out > 0 or i8_out) and n * hh * ww >= AMAX_POST_MIN_ROWS and (hh * ww) % 64 == 0
+    # (at every level: where the GEMM splits K, its reduction kernel takes the post-residual amax)
+    want = (q_out > 0 or i8_out) and (hh * ww) % 64 == 0
     in_amax = None
     for bi, blk in enumerate(tm.transformer_blocks):
         last = bi == len(tm.transformer_blocks) - 1
@@ -993,11 +994,6 @@ def _out_ln(layer, x2d, t, norm, i8_next):
                 return K.linear_ln(x2d, w16, t, g, b, norm.eps, bias=bias, i8_out=i8h)
     t = run_linear(layer, x2d, residual=t)
     return t, (K.layernorm_i8 if i8h else K.layernorm)(t, norm.eps, g, b)
-
-
-# the post-residual amax epilogue runs unsplit (no split-K slabs): used where M is large enough
-# that the GEMM would not split anyway (the 64x64 and 32x32 levels of SD1.5 at CFG batch 8)
-AMAX_POST_MIN_ROWS = 8192
 
 
 def _fake_quant_gemm_operand(layer):

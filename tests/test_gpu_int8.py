@@ -114,8 +114,8 @@ def test_linear_i8_post_residual_amax_and_fused_scale(variant, dev):
     quant_samples_i8(x, amax_nc=...) (qd_quant_samples_i8_amax).  At the SD1.5 64x64 shape (two
     samples of 4096 tokens, K 1280 -> N 320): the output equals the plain residual call bit for bit,
     the amax equals the exact per-(sample, channel) max |output|, and the per-sample codes / scales
-    taken over that amax equal quant_samples_i8 of the output, for every tile variant (split-K ids
-    fall back to the unsplit plan this epilogue needs)."""
+    taken over that amax equal quant_samples_i8 of the output, for every tile variant (an explicit
+    split count reduces the post-residual amax in k_splitk_reduce: int32 slabs, the same bits)."""
     k = K()
     rng = np.random.default_rng(31)
     n, s, Kd, N = 2, 4096, 1280, 320

@@ -569,13 +569,16 @@ def forced_gemm():
     kernels.force_gemm(None)
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 3] + list(range(100, 118)) + [300, 301])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 3] + list(range(100, 118)) + [300, 301]
+                         # explicit split counts: the split-K reduction takes the post-residual amax
+                         + [2104, 4105, 5110, 2117])
 @pytest.mark.parametrize("fmt", ["f16", "i8"])
 def test_linear_post_residual_amax(variant, fmt, forced_gemm, dev):
     """QD_EPI_AMAX_POST: the epilogue adds the residual to the fragments and reduces the
     per-(sample, column) amax of the FINAL output (the consuming conv's input amax).  Output as
-    the plain residual epilogue's, amax equal to the exact max of that output (ping-pong and
-    split-K plans fall back to unsplit tiles that support it)."""
+    the plain residual epilogue's, amax equal to the exact max of that output (ping-pong plans
+    fall back to unsplit tiles that support it; an explicit split count reduces it in
+    k_splitk_reduce after the residual add)."""
     k = K()
     g = torch.Generator().manual_seed(11)
     M, N, Kd, rps = 4 * 1024, 320, 1280, 1024
@@ -593,9 +596,9 @@ def test_linear_post_residual_amax(variant, fmt, forced_gemm, dev):
     amax = torch.full((M // rps * N,), 123.0, device=dev)  # the call zeroes it (amax_zeroed=False)
     got = k.linear(x, op, fmt, sc, grp, bias=b, residual=r, weight_f16=wf, amax=amax, rows_per_sample=rps,
                    amax_post=True)
-    # (the plain call may split K - another fp32 summation order - where the post-residual one
-    # never does: the outputs agree to the fp16 rounding of the projection, an ulp of which can
-    # exceed an ulp of the output where the residual cancels it)
+    # (the two calls may take different split counts - another fp32 summation order: the outputs
+    # agree to the fp16 rounding of the projection, an ulp of which can exceed an ulp of the
+    # output where the residual cancels it)
     gc, pc, rc = got.cpu().float(), plain.cpu().float(), r.cpu().float()
     assert ((gc - pc).abs() <= 2 * ulp16(pc.abs() + rc.abs()) + 1e-3).all()
     ref = got.float().abs().view(M // rps, rps, N).amax(1).reshape(-1)
