@@ -184,6 +184,12 @@ int qd_conv2d_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const 
 int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n_bits,
                    const void* residual, const void* chan_add, int chan_add_ld, void* out,
                    void* stream);
+/* Measurement knobs (sweep scripts only; process-wide, not thread-safe): the per-channel column-max
+ * launch geometry (min_blocks / max_rows_per_thread, <= 0: the defaults 128 / 64) and the attention
+ * kernel choice (0: heuristic; 1-6 the 16x16x32 k_attn configurations, 7 / 8 the 32x32x16 kernel
+ * with 4 / 8 waves). */
+int qd_colmax_geom_force(int min_blocks, int max_rows_per_thread);
+int qd_attn_force(int cfg);
 /* qd_conv2d_fwd (epi = QD_EPI_AMAX [| QD_EPI_AMAX_ZEROED | QD_EPI_BIAS]) followed by
  * qd_fq_finalize(y, amax, ..., n_bits, residual, chan_add, chan_add_ld, out = y): when the plan splits
  * K and a sample's Ho*Wo rows (<= 256, a multiple of 32) fit one reduction block, the split-K

@@ -36,6 +36,8 @@ SIGNATURES = {
     "qd_conv2d_fwd": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P, P, I, P, P, ctypes.c_long, P],
     "qd_conv2d_fq": [P, I, I, I, I, I, P, I, I, I, I, I, I, P, I, P, P, I, P, I, P, P, P, ctypes.c_long, P],
     "qd_fq_finalize": [P, P, I, I, I, I, P, P, I, P, P],
+    "qd_colmax_geom_force": [I, I],
+    "qd_attn_force": [I],
     "qd_groupnorm": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P],
     "qd_groupnorm_xamax": [P, P, I, I, I, I, I, F, P, P, I, I, P, P, P, P],
     "qd_groupnorm_fq_in": [P, P, I, P, I, I, I, I, I, F, P, P, I, I, P, P, P],

@@ -612,16 +612,15 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   }
 }
 
-// tuning knob (benchmark sweeps only): QD_ATTN_CFG = 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2) of k_attn;
-// 6 = k_attn (heuristic) instead of k_attn32 at d = 40 / 80; 7 / 8 = k_attn32 with 4 / 8 waves;
-// unset: heuristic
-static int attn_forced() {
-  static const int forced = [] {
-    const char* e = getenv("QD_ATTN_CFG");
-    return e ? atoi(e) : 0;
-  }();
-  return forced;
+// measurement knob (qd_attn_force, benchmark sweeps only): 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2) of
+// k_attn; 6 = k_attn (heuristic) instead of k_attn32 at d = 40 / 80; 7 / 8 = k_attn32 with 4 / 8
+// waves; 0: heuristic
+static int g_attn_cfg = 0;
+extern "C" int qd_attn_force(int cfg) {
+  g_attn_cfg = cfg > 0 ? cfg : 0;
+  return 0;
 }
+static int attn_forced() { return g_attn_cfg; }
 
 template <int D, int DP, int DV>
 static void launch32(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
@@ -722,7 +721,7 @@ static int attention_impl(const void* q, int ldq, const void* k, int ldk, const 
   // DP: QK^T depth (multiple of 32 >= d); DV: PV rows, a multiple of 16 > d (row d = denominator)
   // the 32x32x16 kernel (QK^T depth: head dims + the running-max column, PV rows: head dims + the
   // denominator row, both rounded up) at head_dim 40 / 80 (at 64 - DP 80, DV 96 - it measured
-  // slower than k_attn: profiles/r04m_attn_ab.log); QD_ATTN_CFG 1-6 select k_attn, 7 / 8 force
+  // slower than k_attn: profiles/r04m_attn_ab.log); qd_attn_force 1-6 select k_attn, 7 / 8 force
   // k_attn32 with 4 / 8 waves
   const int fc = attn_forced();
   if (!c && (fc == 0 || fc == 7 || fc == 8) && (d == 40 || d == 80)) {

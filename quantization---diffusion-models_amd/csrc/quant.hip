@@ -109,16 +109,16 @@ __global__ void __launch_bounds__(256) k_colmax_nhwc(const f16* __restrict__ x, 
 // serialise (per-XCD L2s: they resolve beyond L2), so the row splits per sample - the atomic
 // chain length per address - are kept short: measured (rocprofv3, scripts/colmax_sweep.sh)
 // 16.4 -> 8.4 us at [8, 64x64, 320] and 16.4 -> 5.2 us at [8, 16x16, 1280] against the old
-// >= 512-block geometry.  QD_COLMAX_MINBLK / QD_COLMAX_MAXRPT: sweep-only overrides.
+// >= 512-block geometry.  qd_colmax_geom_force: the sweep's override (measurement knob).
+static int g_colmax_minblk = 128, g_colmax_maxrpt = 64;
+extern "C" int qd_colmax_geom_force(int min_blocks, int max_rows_per_thread) {
+  g_colmax_minblk = min_blocks > 0 ? min_blocks : 128;
+  g_colmax_maxrpt = max_rows_per_thread > 0 ? max_rows_per_thread : 64;
+  return 0;
+}
+
 static void colmax_launch(const f16* x, const f16* x2, int c1, int n, long hw, int c, float* amax, hipStream_t st) {
-  static const int minblk = [] {
-    const char* e = getenv("QD_COLMAX_MINBLK");
-    return e ? atoi(e) : 128;
-  }();
-  static const int maxrpt = [] {
-    const char* e = getenv("QD_COLMAX_MAXRPT");
-    return e ? atoi(e) : 64;
-  }();
+  const int minblk = g_colmax_minblk, maxrpt = g_colmax_maxrpt;
   const int chunks = c / 8;
   const int bx = chunks < 64 ? chunks : 64, by = 256 / bx;
   const int gx = (chunks + bx - 1) / bx;

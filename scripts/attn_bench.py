@@ -1,12 +1,15 @@
 """Attention kernel timing on the path's shapes (HIP events), for configuration sweeps:
-QD_ATTN_CFG=1|2|3 python scripts/attn_bench.py"""
+python scripts/attn_bench.py [cfg]   (cfg: qd_attn_force - 1|2|3|5|6 k_attn, 7|8 k_attn32 waves)"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import qdiff_boot  # noqa
+from qdiff import _lib
 from qdiff import kernels as K
 
 dev = "cuda:0"
+CFG = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+_lib.load().qd_attn_force(CFG)
 for (b, s, skv, heads, d, ld) in ((8, 4096, 4096, 8, 40, 960), (8, 1024, 1024, 10, 64, 1920), (2, 4429, 4429, 38, 64, 7296),
                                   (8, 4096, 77, 8, 40, 320), (8, 1024, 1024, 8, 80, 1920), (8, 256, 256, 8, 160, 3840),
                                   (4, 4096, 4096, 10, 64, 1920), (4, 1024, 1024, 20, 64, 3840)):
@@ -24,4 +27,4 @@ for (b, s, skv, heads, d, ld) in ((8, 4096, 4096, 8, 40, 960), (8, 1024, 1024, 1
     e1.synchronize()
     us = e0.elapsed_time(e1) / 10 * 1e3
     fl = 4.0 * b * heads * s * skv * d
-    print(f"cfg={os.environ.get('QD_ATTN_CFG', '-')} b={b} sq={s} skv={skv} h={heads} d={d}: {us:.1f} us  {fl / us / 1e6:.0f} TFLOP/s", flush=True)
+    print(f"cfg={CFG or '-'} b={b} sq={s} skv={skv} h={heads} d={d}: {us:.1f} us  {fl / us / 1e6:.0f} TFLOP/s", flush=True)

@@ -4,5 +4,5 @@ cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 for cfg in "512 16" "512 64" "128 64" "32 64" "8 256"; do
 set -- $cfg
-QD_COLMAX_MINBLK=$1 QD_COLMAX_MAXRPT=$2 timeout -k 10 90 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/cm_$1_$2 -o run -- python3 $R/scripts/colmax_sweep.py > /dev/null 2>&1
+timeout -k 10 90 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/cm_$1_$2 -o run -- python3 $R/scripts/colmax_sweep.py $1 $2 > /dev/null 2>&1
 done
