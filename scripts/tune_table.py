@@ -122,6 +122,9 @@ def main():
                     help="with --add: also drop the fp16 / int8 conv entries whose input side is <= this")
     ap.add_argument("--retune-i8-linear", action="store_true",
                     help="keep the committed table, re-tune only the int8 linears (SD1.5, both modes run)")
+    ap.add_argument("--retune-f16-linear", action="store_true",
+                    help="keep the committed table, re-tune only the fp16-path linears without int4 operands "
+                         "(SD1.5, both modes run)")
     ap.add_argument("--retune-i4", action="store_true",
                     help="keep the committed table, re-tune only the linears whose operands include packed int4")
     a = ap.parse_args()
@@ -130,6 +133,13 @@ def main():
         K.load_table(OUT)
         dropped = {k: K._TUNE.pop(k) for k in [k for k in K.gemm_choices() if k[0] == "linear_i8"]}
         log(f"committed table without its {len(dropped)} int8 linears")
+        run_sd15(dev)
+        for key, ch in dropped.items():  # shapes this run does not meet keep their committed choice
+            K._TUNE.setdefault(key, ch)
+    elif a.retune_f16_linear:
+        K.load_table(OUT)
+        dropped = {k: K._TUNE.pop(k) for k in [k for k in K.gemm_choices() if k[0] == "linear" and "i4" not in k[-1]]}
+        log(f"committed table without its {len(dropped)} fp16-path linears")
         run_sd15(dev)
         for key, ch in dropped.items():  # shapes this run does not meet keep their committed choice
             K._TUNE.setdefault(key, ch)
