@@ -127,6 +127,8 @@ def main():
                          "(SD1.5, both modes run)")
     ap.add_argument("--retune-f16-conv", action="store_true",
                     help="keep the committed table, re-tune only the fp16-path convs (SD1.5, both modes run)")
+    ap.add_argument("--retune-i8-conv", action="store_true",
+                    help="keep the committed table, re-tune only the int8 convs (SD1.5, both modes run)")
     ap.add_argument("--retune-i4", action="store_true",
                     help="keep the committed table, re-tune only the linears whose operands include packed int4")
     a = ap.parse_args()
@@ -149,6 +151,13 @@ def main():
         K.load_table(OUT)
         dropped = {k: K._TUNE.pop(k) for k in [k for k in K.gemm_choices() if k[0] == "conv"]}
         log(f"committed table without its {len(dropped)} fp16-path convs")
+        run_sd15(dev)
+        for key, ch in dropped.items():  # shapes this run does not meet keep their committed choice
+            K._TUNE.setdefault(key, ch)
+    elif a.retune_i8_conv:
+        K.load_table(OUT)
+        dropped = {k: K._TUNE.pop(k) for k in [k for k in K.gemm_choices() if k[0] == "conv_i8"]}
+        log(f"committed table without its {len(dropped)} int8 convs")
         run_sd15(dev)
         for key, ch in dropped.items():  # shapes this run does not meet keep their committed choice
             K._TUNE.setdefault(key, ch)
