@@ -356,8 +356,12 @@ def cpu_baseline(threads):
     shapes = {k: torch.empty(v.shape, dtype=torch.float16) for k, v in net.state_dict().items()}
     cd = {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(SD15).items()}
     note = None
+    usable, unote = usable_cores()
     if threads is None:
-        threads, note = usable_cores()
+        threads, note = usable, unote
+    elif threads > usable:  # (an explicit count above the affinity / quota oversubscribes: ADVICE r5)
+        note = f"--cpu-threads {threads} capped to the {usable} usable cores ({unote})"
+        threads = usable
     r = CB.c1_baseline(cd, shapes, threads=threads)
     pc = r["per_class"]
     return {"value": round(1.0 / r["seconds_per_image"], 8), "unit": "images/s", "cores": r["threads"],
@@ -720,7 +724,7 @@ def main_sd35(args, model, rank, world, dev, log):
             line["weight_stream"] = weight_footprint(model)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            line["cpu_baseline"] = cpu_baseline_sd35(args.cpu_threads or usable_cores()[0], cfg, s, sc,
+            line["cpu_baseline"] = cpu_baseline_sd35(min(args.cpu_threads or 1 << 30, usable_cores()[0]), cfg, s, sc,
                                                      args.denoise_steps)
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -81,6 +81,12 @@ int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, 
  * (amax [n*(c1+c2)], e.g. qd_groupnorm_xamax over the same concat): no column-max pass. */
 int qd_act_apply_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,
                           const float* amax, void* y, void* stream);
+/* NHWC per_channel fake-quant (qd_act_absmax + qd_act_apply, fake_quant.py:123-131) of a SMALL tensor
+ * in one launch, one workgroup per sample: x, y [n][hw][c] (y may alias x), channels >= c_valid
+ * (c_valid > 0) copied as is; same bits as the two passes.  qd_act_fq_small_ok(hw, c) (returns 0/1,
+ * no status): c % 8 == 0, c / 8 a power of two, hw * c / 8 <= 4096 (the UNet's conv_in latent). */
+int qd_act_fq_small_ok(int hw, int c);
+int qd_act_fq_small_nhwc(const void* x, void* y, int n, int hw, int c, int c_valid, int n_bits, void* stream);
 
 /* ---------------- weight fake-quant (offline, on device) ----------------------------- */
 /* Row-group absmax RTN of quantize_weight_absmax / _per_channel_ / _per_tensor_
@@ -125,6 +131,9 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
                                 GroupNorm (qd_groupnorm_part) needs no statistics pass over the
                                 tensor; rows_per_sample % 64 == 0, never ping-pong tiles */
 #define QD_EPI_LN 512        /* (set by qd_linear_ln / qd_linear_i8_ln) */
+#define QD_EPI_SILU 1024     /* qd_linear_fwd GEMV shapes only (M <= 8): out = half(silu(out)) after the
+                                bias / residual rounding - the diffusers TimestepEmbedding act and
+                                the UNet's silu(temb), bit-identical to qd_silu on the output */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.
@@ -133,8 +142,9 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
  * ping-pong families (qd_gemm_force 110..117, 300..304), dequantized from LDS per fragment with the
  * register tile's rounding (bit-identical results).  lda/ldy in elements.
  * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32).
- * M <= 4 without AMAX / GEGLU runs a weight-stream GEMV (same dequant and epilogue rounding;
- * environment QD_NO_GEMV, read at the first call, keeps the tile GEMM for every M). */
+ * M <= 8 (K <= 2048 at M 5..8) without AMAX / GEGLU runs a weight-stream GEMV (same dequant and
+ * epilogue rounding; v_dot2 fp32 accumulation instead of the MFMA's, so only the summation order
+ * differs from the tile GEMM); QD_EPI_SILU requires such a shape. */
 int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
                   const void* wscale, const void* wscale_t, int group, const void* bias,
                   const void* residual, void* y, int N, int ldy, int epi, float* amax,
@@ -187,7 +197,7 @@ int qd_fq_finalize(const void* y, const float* amax, int n, int hw, int c, int n
 /* Measurement knobs (sweep scripts only; process-wide, not thread-safe): the per-channel column-max
  * launch geometry (min_blocks / max_rows_per_thread, <= 0: the defaults 128 / 64) and the attention
  * kernel choice (0: heuristic; 1-6 the 16x16x32 k_attn configurations, 7 / 8 the 32x32x16 kernel
- * with 4 / 8 waves). */
+ * with 4 / 8 waves (8: the staggered form the heuristic runs), 9 the 8-wave kernel unstaggered). */
 int qd_colmax_geom_force(int min_blocks, int max_rows_per_thread);
 int qd_attn_force(int cfg);
 /* qd_conv2d_fwd (epi = QD_EPI_AMAX [| QD_EPI_AMAX_ZEROED | QD_EPI_BIAS]) followed by

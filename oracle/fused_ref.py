@@ -168,6 +168,13 @@ def linear(a, outs):
     r = a.get("residual")
     amax = a.get("amax")
     post = bool(a.get("amax_post")) and amax is not None and r is not None
+    if a.get("silu"):
+        # GEMV epilogue SiLU (diffusers TimestepEmbedding act / the UNet's silu(temb)) on the rounded
+        # output: silu' <= 1.0998 carries the summation-order slack, +1 ulp for the SiLU itself
+        out = (y16.float() + r.float()).half() if r is not None else y16
+        res.append(Out("y", F.silu(out.float()).half(), atol=1.1 * atol, ulps=3,
+                       ulp_of=y16 if r is not None else None))
+        return res
     if r is not None:
         out = (y16.float() + r.float()).half()
         res.append(Out("y", out, atol=atol, ulps=1, ulp_of=y16))
@@ -324,6 +331,16 @@ def act_apply_nhwc(a, outs):
     return [Out("y", y, ulps=0)]
 
 
+def act_fq_nhwc_small(a, outs):
+    """kernels.act_fq_nhwc_small = act_absmax + act_apply_nhwc in one launch: bit-exact."""
+    x, cv = a["x"], a.get("c_valid", 0)
+    y = per_channel_nhwc(x, a["n_bits"])[0]
+    if cv:
+        y = y.clone()
+        y[..., cv:] = x[..., cv:]
+    return [Out("y", y, ulps=0)]
+
+
 def act_quant_cat_nhwc(a, outs):
     return [Out("y", per_channel_nhwc(torch.cat([a["x"], a["x2"]], dim=-1), a["n_bits"])[0], ulps=0)]
 
@@ -351,6 +368,7 @@ LAUNCHES = {
     "attention": attention,
     "act_absmax": act_absmax,
     "act_apply_nhwc": act_apply_nhwc,
+    "act_fq_nhwc_small": act_fq_nhwc_small,
     "act_quant_cat_nhwc": act_quant_cat_nhwc,
     "concat_c": concat_c,
     "silu": silu,

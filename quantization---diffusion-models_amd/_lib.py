@@ -29,6 +29,7 @@ SIGNATURES = {
     "qd_act_apply": [P, P, I, I, I, I, I, I, I, I, P, P],
     "qd_act_quant_cat_nhwc": [P, I, P, I, I, I, I, P, I, P, P],
     "qd_act_apply_cat_nhwc": [P, I, P, I, I, I, I, P, P, P],
+    "qd_act_fq_small_nhwc": [P, P, I, I, I, I, I, P],
     "qd_weight_quant": [P, I, I, I, I, P, P, P, P],
     "qd_pack_int4": [P, I, I, P, P],
     "qd_conv_weight_khwc": [P, I, I, I, I, I, P, P],
@@ -100,6 +101,7 @@ QUERIES = {
     "qd_gemm_workspace": ([I, I, I, I, I, I, I], ctypes.c_long),
     "qd_groupnorm_workspace": ([I, I, I, I], I),
     "qd_gemm_i8_workspace": ([I, I, I, I, I], ctypes.c_long),
+    "qd_act_fq_small_ok": ([I, I], I),
 }
 
 _lib = None

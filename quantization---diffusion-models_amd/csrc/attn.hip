@@ -368,12 +368,20 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const f16* __restrict__ q, int
 // transposed reads, 32 v_exp_f32 + 16 packs as before.
 constexpr int v_stride32(int dv) { return (dv + 31) / 64 * 64 + 32; }  // 16 x odd dwords per row
 
-template <int D, int DP, int DV, int NB, int NW>
+// STAG (8 waves): a half-tile stagger between the two waves that share a SIMD (waves w and w + 4;
+// MI355X_MICROARCH "Two waves per SIMD", item 9).  The late half (waves 4-7) runs the softmax + PV of
+// tile t - 1 and THEN the QK^T of tile t in the interval between barriers t and t + 1, so on every SIMD
+// one wave's QK^T MFMAs meet its partner's exp / pack VALU instead of the partners issuing the same
+// phase in lock step.  Its scores stay in registers across the barrier; V tiles get a third LDS buffer
+// (tile t - 1's V is still read while tile t + 1 is staged).  Per query the same operations in the same
+// order as the unstaggered kernel: bit-identical output.
+template <int D, int DP, int DV, int NB, int NW, bool STAG = false>
 __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                 int ldk, const f16* __restrict__ v, int ldv,
                                                 f16* __restrict__ o, int ldo, int heads, int sq, int skv,
                                                 float scale_log2) {
   static_assert(DP % 16 == 0 && DV % 32 == 0 && NB == 2, "k_attn32 shapes");
+  static_assert(!STAG || NW == 8, "the stagger pairs waves w and w + 4 of an 8-wave block");
   constexpr int d = D;                      // head_dim; depth d is the running-max column
   constexpr int CD = D / 8;                 // data chunks per row; chunk CD holds the ones column
   static_assert(D % 8 == 0 && DP >= D + 8 && D < DV, "k_attn32 head geometry");
@@ -384,10 +392,13 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   constexpr int KCHP = KCH | 1;
   constexpr int VST = v_stride32(DV);
   constexpr int KSZ = KV_T * KCHP * 8, VSZ = KV_T * VST;
+  constexpr int NVB = STAG ? 3 : 2;         // V tile buffers (K: always 2)
   constexpr int NT = NW * 64;
   constexpr int NL = (KV_T * CD + NT - 1) / NT;  // staged chunks per thread (d / 8 per row)
   constexpr int DB = DV / 32;               // 32-row O^T blocks
-  __shared__ __attribute__((aligned(16))) f16 smem[NB * (KSZ + VSZ)];
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * KSZ + NVB * VSZ];
+  f16* const kbuf = smem;                   // K tile t in kbuf + (t & 1) * KSZ
+  f16* const vbuf = smem + 2 * KSZ;         // V tile t in vbuf + (t % NVB) * VSZ
 
   constexpr int QB = NW * 32;
   const int nqb = (sq + QB - 1) / QB;
@@ -399,6 +410,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   const int q0 = (wg - bh * nqb) * QB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5, fr = lane & 15;
+  const bool late = STAG && wid >= NW / 2;
 
   const f16* qb = q + (long)b * sq * ldq + h * d;
   const f16* kb = k + (long)b * skv * ldk + h * d;
@@ -420,16 +432,16 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   }
 
   // padding, written once: K chunk d/8 = {1, 0, ..}, further chunks 0; V column d = 1.0, columns > d 0
-  for (int i = tid; i < NB * KV_T * (KCHP - CD); i += NT) {
+  for (int i = tid; i < 2 * KV_T * (KCHP - CD); i += NT) {
     const int np = KCHP - CD;
     const int bf = i / (KV_T * np), row = (i / np) % KV_T, c = CD + i % np;
     f16x8 z = {};
     if (c == CD) z[0] = (f16)1.0f;
-    *reinterpret_cast<f16x8*>(smem + bf * (KSZ + VSZ) + row * KCHP * 8 + c * 8) = z;
+    *reinterpret_cast<f16x8*>(kbuf + bf * KSZ + row * KCHP * 8 + c * 8) = z;
   }
-  for (int i = tid; i < NB * KV_T * (VST - d); i += NT) {
+  for (int i = tid; i < NVB * KV_T * (VST - d); i += NT) {
     const int bf = i / (KV_T * (VST - d)), row = (i / (VST - d)) % KV_T, col = d + i % (VST - d);
-    smem[bf * (KSZ + VSZ) + KSZ + row * VST + col] = (f16)(col == d ? 1.0f : 0.0f);
+    vbuf[bf * VSZ + row * VST + col] = (f16)(col == d ? 1.0f : 0.0f);
   }
 
   const unsigned kbytes = (unsigned)(((long)(skv - 1) * ldk + d) * 2);
@@ -445,7 +457,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
     koff[i] = (unsigned)(row * ldk + c * 8) * 2u;
     voff[i] = (unsigned)(row * ldv + c * 8) * 2u;
     kdst[i] = ok ? row * KCHP * 8 + c * 8 : -1;
-    vdst[i] = ok ? KSZ + row * VST + c * 8 : -1;
+    vdst[i] = ok ? row * VST + c * 8 : -1;
   }
   // two register staging sets: tile t + 2 is loaded while tile t is computed and stored to LDS
   // after tile t + 1, so an L2 round trip has two tiles of compute to land in
@@ -458,12 +470,12 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
       vst[set][i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, (int)(voff[i] + vs0), 0, 0));
     }
   };
-  auto store_tile = [&](int set, f16* base) {
+  auto store_tile = [&](int set, f16* kbase, f16* vbase) {
 #pragma unroll
     for (int i = 0; i < NL; ++i)
       if (kdst[i] >= 0) {
-        *reinterpret_cast<f16x8*>(base + kdst[i]) = kst[set][i];
-        *reinterpret_cast<f16x8*>(base + vdst[i]) = vst[set][i];
+        *reinterpret_cast<f16x8*>(kbase + kdst[i]) = kst[set][i];
+        *reinterpret_cast<f16x8*>(vbase + vdst[i]) = vst[set][i];
       }
   };
 
@@ -483,7 +495,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
       kread[jb][s] = row * KCHP * 8 + c * 8;
     }
   // 16-lane group g = lane >> 4 reads rows 4lh + (0..3) (+8 for elements 4..7) x columns 16(g & 1) + 0..15
-  const int vread = KSZ + (4 * lh + (fr >> 2)) * VST + 16 * ((lane >> 4) & 1) + (fr & 3) * 4;
+  const int vread = (4 * lh + (fr >> 2)) * VST + 16 * ((lane >> 4) & 1) + (fr & 3) * 4;
 
   const int ntiles = (skv + KV_T - 1) / KV_T;
   // S'^T = K (c Q)^T - m of the 64-key tile at ks (kv0 = its first key), keys past skv -> -inf
@@ -503,10 +515,11 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
           if (kv0 + jb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh >= skv) sacc[jb][r] = -INFINITY;
     }
   };
-  // online softmax of one tile's scores + O^T += V^T P^T from the tile's V at ks
-  // (a software-pipelined form - QK^T of tile t + 1 issued before the softmax of tile t, three LDS
-  // buffers - measured 339 vs 250 us: its 165 VGPRs leave one 8-wave block per CU)
-  auto softmax_pv = [&](const f16* ks, f32x16 (&sacc)[2], auto first_tag) {
+  // online softmax of one tile's scores -> P (fp16, the PV MFMA's B operand) and O^T += V^T P^T from
+  // the tile's V at vs (a software-pipelined form - QK^T of tile t + 1 issued before the softmax of
+  // tile t, three LDS buffers - measured 339 vs 250 us: its 165 VGPRs leave one 8-wave block per CU)
+  f16x8 pf[2][2];
+  auto softmax = [&](f32x16 (&sacc)[2], auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
     // lane max of the 32 scores: a depth-4 tree of three-input maxes
     float lmx;
@@ -534,20 +547,21 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
       mrow = mnew;
       if (lh == (CD & 1)) qf[CD / 2][0] = (f16)(-mnew);
     }
-    f16x8 pf[2][2];
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int e = 0; e < 8; ++e) pf[jb][s][e] = (f16)__builtin_amdgcn_exp2f(sacc[jb][8 * s + e]);
+  };
+  auto pv = [&](const f16* vs) {
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int j = 0; j < DB; ++j) {
-          const f16* vp = ks + vread + (32 * jb + 16 * s) * VST + 32 * j;
+          const f16* vp = vs + vread + (32 * jb + 16 * s) * VST + 32 * j;
           const f16x4 lo = tr_read(vp);
           const f16x4 hi = tr_read(vp + 8 * VST);
           const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -556,41 +570,52 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   };
 
   {
-    auto tile = [&](const f16* ks, int kv0, auto first_tag) {
-      f32x16 sacc[2];
-      qk(ks, kv0, sacc);
-      softmax_pv(ks, sacc, first_tag);
+    using T = std::true_type;
+    using F = std::false_type;
+    f32x16 sacc[2];
+    // tile t (K at kt, V at vt): the early half (all waves when !STAG) runs QK^T, softmax and PV of
+    // tile t; the late half runs the PV of tile t - 1 (V at vp, P from the previous interval), then
+    // QK^T and softmax of tile t, whose P it keeps across the barrier (16 VGPRs: fewer than the
+    // 32 fp32 scores, so the stagger keeps two 8-wave blocks per CU)
+    auto run = [&](int t, const f16* kt, const f16* vt, const f16* vp, auto first_tag) {
+      if (!late) {
+        qk(kt, t * KV_T, sacc);
+        softmax(sacc, first_tag);
+        pv(vt);
+      } else {
+        if (t > 0) pv(vp);
+        qk(kt, t * KV_T, sacc);
+        softmax(sacc, first_tag);
+      }
     };
-    // K/V double buffer in LDS (odd tiles in b1 / staging set 1, even tiles in b0 / set 0), tile
-    // loop unrolled x2 after the peeled first tile; one barrier per tile
-    f16* const b0 = smem;
-    f16* const b1 = smem + KSZ + VSZ;
+    auto vof = [&](int t) { return vbuf + (NVB == 2 ? (t & 1) : t % 3) * VSZ; };
+    // one barrier per tile; K double-buffered, V in NVB buffers; register staging sets alternate
+    // (tile t in set t & 1, loaded two tiles ahead: unconditional loads - past the last tile they
+    // read zeros off the buffer's end - so every path has the same loads in flight)
     load_tile(0, 0);
     __syncthreads();  // padding writes above
-    store_tile(0, b0);
+    store_tile(0, kbuf, vbuf);
     __syncthreads();
     load_tile(1, KV_T);
     load_tile(0, 2 * KV_T);
-    tile(b0, 0, std::true_type{});
+    run(0, kbuf, vbuf, nullptr, T{});
     int t = 1;
-    for (; t + 1 < ntiles; t += 2) {  // tiles t (b1) and t + 1 (b0)
-      // (unconditional loads - past the last tile they read zeros off the buffer's end - so every
-      // path through the loop has the same loads in flight and the staging stores wait for their
-      // own set only, vmcnt(2))
-      store_tile(1, b1);
+    for (; t + 1 < ntiles; t += 2) {  // tiles t (K buffer 1 / set 1) and t + 1 (K buffer 0 / set 0)
+      store_tile(1, kbuf + KSZ, vof(t));
       __syncthreads();
       load_tile(1, (t + 2) * KV_T);
-      tile(b1, t * KV_T, std::false_type{});
-      store_tile(0, b0);
+      run(t, kbuf + KSZ, vof(t), vof(t - 1), F{});
+      store_tile(0, kbuf, vof(t + 1));
       __syncthreads();
       load_tile(0, (t + 3) * KV_T);
-      tile(b0, (t + 1) * KV_T, std::false_type{});
+      run(t + 1, kbuf, vof(t + 1), vof(t), F{});
     }
     if (t < ntiles) {  // odd tail
-      store_tile(1, b1);
+      store_tile(1, kbuf + KSZ, vof(t));
       __syncthreads();
-      tile(b1, t * KV_T, std::false_type{});
+      run(t, kbuf + KSZ, vof(t), vof(t - 1), F{});
     }
+    if (late) pv(vof(ntiles - 1));  // the late half's last PV (no barrier follows: that V stays put)
   }
   // ---- epilogue: lane holds O^T rows 32j + 8(r>>2) + 4lh + (r&3) of query qrow; row d = sum(P) ----
   constexpr int dj = d >> 5, dw = d & 31, dh = (dw >> 2) & 1, drr = (dw & 3) + 4 * (dw >> 3);
@@ -614,7 +639,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
 
 // measurement knob (qd_attn_force, benchmark sweeps only): 1 (8x2), 2 (8x1), 3 (4x1), 5 (4x2) of
 // k_attn; 6 = k_attn (heuristic) instead of k_attn32 at d = 40 / 80; 7 / 8 = k_attn32 with 4 / 8
-// waves; 0: heuristic
+// waves (8: staggered); 9 = k_attn32, 8 waves without the stagger; 0: heuristic
 static int g_attn_cfg = 0;
 extern "C" int qd_attn_force(int cfg) {
   g_attn_cfg = cfg > 0 ? cfg : 0;
@@ -628,9 +653,16 @@ static void launch32(const void* q, int ldq, const void* k, int ldk, const void*
   const float sl2 = scale * 1.4426950408889634f;
   const int forced = attn_forced();
   // 8 waves (256 queries share each staged K / V tile) while the grid keeps >= 512 blocks
-  if (forced == 8 || (forced != 7 && (long)((sq + 255) / 256) * b * heads >= 512)) {
-    k_attn32<D, DP, DV, 2, 8><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
-        (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
+  if (forced == 8 || forced == 9 || (forced != 7 && (long)((sq + 255) / 256) * b * heads >= 512)) {
+    // the stagger pays on long key sequences (SD1.5 64x64 self-attention: 254 -> 247 / 261 -> 257 us in
+    // alternating rounds, profiles/r06b_attn_ab.log) and costs on 2-tile ones (77-token cross-attention
+    // 21.5 -> 22.9 us: the late half's extra interval is not hidden)
+    if (forced == 9 || (forced != 8 && skv < 512))  // the unstaggered 8-wave kernel
+      k_attn32<D, DP, DV, 2, 8, false><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
+          (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
+    else
+      k_attn32<D, DP, DV, 2, 8, true><<<((sq + 255) / 256) * b * heads, 512, 0, st>>>(
+          (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
   } else {
     k_attn32<D, DP, DV, 2, 4><<<((sq + 127) / 128) * b * heads, 256, 0, st>>>(
         (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, sq, skv, sl2);
@@ -724,7 +756,7 @@ static int attention_impl(const void* q, int ldq, const void* k, int ldk, const 
   // slower than k_attn: profiles/r04m_attn_ab.log); qd_attn_force 1-6 select k_attn, 7 / 8 force
   // k_attn32 with 4 / 8 waves
   const int fc = attn_forced();
-  if (!c && (fc == 0 || fc == 7 || fc == 8) && (d == 40 || d == 80)) {
+  if (!c && (fc == 0 || fc == 7 || fc == 8 || fc == 9) && (d == 40 || d == 80)) {
     if (d == 40) launch32<40, 48, 64>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, scale, st);
     else launch32<80, 96, 96>(q, ldq, k, ldk, v, ldv, o, ldo, b, heads, sq, skv, scale, st);
     QD_CHECK_LAUNCH();

@@ -1797,6 +1797,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
         al.init(p, m0n, kbn, wid);
         bl.init(p, n0n, wid);
         prologue(kbn, nkn);
+        // the first K step's counted wait (wait_vm_rt(... + nst) above) assumes exactly the nst
+        // stores below are younger than the DMA just issued: pin that issue order against both the
+        // IR (memory clobber) and the machine scheduler (sched_barrier 0: nothing crosses)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         nst = direct_stores<TM, TN>(p, wo, m0, n0, wm0, wn0);
       }
     }
@@ -3690,6 +3695,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
   const bool has_bias = (p.epi & QD_EPI_BIAS) && p.bias;
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
   const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
+  const bool silu = (p.epi & QD_EPI_SILU) != 0;
   const long nwaves = (long)gridDim.x * 4;
   for (long n0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R; n0 < p.N; n0 += nwaves * R) {
     float acc[R][MM];
@@ -3722,6 +3728,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
           f16 h = (f16)(v + (has_bias ? (float)p.bias[n] : 0.f));
           if (gtanh) h = (f16)gelu_tanh_f((float)h);
           if (has_res) h = (f16)((float)h + (float)p.res[(long)m * p.ldy + n]);
+          if (silu) h = to_f16(silu_f((float)h));   // = k_silu on the rounded output
           p.y[(long)m * p.ldy + n] = h;
         }
       }
@@ -3729,19 +3736,23 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
 }
 
 // chunks per lane the register-resident activation allows (0: not a GEMV shape)
+// (M 5..8: the CFG-batch-8 time-embedding projections of SD1.5 - 12.8 + 18.8 + 20.6 us per eval on
+// the 64-row register tiles, whose 16-20 blocks leave the GPU idle)
 static int gemv_cpl(const GemmArgs& p) {
-  if (p.M < 1 || p.M > 4 || (p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU)) || p.K % 32) return 0;
+  if (p.M < 1 || p.M > 8 || (p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU)) || p.K % 32) return 0;
   const int cpl = (p.K / 32 + 63) / 64;
-  const int mm = p.M <= 2 ? 2 : 4;
-  const int cap = mm == 2 ? 4 : 2;   // MM * CPL * 16 activation VGPRs <= 128
+  const int mm = p.M <= 2 ? 2 : p.M <= 4 ? 4 : 8;
+  const int cap = mm == 2 ? 4 : mm == 4 ? 2 : 1;   // MM * CPL * 16 activation VGPRs <= 128
   return cpl <= cap ? (cpl <= 1 ? 1 : cpl <= 2 ? 2 : 4) : 0;
 }
 
 template <int BFMT, int MM>
 static void launch_gemv_cpl(const GemmArgs& p, int cpl, int nwg, hipStream_t st) {
   if (cpl == 1) k_gemv<BFMT, MM, 1><<<nwg, 256, 0, st>>>(p);
-  else if (cpl == 2) k_gemv<BFMT, MM, 2><<<nwg, 256, 0, st>>>(p);
-  else if constexpr (MM == 2) k_gemv<BFMT, MM, 4><<<nwg, 256, 0, st>>>(p);
+  else if constexpr (MM <= 4) {
+    if (cpl == 2) k_gemv<BFMT, MM, 2><<<nwg, 256, 0, st>>>(p);
+    else if constexpr (MM == 2) k_gemv<BFMT, MM, 4><<<nwg, 256, 0, st>>>(p);
+  }
 }
 
 template <int BFMT>
@@ -3750,7 +3761,8 @@ static void launch_gemv_fmt(const GemmArgs& p, int cpl, hipStream_t st) {
   const long groups = (p.N + 3) / 4;
   const int nwg = (int)std::min<long>((groups + 3) / 4, 256L * 16);
   if (p.M <= 2) launch_gemv_cpl<BFMT, 2>(p, cpl, nwg, st);
-  else launch_gemv_cpl<BFMT, 4>(p, cpl, nwg, st);
+  else if (p.M <= 4) launch_gemv_cpl<BFMT, 4>(p, cpl, nwg, st);
+  else launch_gemv_cpl<BFMT, 8>(p, cpl, nwg, st);
 }
 
 static void launch_gemv(const GemmArgs& p, int fmt, int cpl, hipStream_t st) {
@@ -3957,6 +3969,7 @@ static int linear_fwd(const void* x, int M, int K, int lda, const void* w, int w
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
   const int cpl = ln ? 0 : gemv_cpl(p);
+  QD_REQUIRE(!(epi & QD_EPI_SILU) || cpl, "SiLU epilogue: GEMV shapes only (M <= 8, no amax / GEGLU)");
   if (cpl) launch_gemv(p, wfmt, cpl, S(stream));
   else run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();
@@ -3987,6 +4000,156 @@ struct FqArgs {
   int cadd_ld;
   float* xamax;
 };
+
+// ---- narrow-output 3x3 conv (Co <= 16: the UNet / VAE conv_out) ----------------------------------
+// A 64-wide tile GEMM idles 15/16 of its MFMA columns and re-reads the input 9x at N = 8 (SD1.5's
+// conv_out, 320 -> 4 (+4 pad) at 64x64, CFG batch 8: 40 us in k_gemm<64, 64> for 0.75 GFLOP and a 21 MB
+// input).  Here a block owns 2 output rows x 64 pixels x every output channel: per 64-channel input
+// chunk the 4 x 66-pixel halo and the chunk's [9 taps][16 co][64] weights are staged into LDS once
+// (register-staged, double-buffered, one barrier per chunk) and each wave runs 2 pixel groups of 16
+// as C^T = W . X^T on v_mfma_f32_16x16x32_f16 (A = weight fragment, shared by both groups).  Blocks are
+// XCD-remapped so one XCD walks consecutive row pairs (the 2 halo rows two neighbouring tiles share
+// stay in that XCD's L2).  Epilogue: + bias, fp16 rounding, the per-(n, co) amax of the rounded output
+// (shuffles -> LDS -> one atomic per channel per block) - the F.conv2d of fake_quant.py:339 with the
+// input of its output fake-quant.  K order: (64-channel chunk, tap, channel) - an fp32 summation order
+// of its own, like the split-K / halo plans.  Requires 3x3, stride 1, pad 1, no upsample, Ci_pad % 64
+// == 0, Co <= 16, Co % 4 == 0, W % 64 == 0, epilogue BIAS / AMAX only.
+constexpr int NC_W = 64;                        // output pixels per tile row
+constexpr int NC_HP = NC_W + 2;                 // halo pixels per row
+constexpr int NC_ACT = 4 * NC_HP * 64;          // halo elements per chunk (4 rows x 66 px x 64 ch)
+constexpr int NC_WT = 9 * 16 * 64;              // weight elements per chunk
+constexpr int NC_AP = (4 * NC_HP * 8 + 255) / 256;  // 16-B activation pieces per thread
+constexpr int NC_WP = (9 * 16 * 8) / 256 + 1;       // 16-B weight pieces per thread (1152 / 256 -> 5)
+
+__global__ void __launch_bounds__(256) k_conv_narrow(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) f16 sm[2 * (NC_ACT + NC_WT)];
+  __shared__ float red[4][16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int segs = p.W / NC_W, rpairs = (p.H + 1) / 2;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int seg = wg % segs, rp = (wg / segs) % rpairs, n = wg / (segs * rpairs);
+  const int r0 = 2 * rp, x0 = seg * NC_W;
+  const int Cip = p.Cip, nch = Cip / 64;
+
+  const __amdgpu_buffer_rsrc_t ars = rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t wrs = rsrc(p.b, p.b_bytes);
+  // staging maps: activation piece q -> (halo row, halo px, 16-B chunk); weight piece -> (tap, co, chunk)
+  unsigned aoff[NC_AP];
+  int adst[NC_AP];
+#pragma unroll
+  for (int i = 0; i < NC_AP; ++i) {
+    const int q = tid + 256 * i;
+    const int row = q / (NC_HP * 8), rem = q % (NC_HP * 8), px = rem >> 3, c = rem & 7;
+    const int ih = r0 - 1 + row, iw = x0 - 1 + px;
+    const bool ok = q < 4 * NC_HP * 8 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+    aoff[i] = ok ? (unsigned)((((long)n * p.H + ih) * p.W + iw) * Cip + c * 8) * 2u : OOB;
+    const int hp = row * NC_HP + px;  // linear halo pixel: the swizzle key of the fragment reads
+    adst[i] = q < 4 * NC_HP * 8 ? hp * 64 + ((c ^ (hp & 7)) << 3) : -1;
+  }
+  unsigned woff[NC_WP];
+  int wdst[NC_WP];
+#pragma unroll
+  for (int i = 0; i < NC_WP; ++i) {
+    const int q = tid + 256 * i;
+    const int tap = q / 128, co = (q >> 3) & 15, c = q & 7;
+    const bool ok = q < 9 * 16 * 8 && co < p.N;
+    woff[i] = ok ? (unsigned)(((long)co * 9 + tap) * Cip + c * 8) * 2u : OOB;
+    wdst[i] = q < 9 * 16 * 8 ? NC_ACT + (tap * 16 + co) * 64 + ((c ^ (co & 7)) << 3) : -1;
+  }
+  f16x8 ast[NC_AP], wst[NC_WP];
+  auto load = [&](int ch) {
+    const unsigned ca = (unsigned)ch * 128u;  // 64 channels x 2 B
+#pragma unroll
+    for (int i = 0; i < NC_AP; ++i) ast[i] = bload(ars, aoff[i] == OOB ? OOB : aoff[i] + ca);
+#pragma unroll
+    for (int i = 0; i < NC_WP; ++i) wst[i] = bload(wrs, woff[i] == OOB ? OOB : woff[i] + ca);
+  };
+  auto store = [&](f16* buf) {
+#pragma unroll
+    for (int i = 0; i < NC_AP; ++i)
+      if (adst[i] >= 0) *reinterpret_cast<f16x8*>(buf + adst[i]) = ast[i];
+#pragma unroll
+    for (int i = 0; i < NC_WP; ++i)
+      if (wdst[i] >= 0) *reinterpret_cast<f16x8*>(buf + wdst[i]) = wst[i];
+  };
+
+  // wave w: pixel groups 2w, 2w + 1 = (tile row g >> 2, pixels 16 (g & 3) + 0..15)
+  const int fr = lane & 15, fq = lane >> 4;
+  int bsrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int g = 2 * wid + j;
+    bsrc[j] = (g >> 2) * NC_HP + 16 * (g & 3) + fr;  // halo pixel of tap (0, 0)
+  }
+  f32x4 acc[2] = {};
+  load(0);
+  store(sm);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    f16* cur = sm + (ch & 1) * (NC_ACT + NC_WT);
+    if (ch + 1 < nch) load(ch + 1);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c16 = 4 * ks + fq;
+        const f16x8 wf = *reinterpret_cast<const f16x8*>(cur + NC_ACT + (tap * 16 + fr) * 64 + ((c16 ^ (fr & 7)) << 3));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int hp = bsrc[j] + dy * NC_HP + dx;
+          const f16x8 xf = *reinterpret_cast<const f16x8*>(cur + hp * 64 + ((c16 ^ (hp & 7)) << 3));
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf, xf, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    if (ch + 1 < nch) store(sm + ((ch + 1) & 1) * (NC_ACT + NC_WT));
+    __syncthreads();
+  }
+  // epilogue: lane holds channels 4 fq + r of pixel fr of each group
+  const bool amax = (p.epi & QD_EPI_AMAX) != 0;
+  const int co0 = 4 * fq;
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((p.epi & QD_EPI_BIAS) && p.bias && co0 < p.N) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = (float)p.bias[co0 + r];
+  }
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int g = 2 * wid + j;
+    const int oh = r0 + (g >> 2), ow = x0 + 16 * (g & 3) + fr;
+    if (oh < p.H) {  // (odd H: the second row of the last pair lies outside)
+      f16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o[r] = (f16)(acc[j][r] + bv[r]);
+        m[r] = fmaxf(m[r], fabsf((float)o[r]));   // channels >= N: zero weights and bias, o = 0
+      }
+      if (co0 < p.N) *reinterpret_cast<f16x4*>(p.y + (((long)n * p.H + oh) * p.W + ow) * p.ldy + co0) = o;
+    }
+  }
+  if (amax) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) m[r] = fmaxf(m[r], __shfl_xor(m[r], o, 64));
+      if (fr == 0) red[wid][co0 + r] = m[r];
+    }
+    __syncthreads();
+    if (tid < p.N) {
+      const float v = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+      atomic_max_pos(p.amax + (long)n * p.N + tid, v);
+    }
+  }
+}
+
+static bool narrow_conv_ok(const GemmArgs& p) {
+  return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && !p.ups && p.Cip % 64 == 0 && p.N <= 16 &&
+         p.N % 4 == 0 && p.ldy == p.N && p.W % NC_W == 0 && !(p.epi & ~(QD_EPI_BIAS | QD_EPI_AMAX | QD_EPI_AMAX_ZEROED));
+}
 
 static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, const void* wt, int co, int kh, int kw,
                     int stride, int pad, int upsample2x, const void* bias, const void* residual, void* y, int epi,
@@ -4039,7 +4202,10 @@ static int conv_fwd(const void* x, int n, int h, int w, int ci, int ci_pad, cons
     p.fq_cadd_ld = fq->cadd_ld > 0 ? fq->cadd_ld : co;
     p.fq_xamax = fq->xamax;
   }
-  if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && !upsample2x) {
+  if (narrow_conv_ok(p)) {
+    // Co <= 16 (conv_out): one block per 2 x 64 output pixels; any fused finalize runs as its own pass
+    k_conv_narrow<<<n * ((Ho + 1) / 2) * (Wo / NC_W), 256, 0, S(stream)>>>(p);
+  } else if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && !upsample2x) {
     // a pointwise conv IS a GEMM over the NHWC pixel rows (x [N*H*W][Ci_pad]): no tap decode
     p.lda = ci_pad;
     run_gemm<AM_LINEAR>(p, QD_WFMT_F16, ws, ws_elems, S(stream));

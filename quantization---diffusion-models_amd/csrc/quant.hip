@@ -651,6 +651,77 @@ extern "C" int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int 
   return 0;
 }
 
+// quantize_activation_per_channel_absmax (fake_quant.py:123-131) of a SMALL NHWC tensor in one launch:
+// one block per sample holds the sample in registers (<= 16 rows of 8 channels per thread), reduces the
+// per-channel max in LDS (fixed tree, exact) and applies the fake-quant from the same registers.  The
+// UNet's conv_in input (the [2B, 64, 64, 8] latent) took a column-max pass (13.6 us: 16-deep atomic
+// chains per channel at 4096 rows x 1 chunk) + an apply pass (5.4 us).  Same bits as the two passes
+// (max is exact; fq_scale / fq_apply_r as k_apply_nhwc).  chunks = c / 8 a power of two <= 256.
+constexpr int FQS_RPT = 16;
+__global__ void __launch_bounds__(256) k_fq_small_nhwc(const f16* __restrict__ x, f16* __restrict__ y, int hw, int c,
+                                                       int c_valid, int qmax) {
+  __shared__ __attribute__((aligned(16))) float red[256][8];
+  const int chunks = c >> 3, t = threadIdx.x;
+  const int chunk = t & (chunks - 1), rl = t / chunks, rstride = 256 / chunks;
+  const long n = blockIdx.x;
+  const f16* src = x + n * hw * c + chunk * 8;
+  f16x8 v[FQS_RPT];
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < FQS_RPT; ++u) {
+    const int row = rl + u * rstride;
+    v[u] = row < hw ? *reinterpret_cast<const f16x8*>(src + (long)row * c) : f16x8{};
+  }
+#pragma unroll
+  for (int u = 0; u < FQS_RPT; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)v[u][j]));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = m[j];
+  __syncthreads();
+  for (int s = rstride >> 1; s >= 1; s >>= 1) {  // rows rl, rl + s of the same chunk
+    if (rl < s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[t][j] = fmaxf(red[t][j], red[t + s * chunks][j]);
+    __syncthreads();
+  }
+  float sc[8];
+  double rs[8];
+  fq_scales8(&red[chunk][0], qmax, sc, rs);
+  f16* dst = y + n * hw * c + chunk * 8;
+#pragma unroll
+  for (int u = 0; u < FQS_RPT; ++u) {
+    const int row = rl + u * rstride;
+    if (row >= hw) break;
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = chunk * 8 + j < c_valid ? fq_apply_r((float)v[u][j], sc[j], rs[j]) : v[u][j];
+    *reinterpret_cast<f16x8*>(dst + (long)row * c) = o;
+  }
+}
+
+extern "C" int qd_act_fq_small_ok(int hw, int c) {
+  const int chunks = c / 8;
+  return (c % 8 == 0 && chunks >= 1 && chunks <= 256 && (chunks & (chunks - 1)) == 0 &&
+          (long)hw * chunks <= 256L * FQS_RPT && hw > 0) ? 1 : 0;
+}
+
+extern "C" int qd_act_fq_small_nhwc(const void* x, void* y, int n, int hw, int c, int c_valid, int n_bits,
+                                    void* stream) {
+  QD_REQUIRE(x && y, "null pointer");
+  QD_REQUIRE(qd_act_fq_small_ok(hw, c), "qd_act_fq_small_nhwc: c / 8 a power of two, hw * c / 8 <= 4096 (qd_act_fq_small_ok)");
+  QD_REQUIRE(n_bits >= 2 && n_bits <= 16, "bad n_bits");
+  QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
+             "x / y must be 16-B aligned");
+  if (n == 0) return 0;
+  k_fq_small_nhwc<<<n, 256, 0, S(stream)>>>((const f16*)x, (f16*)y, hw, c, c_valid > 0 ? c_valid : c,
+                                            qmax_of(n_bits));
+  QD_CHECK_LAUNCH();
+  return 0;
+}
+
 // qd_act_quant_cat_nhwc's apply pass with the per-(n, c) maxima of [x | x2] given (amax [n][c1 + c2],
 // e.g. from qd_groupnorm_xamax over the same concat): no column-max pass
 extern "C" int qd_act_apply_cat_nhwc(const void* x, int c1, const void* x2, int c2, int n, int hw, int n_bits,

@@ -25,6 +25,7 @@ EPI_GELU_TANH = 32
 EPI_AMAX_POST = 64
 EPI_CADD = 128
 EPI_GNSTATS = 256
+EPI_SILU = 1024
 GRAN_ZEROED = 0x100
 
 
@@ -120,6 +121,28 @@ def act_apply_nhwc(x, amax, n_bits, out=None, c_valid=0):
     y = out if out is not None else _empty(x.shape, x.dtype, x.device)
     _lib.call("qd_act_apply", _p(x), _p(y), NHWC, n, c, h, w, GRAN["per_channel"], c_valid, n_bits, _p(amax),
               _stream())
+    return y
+
+
+_FQ_SMALL = {}
+
+
+def act_fq_small_ok(x):
+    """True when act_fq_nhwc_small takes x [N, H, W, C] (one workgroup per sample)."""
+    n, h, w, c = x.shape
+    key = (h * w, c)
+    if key not in _FQ_SMALL:
+        _FQ_SMALL[key] = bool(_lib.load().qd_act_fq_small_ok(h * w, c))
+    return _FQ_SMALL[key]
+
+
+def act_fq_nhwc_small(x, n_bits, out=None, c_valid=0):
+    """act_absmax(x, "per_channel") + act_apply_nhwc(...) of a small NHWC tensor in ONE launch
+    (the UNet's conv_in latent): the same bits; act_fq_small_ok(x) must hold."""
+    _chk(x, "x")
+    n, h, w, c = x.shape
+    y = out if out is not None else _empty(x.shape, x.dtype, x.device)
+    _lib.call("qd_act_fq_small_nhwc", _p(x), _p(y), n, h * w, c, c_valid, n_bits, _stream())
     return y
 
 
@@ -385,9 +408,18 @@ def scales_t(sc):
     return t
 
 
+def gemv_shape(M, K, epi):
+    """True when qd_linear_fwd runs this shape on the weight-stream GEMV (gemm.hip gemv_cpl):
+    M <= 8 rows without an amax / GEGLU epilogue, K % 32 == 0 and the activation in registers."""
+    if M < 1 or M > 8 or epi & (EPI_AMAX | EPI_GEGLU) or K % 32:
+        return False
+    cap = 4 if M <= 2 else 2 if M <= 4 else 1
+    return (K // 32 + 63) // 64 <= cap
+
+
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
            amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None, gelu_tanh=False,
-           amax_post=False):
+           amax_post=False, silu=False):
     """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K).
     geglu: W rows (and bias) interleaved in 16-row [hidden | gate] blocks (geglu_interleave);
     returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue).
@@ -395,7 +427,9 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     amax_post (with amax and residual): the per-(sample, column) amax is of the final output
     half(y + residual) - the input amax of the quantized conv that consumes it.
     weight_f16: the same weight's fp16 dequantized buffer (bit-identical to dequantizing the
-    codes); when given, the kernel search also considers the fp16 LDS-DMA family."""
+    codes); when given, the kernel search also considers the fp16 LDS-DMA family.
+    silu (GEMV shapes only, gemv_shape(M, K, ...)): returns half(silu(out)) - the diffusers
+    TimestepEmbedding activation / the UNet's silu(temb) - bit-identical to silu() on the output."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
         raise ValueError("x must be an fp16 HIP tensor")
     if x2d.dim() != 2 or x2d.stride(1) != 1:
@@ -407,7 +441,10 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
           (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0) | \
-          (EPI_AMAX_POST if amax_post and amax is not None and residual is not None else 0)
+          (EPI_AMAX_POST if amax_post and amax is not None and residual is not None else 0) | \
+          (EPI_SILU if silu else 0)
+    if silu and not gemv_shape(M, K, epi):
+        raise ValueError("linear(silu=True) needs a GEMV shape (M <= 8, no amax / GEGLU epilogue)")
     if residual is not None:
         _chk(residual, "residual")
     ops = [(weight, wfmt, scales, group)]
@@ -435,8 +472,10 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty_like(out)
         ta = torch.empty_like(amax) if amax is not None else None
-        c = _choose(key, _cands(ops) + _split_cands(M, N, K, ops),
-                    lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
+        # a GEMV shape ignores the tile variant: only the operand (codes / fp16 buffer) is a choice
+        cands = [(i, -1) for i in range(len(ops))] if gemv_shape(M, K, epi) else \
+            _cands(ops) + _split_cands(M, N, K, ops)
+        c = _choose(key, cands, lambda c: launch(c, ty, ta, epi & ~EPI_AMAX_ZEROED, True))
     else:
         c = _TUNE.get(key)
     launch(c if c is not None else (0, -1), out, amax, epi, False)
@@ -585,7 +624,8 @@ def conv2d_nhwc(x, w_khwc, ci, stride=1, pad=0, upsample2x=False, bias=None, res
             _force(-1)
 
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi & ~EPI_AMAX_ZEROED)
-    _USED.add(key)
+    if out is not _TUNE_ONLY:  # (a tune-only call launches nothing: not a key this process ran)
+        _USED.add(key)
     if key not in _TUNE and _TUNE_ON and not torch.cuda.is_current_stream_capturing():
         ty = torch.empty((n, ho, wo, co), dtype=torch.float16, device=x.device)
         ta = torch.empty(n * co, dtype=torch.float32, device=x.device) if epi & EPI_AMAX else None
@@ -617,9 +657,11 @@ def _tune_conv_fq_key(x, w_khwc, ci, stride, pad, upsample2x, bias, key):
                 amax=torch.empty(1, dtype=torch.float32, device=x.device))
 
 
-def conv2d_fq_fuses(x, w_khwc, stride=1, pad=0, upsample2x=False, bias=None):
+def conv2d_fq_fuses(x, w_khwc, stride=1, pad=0, upsample2x=False, bias=None, ci=None):
     """True when conv2d_fq on these operands finalizes in the split-K reduction (its tuned plan
-    splits K and a sample's output rows fit one reduction block); nothing is launched."""
+    splits K and a sample's output rows fit one reduction block).  An untuned key is tuned here
+    first (timed launches on scratch buffers, as conv2d_fq would), with the layer's real input
+    width ci (default: x's padded width) so both callers time the key on the same shape."""
     n, h, w, cip = x.shape
     co, kh, kw, _ = w_khwc.shape
     H, W = (2 * h, 2 * w) if upsample2x else (h, w)
@@ -629,7 +671,7 @@ def conv2d_fq_fuses(x, w_khwc, stride=1, pad=0, upsample2x=False, bias=None):
     key = ("conv", n, h, w, cip, co, kh, kw, stride, pad, bool(upsample2x), epi)
     if rps % 32 or rps // 32 not in (1, 2, 4, 8) or co % 32 or cip % 64:
         return False
-    _tune_conv_fq_key(x, w_khwc, cip, stride, pad, upsample2x, bias, key)
+    _tune_conv_fq_key(x, w_khwc, cip if ci is None else ci, stride, pad, upsample2x, bias, key)
     if key not in _TUNE and _OVERRIDE is None:
         return False
     c = _TUNE.get(key)
@@ -908,6 +950,9 @@ def linear_i8_geglu_q(xq, sa, wq, sw, bias=None):
     N = wq.shape[0]
     if not linear_i8_geglu_q_ok(Kd, N):
         raise ValueError(f"linear_i8_geglu_q: no fused kernel for K {Kd}, N {N}")
+    # the kernel reads sa as one fp32 per row (as linear_i8)
+    if sa.dtype != torch.float32 or not sa.is_contiguous() or sa.numel() < M or not sa.is_cuda:
+        raise ValueError("sa must be a contiguous fp32 HIP tensor with at least M elements")
     _chk(sw, "sw", torch.float32)
     if bias is not None:
         _chk(bias, "bias")

@@ -340,16 +340,17 @@ class UNet2DConditionModel(nn.Module):
         """x: [2B, H, W, Cp] fp16 NHWC (Cp = in_channels padded to 8); temb_in: [2B, C0] fp16
         sinusoidal timestep features; returns the noise prediction [2B, H, W, 8] (4 real ch)."""
         cfg = self.config
-        t = run_linear(self.time_embedding.linear_1, temb_in)
-        t = K.silu(t, out=t)
-        temb = run_linear(self.time_embedding.linear_2, t)
+        # TimestepEmbedding linear_1 -> SiLU -> linear_2, then the resnets' silu(temb): the SiLUs
+        # ride in the GEMV epilogues at the CFG batch (M <= 8), else separate passes
+        t = run_linear(self.time_embedding.linear_1, temb_in, silu=True)
         if self.add_embedding is not None:
             if add_emb_in is None:
                 raise ValueError("SDXL UNet needs the text_time additional embedding input")
-            a = run_linear(self.add_embedding.linear_1, add_emb_in)
-            a = K.silu(a, out=a)
-            temb = run_linear(self.add_embedding.linear_2, a, residual=temb)
-        temb_silu = K.silu(temb)
+            temb = run_linear(self.time_embedding.linear_2, t)
+            a = run_linear(self.add_embedding.linear_1, add_emb_in, silu=True)
+            temb_silu = run_linear(self.add_embedding.linear_2, a, residual=temb, silu=True)
+        else:
+            temb_silu = run_linear(self.time_embedding.linear_2, t, silu=True)
         tps = self.temb_projections(temb_silu)
 
         h = run_conv(self.conv_in, x, c_valid=cfg.in_channels)
@@ -511,8 +512,11 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
         y = _conv_via_module(layer, x, residual, chan_add, upsample, co_pad)
         return (y, None) if defer else y
     if q and not prequant:
-        amax = in_amax if in_amax is not None else K.act_absmax(x, "per_channel", K.NHWC)
-        x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
+        if in_amax is None and K.act_fq_small_ok(x):  # (conv_in's latent: column max + apply in one launch)
+            x = K.act_fq_nhwc_small(x, q, c_valid=c_valid)
+        else:
+            amax = in_amax if in_amax is not None else K.act_absmax(x, "per_channel", K.NHWC)
+            x = K.act_apply_nhwc(x, amax, q, c_valid=c_valid)
     if q:
         n = x.shape[0]
         hh, ww = (2 * x.shape[1], 2 * x.shape[2]) if upsample else (x.shape[1], x.shape[2])
@@ -541,7 +545,7 @@ def run_conv(layer, x, prequant=False, residual=None, chan_add=None, upsample=Fa
                 # channel - a reduction that finalizes it hands over that amax too (an unsplit plan
                 # would need a column-max pass of its own: left to the consumer, as before)
                 xam = A.empty((n * wk.shape[0],), torch.float32, x.device) \
-                    if pn_out and ho * wo <= 256 and K.conv2d_fq_fuses(x, wk, stride, pad, upsample, bias) else None
+                    if pn_out and ho * wo <= 256 and K.conv2d_fq_fuses(x, wk, stride, pad, upsample, bias, ci=ci) else None
                 xo = K.conv2d_fq(x, wk, ci, q, amax, stride, pad, upsample, bias=bias, amax_zeroed=zeroed,
                                  residual=residual, chan_add=chan_add, xamax=xam)
                 if pn_out:
@@ -616,10 +620,18 @@ def _conv_via_module(layer, x, residual, chan_add, upsample, co_pad):
 I8_MIN_ROWS = 64
 
 
-def run_linear(layer, x2d, residual=None, out=None):
+def run_linear(layer, x2d, residual=None, out=None, silu=False):
     """x2d [M, K] -> [M, N] for an nn.Linear or WxAxLinear (fake_quant.py:214-225 semantics).
     out: optional contiguous [M, N] destination.  x2d may be (int8 codes, per-row scales) from a
-    fused producer (int8-MFMA mode layers only)."""
+    fused producer (int8-MFMA mode layers only).  silu: return silu(layer(x2d)) - in the GEMV
+    epilogue where the shape runs on the GEMV (the time-embedding projections), else a SiLU pass."""
+    if silu:
+        if not isinstance(x2d, tuple) and getattr(layer, "_qd_hook", None) is None and \
+                not (isinstance(layer, WxAxLinear) and layer.output_quant_name != "None") and \
+                K.gemv_shape(x2d.shape[0], x2d.shape[1], 0):
+            return _run_linear_silu(layer, x2d, residual, out)
+        y = run_linear(layer, x2d, residual=residual, out=out)
+        return K.silu(y, out=y)
     if isinstance(x2d, tuple):
         xq, sa = x2d
         i8 = layer.i8_operand()
@@ -653,6 +665,17 @@ def run_linear(layer, x2d, residual=None, out=None):
             return K.add(y, residual, out=y) if residual is not None else y
         return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual, weight_f16=wf, out=out)
     return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual, out=out)
+
+
+def _run_linear_silu(layer, x2d, residual, out):
+    """run_linear(..., silu=True) on a GEMV shape: the SiLU in the GEMV epilogue (M <= 8 rows never
+    take the int8 / fp8 operand paths, I8_MIN_ROWS)."""
+    if isinstance(layer, WxAxLinear):
+        xin = layer.act_quant(x2d) if layer.quantize_act else x2d
+        w, fmt, sc, g = layer.gemm_weight()
+        wf = layer.weight if fmt != "f16" else None
+        return K.linear(xin, w, fmt, sc, g, bias=layer.bias, residual=residual, weight_f16=wf, out=out, silu=True)
+    return K.linear(x2d, _f16(layer.weight), "f16", bias=_f16(layer.bias), residual=residual, out=out, silu=True)
 
 
 def _geglu_operand(layer):

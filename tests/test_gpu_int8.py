@@ -77,6 +77,31 @@ def test_linear_i8_bit_exact(M, N, Kd, variant, dev):
     assert np.array_equal(_bits(y), _bits(ref)), np.abs(y.astype(np.float32) - ref.astype(np.float32)).max()
 
 
+@pytest.mark.parametrize("variant", [170, 175, 160, 165])
+@pytest.mark.parametrize("epi", ["plain", "residual"])
+def test_linear_i8_persistent_ragged_many_tiles(variant, epi, dev):
+    """the persistent tiles' first K step waits with a count that includes the previous
+    tile's direct stores (gemm.hip, issue order pinned by a sched_barrier).  M 4097 leaves every
+    persistent block 3+ tiles and a ragged last one; N 2560, K 320 as the SD1.5 64x64 projections."""
+    k = K()
+    rng = np.random.default_rng(4097 + variant)
+    M, N, Kd = 4097, 2560, 320
+    x = rng.standard_normal((M, Kd)).astype(np.float16)
+    w = (rng.standard_normal((N, Kd)) / Kd ** 0.5).astype(np.float16)
+    b = rng.standard_normal(N).astype(np.float16)
+    res = rng.standard_normal((M, N)).astype(np.float16) if epi == "residual" else None
+    xq, sa = R.quant_rows_i8(x)
+    wq, sw = R.weight_rows_i8(w)
+    ref = R.linear_i8(xq, sa, wq, sw, b, res)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    k.force_gemm(variant)
+    try:
+        y = k.linear_i8(t(xq), t(sa), t(wq), t(sw), bias=t(b), residual=None if res is None else t(res)).cpu().numpy()
+    finally:
+        k.force_gemm(None)
+    assert np.array_equal(_bits(y), _bits(ref))
+
+
 @pytest.mark.parametrize("variant", [None, 110, 130, 131, 133, 160, 166, 167, 177])
 def test_linear_i8_geglu_and_amax(variant, dev):
     k = K()

@@ -320,6 +320,30 @@ def test_attention(b, heads, sq, skv, d, dev):
     assert (o - ref).abs().max().item() < 1e-2
 
 
+@pytest.mark.parametrize("b,heads,sq,skv,d", [(2, 2, 256, 40, 40), (2, 2, 300, 77, 40), (1, 2, 256, 192, 40),
+                                              (2, 3, 520, 333, 40), (1, 2, 512, 4096, 40), (2, 2, 256, 256, 80)])
+def test_attention_stagger_bit_identical(b, heads, sq, skv, d, dev):
+    """Round 6: the 8-wave 32x32x16 kernel with the half-tile stagger between SIMD partners
+    (qd_attn_force 8; the heuristic's choice) runs the same operations per query in the same order
+    as the unstaggered form (force 9): identical bits at 1 / 2 / odd / even key-tile counts."""
+    from qdiff import _lib
+    k = K()
+    g = torch.Generator().manual_seed(sq * 7 + skv + d)
+    c = heads * d
+    q = torch.randn(b, sq, c, generator=g).half().to(dev)
+    kk = (torch.randn(b, skv, c, generator=g) * 2).half().to(dev)
+    v = torch.randn(b, skv, c, generator=g).half().to(dev)
+    lib = _lib.load()
+    try:
+        lib.qd_attn_force(8)
+        o8 = k.attention(q, kk, v, heads)
+        lib.qd_attn_force(9)
+        o9 = k.attention(q, kk, v, heads)
+    finally:
+        lib.qd_attn_force(0)
+    assert torch.equal(o8.view(torch.int16), o9.view(torch.int16))
+
+
 @pytest.mark.parametrize("d,gain", [(40, 3.0), (80, 2.5), (64, 3.0), (160, 2.5)])
 def test_attention_sharp_softmax(d, gain, dev):
     """large-norm Q / K (logits of magnitude 30-60, a near one-hot softmax).  The kernel
