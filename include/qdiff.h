@@ -131,7 +131,7 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
                                 GroupNorm (qd_groupnorm_part) needs no statistics pass over the
                                 tensor; rows_per_sample % 64 == 0, never ping-pong tiles */
 #define QD_EPI_LN 512        /* (set by qd_linear_ln / qd_linear_i8_ln) */
-#define QD_EPI_SILU 1024     /* qd_linear_fwd GEMV shapes only (M <= 8): out = half(silu(out)) after the
+#define QD_EPI_SILU 1024     /* qd_linear_fwd GEMV shapes only (M <= 4): out = half(silu(out)) after the
                                 bias / residual rounding - the diffusers TimestepEmbedding act and
                                 the UNet's silu(temb), bit-identical to qd_silu on the output */
 
@@ -142,9 +142,9 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
  * ping-pong families (qd_gemm_force 110..117, 300..304), dequantized from LDS per fragment with the
  * register tile's rounding (bit-identical results).  lda/ldy in elements.
  * rows_per_sample: sample boundary for QD_EPI_AMAX (multiple of 32).
- * M <= 8 (K <= 2048 at M 5..8) without AMAX / GEGLU runs a weight-stream GEMV (same dequant and
- * epilogue rounding; v_dot2 fp32 accumulation instead of the MFMA's, so only the summation order
- * differs from the tile GEMM); QD_EPI_SILU requires such a shape. */
+ * M <= 4 without AMAX / GEGLU runs a weight-stream GEMV (same dequant and epilogue rounding; v_dot2
+ * fp32 accumulation instead of the MFMA's, so only the summation order differs from the tile GEMM);
+ * QD_EPI_SILU requires such a shape. */
 int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
                   const void* wscale, const void* wscale_t, int group, const void* bias,
                   const void* residual, void* y, int N, int ldy, int epi, float* amax,

@@ -3736,23 +3736,23 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
 }
 
 // chunks per lane the register-resident activation allows (0: not a GEMV shape)
-// (M 5..8: the CFG-batch-8 time-embedding projections of SD1.5 - 12.8 + 18.8 + 20.6 us per eval on
-// the 64-row register tiles, whose 16-20 blocks leave the GPU idle)
+// (M 5..8 - SD1.5's CFG-batch-8 time-embedding projections - was measured on an 8-row form of this
+// kernel and left on the tile GEMM: 16.5 / 16.2 / 49.2 us against 12.8 / 18.8 / 20.6 us for
+// 320 -> 1280, 1280 -> 1280 and the stacked 1280 -> 20160 projection, profiles/r06c_*: every wave
+// re-reads the whole 8 x K activation, 20 KB per 4 weight rows at N 20160)
 static int gemv_cpl(const GemmArgs& p) {
-  if (p.M < 1 || p.M > 8 || (p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU)) || p.K % 32) return 0;
+  if (p.M < 1 || p.M > 4 || (p.epi & (QD_EPI_AMAX | QD_EPI_GEGLU)) || p.K % 32) return 0;
   const int cpl = (p.K / 32 + 63) / 64;
-  const int mm = p.M <= 2 ? 2 : p.M <= 4 ? 4 : 8;
-  const int cap = mm == 2 ? 4 : mm == 4 ? 2 : 1;   // MM * CPL * 16 activation VGPRs <= 128
+  const int mm = p.M <= 2 ? 2 : 4;
+  const int cap = mm == 2 ? 4 : 2;   // MM * CPL * 16 activation VGPRs <= 128
   return cpl <= cap ? (cpl <= 1 ? 1 : cpl <= 2 ? 2 : 4) : 0;
 }
 
 template <int BFMT, int MM>
 static void launch_gemv_cpl(const GemmArgs& p, int cpl, int nwg, hipStream_t st) {
   if (cpl == 1) k_gemv<BFMT, MM, 1><<<nwg, 256, 0, st>>>(p);
-  else if constexpr (MM <= 4) {
-    if (cpl == 2) k_gemv<BFMT, MM, 2><<<nwg, 256, 0, st>>>(p);
-    else if constexpr (MM == 2) k_gemv<BFMT, MM, 4><<<nwg, 256, 0, st>>>(p);
-  }
+  else if (cpl == 2) k_gemv<BFMT, MM, 2><<<nwg, 256, 0, st>>>(p);
+  else if constexpr (MM == 2) k_gemv<BFMT, MM, 4><<<nwg, 256, 0, st>>>(p);
 }
 
 template <int BFMT>
@@ -3761,8 +3761,7 @@ static void launch_gemv_fmt(const GemmArgs& p, int cpl, hipStream_t st) {
   const long groups = (p.N + 3) / 4;
   const int nwg = (int)std::min<long>((groups + 3) / 4, 256L * 16);
   if (p.M <= 2) launch_gemv_cpl<BFMT, 2>(p, cpl, nwg, st);
-  else if (p.M <= 4) launch_gemv_cpl<BFMT, 4>(p, cpl, nwg, st);
-  else launch_gemv_cpl<BFMT, 8>(p, cpl, nwg, st);
+  else launch_gemv_cpl<BFMT, 4>(p, cpl, nwg, st);
 }
 
 static void launch_gemv(const GemmArgs& p, int fmt, int cpl, hipStream_t st) {
@@ -3969,7 +3968,7 @@ static int linear_fwd(const void* x, int M, int K, int lda, const void* w, int w
   if ((epi & QD_EPI_AMAX) && !(epi & QD_EPI_AMAX_ZEROED))  // stream-ordered, graph-capturable
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
   const int cpl = ln ? 0 : gemv_cpl(p);
-  QD_REQUIRE(!(epi & QD_EPI_SILU) || cpl, "SiLU epilogue: GEMV shapes only (M <= 8, no amax / GEGLU)");
+  QD_REQUIRE(!(epi & QD_EPI_SILU) || cpl, "SiLU epilogue: GEMV shapes only (M <= 4, no amax / GEGLU)");
   if (cpl) launch_gemv(p, wfmt, cpl, S(stream));
   else run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();

@@ -652,17 +652,17 @@ extern "C" int qd_act_quant_cat_nhwc(const void* x, int c1, const void* x2, int 
 }
 
 // quantize_activation_per_channel_absmax (fake_quant.py:123-131) of a SMALL NHWC tensor in one launch:
-// one block per sample holds the sample in registers (<= 16 rows of 8 channels per thread), reduces the
-// per-channel max in LDS (fixed tree, exact) and applies the fake-quant from the same registers.  The
-// UNet's conv_in input (the [2B, 64, 64, 8] latent) took a column-max pass (13.6 us: 16-deep atomic
-// chains per channel at 4096 rows x 1 chunk) + an apply pass (5.4 us).  Same bits as the two passes
-// (max is exact; fq_scale / fq_apply_r as k_apply_nhwc).  chunks = c / 8 a power of two <= 256.
-constexpr int FQS_RPT = 16;
-__global__ void __launch_bounds__(256) k_fq_small_nhwc(const f16* __restrict__ x, f16* __restrict__ y, int hw, int c,
-                                                       int c_valid, int qmax) {
-  __shared__ __attribute__((aligned(16))) float red[256][8];
+// one 1024-thread block per sample holds the sample in registers (<= 4 rows of 8 channels per thread),
+// reduces the per-channel max in LDS (fixed tree, exact) and applies the fake-quant from the same
+// registers.  The UNet's conv_in input (the [2B, 64, 64, 8] latent) took a column-max pass (13.6 us:
+// 16-deep atomic chains per channel at 4096 rows x 1 chunk) + an apply pass (5.4 us).  Same bits as the
+// two passes (max is exact; fq_scale / fq_apply_r as k_apply_nhwc).  chunks = c / 8 a power of two.
+constexpr int FQS_T = 1024, FQS_RPT = 4;
+__global__ void __launch_bounds__(FQS_T) k_fq_small_nhwc(const f16* __restrict__ x, f16* __restrict__ y, int hw, int c,
+                                                         int c_valid, int qmax) {
+  __shared__ __attribute__((aligned(16))) float red[FQS_T][8];
   const int chunks = c >> 3, t = threadIdx.x;
-  const int chunk = t & (chunks - 1), rl = t / chunks, rstride = 256 / chunks;
+  const int chunk = t & (chunks - 1), rl = t / chunks, rstride = FQS_T / chunks;
   const long n = blockIdx.x;
   const f16* src = x + n * hw * c + chunk * 8;
   f16x8 v[FQS_RPT];
@@ -704,8 +704,8 @@ __global__ void __launch_bounds__(256) k_fq_small_nhwc(const f16* __restrict__ x
 
 extern "C" int qd_act_fq_small_ok(int hw, int c) {
   const int chunks = c / 8;
-  return (c % 8 == 0 && chunks >= 1 && chunks <= 256 && (chunks & (chunks - 1)) == 0 &&
-          (long)hw * chunks <= 256L * FQS_RPT && hw > 0) ? 1 : 0;
+  return (c % 8 == 0 && chunks >= 1 && chunks <= FQS_T && (chunks & (chunks - 1)) == 0 &&
+          (long)hw * chunks <= (long)FQS_T * FQS_RPT && hw > 0) ? 1 : 0;
 }
 
 extern "C" int qd_act_fq_small_nhwc(const void* x, void* y, int n, int hw, int c, int c_valid, int n_bits,
@@ -716,7 +716,7 @@ extern "C" int qd_act_fq_small_nhwc(const void* x, void* y, int n, int hw, int c
   QD_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
              "x / y must be 16-B aligned");
   if (n == 0) return 0;
-  k_fq_small_nhwc<<<n, 256, 0, S(stream)>>>((const f16*)x, (f16*)y, hw, c, c_valid > 0 ? c_valid : c,
+  k_fq_small_nhwc<<<n, FQS_T, 0, S(stream)>>>((const f16*)x, (f16*)y, hw, c, c_valid > 0 ? c_valid : c,
                                             qmax_of(n_bits));
   QD_CHECK_LAUNCH();
   return 0;

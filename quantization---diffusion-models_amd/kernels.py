@@ -410,10 +410,10 @@ def scales_t(sc):
 
 def gemv_shape(M, K, epi):
     """True when qd_linear_fwd runs this shape on the weight-stream GEMV (gemm.hip gemv_cpl):
-    M <= 8 rows without an amax / GEGLU epilogue, K % 32 == 0 and the activation in registers."""
-    if M < 1 or M > 8 or epi & (EPI_AMAX | EPI_GEGLU) or K % 32:
+    M <= 4 rows without an amax / GEGLU epilogue, K % 32 == 0 and the activation in registers."""
+    if M < 1 or M > 4 or epi & (EPI_AMAX | EPI_GEGLU) or K % 32:
         return False
-    cap = 4 if M <= 2 else 2 if M <= 4 else 1
+    cap = 4 if M <= 2 else 2
     return (K // 32 + 63) // 64 <= cap
 
 
@@ -444,7 +444,7 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
           (EPI_AMAX_POST if amax_post and amax is not None and residual is not None else 0) | \
           (EPI_SILU if silu else 0)
     if silu and not gemv_shape(M, K, epi):
-        raise ValueError("linear(silu=True) needs a GEMV shape (M <= 8, no amax / GEGLU epilogue)")
+        raise ValueError("linear(silu=True) needs a GEMV shape (M <= 4, no amax / GEGLU epilogue)")
     if residual is not None:
         _chk(residual, "residual")
     ops = [(weight, wfmt, scales, group)]

@@ -341,7 +341,8 @@ class UNet2DConditionModel(nn.Module):
         sinusoidal timestep features; returns the noise prediction [2B, H, W, 8] (4 real ch)."""
         cfg = self.config
         # TimestepEmbedding linear_1 -> SiLU -> linear_2, then the resnets' silu(temb): the SiLUs
-        # ride in the GEMV epilogues at the CFG batch (M <= 8), else separate passes
+        # ride in the GEMV epilogues where the CFG batch runs on the GEMV (M <= 4: SDXL / SD3 at
+        # one prompt per GPU), else separate passes (SD1.5's M = 8 stays on the tile GEMM)
         t = run_linear(self.time_embedding.linear_1, temb_in, silu=True)
         if self.add_embedding is not None:
             if add_emb_in is None:
@@ -668,7 +669,7 @@ def run_linear(layer, x2d, residual=None, out=None, silu=False):
 
 
 def _run_linear_silu(layer, x2d, residual, out):
-    """run_linear(..., silu=True) on a GEMV shape: the SiLU in the GEMV epilogue (M <= 8 rows never
+    """run_linear(..., silu=True) on a GEMV shape: the SiLU in the GEMV epilogue (M <= 4 rows never
     take the int8 / fp8 operand paths, I8_MIN_ROWS)."""
     if isinstance(layer, WxAxLinear):
         xin = layer.act_quant(x2d) if layer.quantize_act else x2d

@@ -10,8 +10,10 @@ import os
 import sys
 
 d, out, variants = sys.argv[1], sys.argv[2], sys.argv[3].split()
+# the step's forms (scripts/roof_kernel.py): int8 adds the GroupNorm slot moments (16 B per 64-row slot
+# and column) to codes + weights + fp16 output
 ALG = {"f16": 8 * 64 * 64 * 320 * 2 + 320 * 9 * 320 * 2 + 8 * 64 * 64 * 320 * 2,
-       "i8": 8 * 64 * 64 * 320 * 1 + 320 * 9 * 320 * 1 + 8 * 64 * 64 * 320 * 2}
+       "i8": 8 * 64 * 64 * 320 * 1 + 320 * 9 * 320 * 1 + 8 * 64 * 64 * 320 * 2 + 8 * 64 * 64 // 64 * 320 * 16}
 
 
 def per_launch(path, counter):
@@ -40,6 +42,8 @@ res = {"shape": "conv3x3 320->320 @64x64 b8 (M=32768,N=320,K=2880)",
        "algorithmic_bytes_per_launch_i8": ALG["i8"],
        "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 scripts/roof_kernel.py "
                   "10 <variant> [--i8]",
+       "forms": {"f16": "bias + output-fake-quant amax epilogue, pre-zeroed amax (the step's form)",
+                 "i8": "bias + time-embedding add + GroupNorm slot statistics (the step's resnet conv1)"},
        "by_variant": {}}
 for mv in variants:
     mode, v = mv.split(":")
