@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
 
   const int ntiles = (skv + KV_T - 1) / KV_T;
   // S'^T = K (c Q)^T - m of the 64-key tile at ks (kv0 = its first key), keys past skv -> -inf
-  auto qk = [&](const f16* ks, int kv0, f32x16 (&sacc)[2]) {
+  auto qk = [&](const f16* ks, int kv0, f32x16 (&sacc)[2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
   // the tile's V at vs (a software-pipelined form - QK^T of tile t + 1 issued before the softmax of
   // tile t, three LDS buffers - measured 339 vs 250 us: its 165 VGPRs leave one 8-wave block per CU)
   f16x8 pf[2][2];
-  auto softmax = [&](f32x16 (&sacc)[2], auto first_tag) {
+  auto softmax = [&](f32x16 (&sacc)[2], auto first_tag) __attribute__((always_inline)) {
     constexpr bool FIRST = decltype(first_tag)::value;
     // lane max of the 32 scores: a depth-4 tree of three-input maxes
     float lmx;
@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
 #pragma unroll
         for (int e = 0; e < 8; ++e) pf[jb][s][e] = (f16)__builtin_amdgcn_exp2f(sacc[jb][8 * s + e]);
   };
-  auto pv = [&](const f16* vs) {
+  auto pv = [&](const f16* vs) __attribute__((always_inline)) {
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
@@ -577,7 +577,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn32(const f16* __restrict__ q, i
     // tile t; the late half runs the PV of tile t - 1 (V at vp, P from the previous interval), then
     // QK^T and softmax of tile t, whose P it keeps across the barrier (16 VGPRs: fewer than the
     // 32 fp32 scores, so the stagger keeps two 8-wave blocks per CU)
-    auto run = [&](int t, const f16* kt, const f16* vt, const f16* vp, auto first_tag) {
+    auto run = [&](int t, const f16* kt, const f16* vt, const f16* vp, auto first_tag) __attribute__((always_inline)) {
       if (!late) {
         qk(kt, t * KV_T, sacc);
         softmax(sacc, first_tag);

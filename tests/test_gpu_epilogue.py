@@ -1,4 +1,5 @@
-"""The two GEMM / conv epilogue forms give the same bits (round 5).
+"""The two GEMM / conv epilogue forms give the same bits (round 5; the post-residual amax - ff.net.2's -
+joined the direct form in round 6).
 
 gemm.hip's shared epilogue stores either straight from the MFMA fragments (v_permlane16_swap pairs
 -> 16-B stores; the default wherever the epilogue needs no row-complete / slot view of the tile) or
@@ -62,8 +63,8 @@ def _forced(v, fn):
         K.force_gemm(None)
 
 
-@pytest.mark.parametrize("epi", ["bias", "bias_res", "plain", "amax", "geglu", "gelu_tanh"])
-@pytest.mark.parametrize("M,N,Kd", [(1000, 320, 320), (4096, 640, 640), (520, 1280, 2560)])
+@pytest.mark.parametrize("epi", ["bias", "bias_res", "plain", "amax", "amax_post", "geglu", "gelu_tanh"])
+@pytest.mark.parametrize("M,N,Kd", [(1000, 320, 320), (4096, 640, 640), (520, 1280, 2560), (8192, 320, 1280)])
 def test_linear_f16_direct_equals_lds(epi, M, N, Kd):
     from qdiff import kernels as K
     g = torch.Generator().manual_seed(M + N + Kd)
@@ -72,17 +73,20 @@ def test_linear_f16_direct_equals_lds(epi, M, N, Kd):
     w = (torch.randn(n2, Kd, generator=g) / Kd ** 0.5).half().to(DEV)
     b = torch.randn(n2, generator=g).half().to(DEV)
     r = torch.randn(M, N, generator=g).half().to(DEV)
-    if epi == "amax" and M % 1024:
+    amx = epi in ("amax", "amax_post")
+    if amx and M % 1024:
         pytest.skip("the amax epilogue needs whole-sample 64-row wave tiles")
     rps = 1024  # amax rows per sample
-    am = torch.zeros((M // rps) * N, dtype=torch.float32, device=DEV) if epi == "amax" else None
+    am = torch.zeros((M // rps) * N, dtype=torch.float32, device=DEV) if amx else None
+    post = epi == "amax_post"  # (ff.net.2: the amax of the final output, residual added)
 
     def run():
         if am is not None:
             am.zero_()
-        y = K.linear(x, w, "f16", bias=None if epi == "plain" else b, residual=r if epi == "bias_res" else None,
-                     amax=am, rows_per_sample=rps if epi == "amax" else 0, geglu=epi == "geglu",
-                     gelu_tanh=epi == "gelu_tanh")
+        y = K.linear(x, w, "f16", bias=None if epi == "plain" else b,
+                     residual=r if epi in ("bias_res", "amax_post") else None,
+                     amax=am, rows_per_sample=rps if amx else 0, geglu=epi == "geglu",
+                     gelu_tanh=epi == "gelu_tanh", amax_post=post)
         return [y] + ([am] if am is not None else [])
     n = 0
     for v in _variants("f16"):
@@ -94,8 +98,8 @@ def test_linear_f16_direct_equals_lds(epi, M, N, Kd):
     assert n > 3
 
 
-@pytest.mark.parametrize("epi", ["bias", "bias_res", "geglu"])
-@pytest.mark.parametrize("M,N,Kd", [(32768, 320, 320), (1000, 640, 640), (2048, 1280, 5120)])
+@pytest.mark.parametrize("epi", ["bias", "bias_res", "amax_post", "geglu"])
+@pytest.mark.parametrize("M,N,Kd", [(32768, 320, 320), (1000, 640, 640), (2048, 1280, 5120), (8192, 320, 1280)])
 def test_linear_i8_direct_equals_lds(epi, M, N, Kd):
     from qdiff import kernels as K
     g = torch.Generator().manual_seed(7 * M + N)
@@ -108,7 +112,15 @@ def test_linear_i8_direct_equals_lds(epi, M, N, Kd):
     wq, sw16, _ = K.weight_quant(w, Kd, 8, want_dq=False)
     sw = sw16.float().view(-1).contiguous()
 
+    post = epi == "amax_post"
+    if post and M % 1024:
+        pytest.skip("the amax epilogue needs whole-sample 64-row wave tiles")
+    am = torch.zeros((M // 1024) * N, dtype=torch.float32, device=DEV) if post else None
+
     def run():
+        if post:
+            am.zero_()
+            return [K.linear_i8(xq, sa, wq, sw, bias=b, residual=r, amax=am, rows_per_sample=1024, amax_post=True), am]
         return [K.linear_i8(xq, sa, wq, sw, bias=b, residual=r if epi == "bias_res" else None, geglu=epi == "geglu")]
     n = 0
     for v in _variants("i8"):
