@@ -74,16 +74,30 @@ __device__ __forceinline__ double rcp_exact(float s) {
   return s == 0.f ? __builtin_inf() : r;
 }
 
+// fq_scale with the fp32 division by qmax replaced by an f64 product with rq ~ 1 / qmax (relative
+// error <= 2^-50; rcp_exact((float)qmax)): bit-identical for every odd qmax (all 2^(b-1) - 1).  With
+// x = a / qmax in the binade [2^e, 2^(e+1)), a (an fp32 >= 2^e) is a multiple of 2^(e-24), as is
+// qmax * M for any fp32 rounding midpoint M (an odd multiple of 2^(e-24)); so |x - M| >= 2^(e-24) / qmax
+// >= 2^-40 x unless a = qmax * M, impossible for odd qmax (an odd multiple of 2^(e-24) of at least 25
+// significant bits).  The f64 product therefore rounds to the fp32 quotient, then to the same fp16.
+__device__ __forceinline__ float fq_scale_rq(float amax, double rq) {
+  const float a = fmaxf(amax, clamp_min_f16());
+  return (float)(f16)(float)((double)a * rq);
+}
+
 // Per-channel fake-quant state of 8 consecutive channels: two 16-B amax loads issued together
-// (a per-element conditional load would make hipcc serialise them), then s and 1/s.
+// (a per-element conditional load would make hipcc serialise them), then s and 1/s; the 8 scale
+// divisions by qmax as one reciprocal and 8 f64 products (fq_scale_rq: ~30 VALU instead of ~80).
 // amax8 must be 16-B aligned (channel offsets are multiples of 8).
 __device__ __forceinline__ void fq_scales8(const float* amax8, int qmax, float (&s)[8], double (&rs)[8]) {
   const float4 a0 = reinterpret_cast<const float4*>(amax8)[0];
   const float4 a1 = reinterpret_cast<const float4*>(amax8)[1];
   const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const double rq = rcp_exact((float)qmax);
+  const bool odd = (qmax & 1) != 0;  // (uniform; an even qmax keeps the division)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    s[j] = fq_scale(a[j], qmax);
+    s[j] = odd ? fq_scale_rq(a[j], rq) : fq_scale(a[j], qmax);
     rs[j] = rcp_exact(s[j]);
   }
 }

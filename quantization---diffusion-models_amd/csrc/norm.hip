@@ -104,6 +104,32 @@ __device__ __forceinline__ f16x8 gn_xf8(const GnIn& in, f16x8 v, const GnXf& t) 
   return v;
 }
 
+// Compile-time-flag forms of gn_xf8<1> / gn_fin8 for the statistics pass (same operations, so the
+// same bits): without the per-element uniform branches on in.qmax / in.cadd the 8 channels'
+// conversion chains interleave instead of issuing one dependent chain at a time.
+template <bool Q, bool A>
+__device__ __forceinline__ f16x8 gn_xf8c(f16x8 v, const GnXf& t) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f16 o = v[j];
+    if constexpr (Q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
+    if constexpr (A) o = to_f16((float)o + t.ca[j]);
+    v[j] = o;
+  }
+  return v;
+}
+
+template <bool Q>
+__device__ __forceinline__ f16x8 gn_fin8c(f16x8 v, const GnXf& t, f16x8 r) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f16 o = v[j];
+    if constexpr (Q) o = fq_apply_r((float)o, t.s[j], t.rs[j]);
+    v[j] = to_f16((float)o + (float)r[j]);
+  }
+  return v;
+}
+
 template <int XF>
 __device__ __forceinline__ f16x8 gn_load8(const GnIn& in, int c, long row, int ch, const GnXf& t) {
   const f16* p = ch < in.c1 ? in.x + row * in.c1 + ch : in.x2 + row * (c - in.c1) + (ch - in.c1);
@@ -175,9 +201,17 @@ __device__ __forceinline__ float gn_out(float xv, float2 k, int silu) {
   return (float)o;
 }
 
-template <int XF>
+// F: the input transform's flags, fixed at compile time (GN_FQ output quant, GN_FA + cadd, GN_FR
+// + residual; the host maps in.qmax / in.cadd / in.res onto them)
+constexpr int GN_FQ = 1, GN_FA = 2, GN_FR = 4;
+
+template <int XF, int F = 0>
 __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg, int rows_per_block,
                                                   float4* __restrict__ part, float* __restrict__ amax_n) {
+  constexpr bool FQ = (F & GN_FQ) != 0, FA = (F & GN_FA) != 0, FR = XF == 2 && (F & GN_FR) != 0;
+  // rows per batch, all loads issued before any use (memory-level parallelism); the residual form
+  // holds two tiles per row, so it batches 4 rows (VGPR budget: more waves per SIMD instead)
+  constexpr int UB = FR ? 4 : 8;
   __shared__ float2 red[256][8];
   const int tx = threadIdx.x, ty = threadIdx.y, bx = blockDim.x, by = blockDim.y;
   const int chunk = blockIdx.x * bx + tx;
@@ -189,38 +223,49 @@ __global__ void __launch_bounds__(256) k_gn_stats(GnIn in, int hw, int c, int cg
   float s1[8], s2[8], sh[8], mn[8], mx[8];
   GnXf xf;
   if (active) gn_xf_init(in, c, n, ch, xf);
+  // the shift of channel ch + j is its group's first element; with >= 8 channels per group the
+  // chunk spans at most two groups, so two (transformed) loads serve all 8 channels
+  const int f0 = ch / cg * cg, f7 = (ch + 7) / cg * cg;
+  float sh0 = 0.f, sh7 = 0.f;
+  if (active && cg >= 8) {
+    sh0 = gn_load1(in, c, n, n * hw, f0);
+    sh7 = gn_load1(in, c, n, n * hw, f7);
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     s1[j] = s2[j] = 0.f;
     mn[j] = INFINITY;
     mx[j] = -INFINITY;
-    sh[j] = active ? gn_load1(in, c, n, n * hw, (ch + j) / cg * cg) : 0.f;
+    sh[j] = !active ? 0.f : cg >= 8 ? ((ch + j) / cg * cg == f0 ? sh0 : sh7) : gn_load1(in, c, n, n * hw, (ch + j) / cg * cg);
   }
+  // (Issuing the first row batch before this setup, and a two-register-set ping-pong that keeps
+  // batch b + 1 in flight while batch b is reduced, measured no faster and cost a wave per SIMD:
+  // profiles/r06i_gn_stats_variants.log.)
   if (active) {
-    // 8 rows per batch, all loads issued before any use (memory-level parallelism)
-    for (int rb = r0 + ty; rb < r1; rb += 8 * by) {
-      f16x8 v[8];
+    for (int rb = r0 + ty; rb < r1; rb += UB * by) {
+      f16x8 v[UB];
       // unconditional loads (row clamped): a guarded load makes hipcc wait per load
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * by, r1 - 1), ch);
-      f16x8 rr[8];
-      if constexpr (XF == 2) {
-        if (in.res) {
+      for (int u = 0; u < UB; ++u) v[u] = gn_raw8(in, c, n * hw + min(rb + u * by, r1 - 1), ch);
+      f16x8 rr[UB];
+      if constexpr (FR) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) rr[u] = *reinterpret_cast<const f16x8*>(in.res + (n * hw + min(rb + u * by, r1 - 1)) * c + ch);
-        }
+        for (int u = 0; u < UB; ++u) rr[u] = *reinterpret_cast<const f16x8*>(in.res + (n * hw + min(rb + u * by, r1 - 1)) * c + ch);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) QD_PIN(v[u]);
+      for (int u = 0; u < UB; ++u) QD_PIN(v[u]);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < UB; ++u) {
         if (rb + u * by >= r1) break;
         f16x8 w;
         if constexpr (XF == 2) {
-          w = in.res ? gn_fin8(in, v[u], xf, rr[u]) : gn_xf8<1>(in, v[u], xf);
+          if constexpr (FR) w = gn_fin8c<FQ>(v[u], xf, rr[u]);
+          else w = gn_xf8c<FQ, FA>(v[u], xf);
           *reinterpret_cast<f16x8*>(in.xout + (n * hw + rb + u * by) * c + ch) = w;
+        } else if constexpr (XF == 1) {
+          w = gn_xf8c<FQ, FA>(v[u], xf);
         } else {
-          w = gn_xf8<XF>(in, v[u], xf);
+          w = v[u];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -301,6 +346,8 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
   // the affine parameters of the thread's first channel, loaded before the partials pass (their
   // latency hides under it instead of following the group statistics)
   const float gm0 = t < cg ? (float)gamma[g0 + t] : 0.f, bt0 = t < cg ? (float)beta[g0 + t] : 0.f;
+  // MODE 0's shift (the group's first element), likewise issued up front by the thread that uses it
+  const float shift0 = MODE == 0 && t == 0 ? gn_load1(in, c, ni, (long)ni * hw, g0) : 0.f;
   if (t == 0) nflag = 0;
   for (int j = t; j < cg; j += 256) {
     cmin[j] = 0x7fffffff;
@@ -320,21 +367,36 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
   // - then MODE 0's finalisation with the shift K1
   const float K1 = MODE == 1 ? pv(0, 0).x : 0.f;
   float s1 = 0.f, s2 = 0.f;
-  for (int e = t; e < Z * cg; e += 256) {
-    const int z = e / cg, j = e - z * cg;
-    const float4 v = pv(z, j);
-    if constexpr (MODE == 0) {
-      s1 += v.x;
-      s2 += v.y;
-    } else {
-      const float d = v.x - K1;
-      s1 += 64.0f * d;
-      s2 += v.y + 64.0f * (d * d);
+  // PF partials per thread in flight before the first is used (one memory round trip instead of
+  // one per 256 partials); the per-thread accumulation order is unchanged (e ascending)
+  constexpr int PF = 4;
+  const int ne = Z * cg;
+  for (int e0 = t; e0 < ne; e0 += 256 * PF) {
+    float4 v[PF];
+    int jj[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const int e = min(e0 + 256 * k, ne - 1);
+      const int z = e / cg;
+      jj[k] = e - z * cg;
+      v[k] = pv(z, jj[k]);
     }
-    if (quant) {
-      const int a = __float_as_int(v.z), b = __float_as_int(v.w);
-      atomicMin(&cmin[j], a ^ ((a >> 31) & 0x7fffffff));
-      atomicMax(&cmax[j], b ^ ((b >> 31) & 0x7fffffff));
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      if (e0 + 256 * k >= ne) break;
+      if constexpr (MODE == 0) {
+        s1 += v[k].x;
+        s2 += v[k].y;
+      } else {
+        const float d = v[k].x - K1;
+        s1 += 64.0f * d;
+        s2 += v[k].y + 64.0f * (d * d);
+      }
+      if (quant) {
+        const int a = __float_as_int(v[k].z), b = __float_as_int(v[k].w);
+        atomicMin(&cmin[jj[k]], a ^ ((a >> 31) & 0x7fffffff));
+        atomicMax(&cmax[jj[k]], b ^ ((b >> 31) & 0x7fffffff));
+      }
     }
   }
   s1 = wave_sum(s1);
@@ -350,7 +412,7 @@ __global__ void __launch_bounds__(256) k_gn_coeff(const float4* __restrict__ par
     const float cnt = (float)cg * (float)hw;
     const float m = S1 / cnt;                        // mean of the shifted values
     const float var = fmaxf(S2 / cnt - m * m, 0.f);  // population variance
-    stat[0] = m + (MODE == 0 ? gn_load1(in, c, ni, (long)ni * hw, g0) : K1);
+    stat[0] = m + (MODE == 0 ? shift0 : K1);
     stat[1] = 1.0f / sqrtf(var + eps);
   }
   __syncthreads();
@@ -716,9 +778,30 @@ static int run_groupnorm(const GnIn& in, int n, int hw, int c, int groups, float
     return 0;
   }
   const dim3 gs(g.gx, n, g.zs), bs(g.bx, g.bys);
-  if (fin) k_gn_stats<2><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
-  else if (xf) k_gn_stats<1><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
-  else k_gn_stats<0><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n);
+  {
+    const int f = (in.qmax > 0 ? GN_FQ : 0) | (in.cadd ? GN_FA : 0) | (in.res ? GN_FR : 0);
+#define QD_GN_STATS(XFV, FV) k_gn_stats<XFV, FV><<<gs, bs, 0, st>>>(in, hw, c, cg, g.rpbs, part, amax_n)
+    if (fin) {
+      switch (f) {  // (the residual and cadd forms exclude each other: host check above)
+        case 0: QD_GN_STATS(2, 0); break;
+        case GN_FQ: QD_GN_STATS(2, GN_FQ); break;
+        case GN_FA: QD_GN_STATS(2, GN_FA); break;
+        case GN_FQ | GN_FA: QD_GN_STATS(2, GN_FQ | GN_FA); break;
+        case GN_FR: QD_GN_STATS(2, GN_FR); break;
+        default: QD_GN_STATS(2, GN_FQ | GN_FR); break;
+      }
+    } else if (xf) {
+      QD_REQUIRE(!in.res, "the residual input form is the materialising statistics pass");
+      switch (f) {
+        case GN_FQ: QD_GN_STATS(1, GN_FQ); break;
+        case GN_FA: QD_GN_STATS(1, GN_FA); break;
+        default: QD_GN_STATS(1, GN_FQ | GN_FA); break;
+      }
+    } else {
+      QD_GN_STATS(0, 0);
+    }
+#undef QD_GN_STATS
+  }
   // (the coefficient stage recomputes its shift / fallback elements from the raw sources; the
   // apply pass reads the materialised x)
   k_gn_coeff<0><<<n * groups, 256, 0, st>>>(part, in, hw, c, cg, g.zs, eps, (const f16*)gamma, (const f16*)beta,

@@ -66,5 +66,7 @@ def run(settings):
 if __name__ == "__main__":
     if "--sweep" in sys.argv:
         run([(0, 0)] + [(s, a) for s in (4, 8, 16, 32) for a in (2, 4, 8, 16)])
+    elif "--srpt" in sys.argv:  # statistics-pass rows per thread only (apply pass at its rule)
+        run([(0, 0)] + [(s, 0) for s in (2, 4, 8, 16, 32)])
     else:
         run([(0, 0)])

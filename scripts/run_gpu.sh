@@ -12,11 +12,14 @@
 #   bench:<args>   bench.py with extra args (',' for spaces), e.g. bench:--model,sdxl
 #   prof_fq        rocprofv3 step profile of the fake-quant mode (scripts/prof_bench.sh)
 #   prof_int8      the same for the int8-MFMA mode
+#   py:<script args, ',' for spaces>   a measurement script, 300 s limit (log: TAG_py<n>.log)
+#   rprof:<script args>  the same under rocprofv3 --kernel-trace --stats (dir: TAG_rprof<n>/)
 set -o pipefail
 TAG=$1
 shift
 mkdir -p gpurun_out
 nt=0
+np=0
 for st in "$@"; do
   case "$st" in
     tests:*)
@@ -50,6 +53,22 @@ for st in "$@"; do
       timeout -k 10 450 bash scripts/prof_bench.sh ${TAG}_int8 400 --mode w8a8-sq-int8 \
         > gpurun_out/${TAG}_prof_int8.log 2>&1 || exit 17
       head -14 gpurun_out/prof_${TAG}_int8/step_classes.txt ;;
+    py:*)
+      args=${st#py:}
+      args=${args//,/ }
+      np=$((np + 1))
+      timeout -k 10 300 python3 -u $args > gpurun_out/${TAG}_py${np}.log 2>&1
+      rc=$?; tail -5 gpurun_out/${TAG}_py${np}.log; [ $rc -eq 0 ] || exit 18 ;;
+    rprof:*)
+      args=${st#rprof:}
+      args=${args//,/ }
+      np=$((np + 1))
+      od=$PWD/gpurun_out/${TAG}_rprof${np}
+      mkdir -p "$od"
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$od" -o run \
+        -- python3 -u $OLDPWD/$args) > "$od/run.log" 2>&1
+      rc=$?; find "$od" -name "*kernel_trace.csv" -size +8M -delete
+      tail -3 "$od/run.log"; [ $rc -eq 0 ] || exit 19 ;;
     *)
       echo "unknown stage $st"; exit 2 ;;
   esac

@@ -401,7 +401,8 @@ def test_groupnorm_fused(c, hw, silu, q, dev):
 
 
 @pytest.mark.parametrize("c,hw,silu,q", [(320, 4096, True, 8), (640, 1024, True, 8), (960, 1024, False, 8),
-                                         (1280, 1024, True, 8), (640, 4096, True, 0)])
+                                         (1280, 1024, True, 8), (640, 4096, True, 0),
+                                         (128, 1024, True, 8)])  # 4 channels per group: per-channel shifts
 def test_groupnorm_streaming_path(c, hw, silu, q, dev):
     """hw > 256: the two streaming passes (statistics -> coefficients -> apply) against torch,
     with channels whose tiny gamma / negative beta keep the SiLU output below the extremes
