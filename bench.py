@@ -151,21 +151,26 @@ def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320, int8=False):
     wt = (torch.randn(c, 3, 3, c, generator=g) / 54).half().to(dev)
     b = torch.zeros(c, dtype=torch.float16, device=dev)
     amax = torch.zeros(n * c, dtype=torch.float32, device=dev)
+    # the input rotates over NROT copies (> the XCDs' aggregate 32 MB of L2): in the step each conv
+    # reads an activation another kernel just wrote, not one its own previous launch left in L2
+    NROT = 4
     if int8:
         xq, sa = K.quant_samples_i8(x)
+        xqs = [xq] + [xq.clone() for _ in range(NROT - 1)]
         wq, sw16, _ = K.weight_quant(wt.view(c, -1).contiguous(), 9 * c, 8, want_dq=False)
         wq, sw = wq.view(c, 3, 3, c), sw16.float().view(-1).contiguous()
         temb = (torch.randn(n, c, generator=g) * 0.1).half().to(dev)
-        run = lambda: K.conv2d_i8(xq, sa, wq, sw, c, 1, 1, bias=b, chan_add=temb, gn_stats=True)
+        run = lambda i: K.conv2d_i8(xqs[i % NROT], sa, wq, sw, c, 1, 1, bias=b, chan_add=temb, gn_stats=True)
     else:
-        run = lambda: K.conv2d_nhwc(x, wt, c, 1, 1, bias=b, amax=amax, amax_zeroed=True)
-    for _ in range(3):
-        run()
+        xs = [x] + [x.clone() for _ in range(NROT - 1)]
+        run = lambda i: K.conv2d_nhwc(xs[i % NROT], wt, c, 1, 1, bias=b, amax=amax, amax_zeroed=True)
+    for i in range(NROT):
+        run(i)
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(iters):
-        run()
+    for i in range(iters):
+        run(i)
     e1.record(st)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters

@@ -134,6 +134,10 @@ int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw, int ci_pa
 #define QD_EPI_SILU 1024     /* qd_linear_fwd GEMV shapes only (M <= 4): out = half(silu(out)) after the
                                 bias / residual rounding - the diffusers TimestepEmbedding act and
                                 the UNet's silu(temb), bit-identical to qd_silu on the output */
+#define QD_EPI_ROWREP 2048   /* qd_linear_fwd GEMV shapes with M == 1, no residual: the output row is
+                                stored to rows 0 .. rows_per_sample - 1 of y (stride ldy) - a batch whose
+                                rows share one input (the CFG batch's time embedding: every row embeds
+                                the same timestep) computed once, every row bit-identical */
 
 /* y[M, N] = x[M, K] . W[N, K]^T (+ epilogue).  WxAxLinear.forward's F.linear
  * (fake_quant.py:223) with the dequant of the stored codes fused into the B-tile staging.

@@ -152,6 +152,9 @@ def linear(a, outs):
     y16 = acc.half()
     k = x.shape[1]
     atol = sum_atol(x.abs() @ w.abs().t(), k)
+    if a.get("rep_rows"):  # QD_EPI_ROWREP: the one computed row stored to rep_rows rows
+        y16 = y16.expand(a["rep_rows"], -1).contiguous()
+        atol = atol.expand(a["rep_rows"], -1).contiguous()
     res = []
     if a.get("geglu"):
         m, n2 = y16.shape

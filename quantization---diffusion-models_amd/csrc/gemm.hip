@@ -3696,6 +3696,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
   const bool gtanh = (p.epi & QD_EPI_GELU_TANH) != 0;
   const bool silu = (p.epi & QD_EPI_SILU) != 0;
+  const int reps = (p.epi & QD_EPI_ROWREP) ? p.rows_per_sample : 1;
   const long nwaves = (long)gridDim.x * 4;
   for (long n0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R; n0 < p.N; n0 += nwaves * R) {
     float acc[R][MM];
@@ -3730,6 +3731,7 @@ __global__ void __launch_bounds__(256) k_gemv(GemmArgs p) {
           if (has_res) h = (f16)((float)h + (float)p.res[(long)m * p.ldy + n]);
           if (silu) h = to_f16(silu_f((float)h));   // = k_silu on the rounded output
           p.y[(long)m * p.ldy + n] = h;
+          for (int q = 1; q < reps; ++q) p.y[(long)q * p.ldy + n] = h;   // QD_EPI_ROWREP (M == 1)
         }
       }
   }
@@ -3969,6 +3971,9 @@ static int linear_fwd(const void* x, int M, int K, int lda, const void* w, int w
     qd_zero_f32(amax, (size_t)((M + rows_per_sample - 1) / rows_per_sample) * N, S(stream));
   const int cpl = ln ? 0 : gemv_cpl(p);
   QD_REQUIRE(!(epi & QD_EPI_SILU) || cpl, "SiLU epilogue: GEMV shapes only (M <= 4, no amax / GEGLU)");
+  QD_REQUIRE(!(epi & QD_EPI_ROWREP) || (cpl && M == 1 && rows_per_sample >= 1 && !(epi & QD_EPI_RESIDUAL) &&
+                                        (double)rows_per_sample * ldy * 2 < 2147483648.0),
+             "row-replicating epilogue: GEMV shapes with M == 1, rows_per_sample >= 1 output rows, no residual");
   if (cpl) launch_gemv(p, wfmt, cpl, S(stream));
   else run_gemm<AM_LINEAR>(p, wfmt, ws, ws_elems, S(stream));
   QD_CHECK_LAUNCH();

@@ -26,6 +26,7 @@ EPI_AMAX_POST = 64
 EPI_CADD = 128
 EPI_GNSTATS = 256
 EPI_SILU = 1024
+EPI_ROWREP = 2048
 GRAN_ZEROED = 0x100
 
 
@@ -419,7 +420,7 @@ def gemv_shape(M, K, epi):
 
 def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=None, out=None,
            amax=None, rows_per_sample=0, amax_zeroed=False, geglu=False, weight_f16=None, gelu_tanh=False,
-           amax_post=False, silu=False):
+           amax_post=False, silu=False, rep_rows=0):
     """y = x . W^T (+bias) (+residual); x2d [M, K] fp16 (row stride may exceed K).
     geglu: W rows (and bias) interleaved in 16-row [hidden | gate] blocks (geglu_interleave);
     returns half(h * half(gelu(g))) of width N / 2 (diffusers GEGLU fused into the epilogue).
@@ -429,22 +430,30 @@ def linear(x2d, weight, wfmt="f16", scales=None, group=0, bias=None, residual=No
     weight_f16: the same weight's fp16 dequantized buffer (bit-identical to dequantizing the
     codes); when given, the kernel search also considers the fp16 LDS-DMA family.
     silu (GEMV shapes only, gemv_shape(M, K, ...)): returns half(silu(out)) - the diffusers
-    TimestepEmbedding activation / the UNet's silu(temb) - bit-identical to silu() on the output."""
+    TimestepEmbedding activation / the UNet's silu(temb) - bit-identical to silu() on the output.
+    rep_rows (x2d of ONE row on a GEMV shape, no residual): returns [rep_rows, N], every row the
+    one computed row (QD_EPI_ROWREP: a batch whose rows share one input, computed once)."""
     if x2d.dtype != torch.float16 or not x2d.is_cuda:
         raise ValueError("x must be an fp16 HIP tensor")
     if x2d.dim() != 2 or x2d.stride(1) != 1:
         raise ValueError("x must be 2-D with unit column stride")
     M, K = x2d.shape
     N = weight.shape[0]
+    if rep_rows:
+        if M != 1 or residual is not None or rep_rows < 1:
+            raise ValueError("linear(rep_rows=R) takes one input row and no residual")
+        rows_per_sample = rep_rows
     if out is None:
-        out = _empty((M, N // 2 if geglu else N), torch.float16, x2d.device)
+        out = _empty((rep_rows or M, N // 2 if geglu else N), torch.float16, x2d.device)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) | \
           (EPI_AMAX if amax is not None else 0) | (EPI_AMAX_ZEROED if amax is not None and amax_zeroed else 0) | \
           (EPI_GEGLU if geglu else 0) | (EPI_GELU_TANH if gelu_tanh else 0) | \
           (EPI_AMAX_POST if amax_post and amax is not None and residual is not None else 0) | \
-          (EPI_SILU if silu else 0)
+          (EPI_SILU if silu else 0) | (EPI_ROWREP if rep_rows else 0)
     if silu and not gemv_shape(M, K, epi):
         raise ValueError("linear(silu=True) needs a GEMV shape (M <= 4, no amax / GEGLU epilogue)")
+    if rep_rows and not gemv_shape(M, K, epi):
+        raise ValueError("linear(rep_rows=R) needs a GEMV shape (no amax / GEGLU epilogue)")
     if residual is not None:
         _chk(residual, "residual")
     ops = [(weight, wfmt, scales, group)]

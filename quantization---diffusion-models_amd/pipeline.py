@@ -94,7 +94,7 @@ class DenoiseLoop:
         with A.using(self.arena, frozen=frozen):
             K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
                                  shift=float(self.unet.config.freq_shift), out=self.temb_in)
-            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
+            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv, temb_shared=True)
             K.cfg_ddim_step(self.lat, out, self.guidance, self.a_t, self.a_p, self.step_idx, self.next_in,
                             c=self.cin)
         self.last_out = out
@@ -170,7 +170,7 @@ class PNDMDenoiseLoop(DenoiseLoop):
         with A.using(self.arena, frozen=frozen):
             K.timestep_embedding(self.ts_f32, self.step_idx, 2 * self.B, self.c0, flip_sin_to_cos=True,
                                  shift=float(self.unet.config.freq_shift), out=self.temb_in)
-            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv)
+            out = self.unet.fwd(self.next_in, self.temb_in, self.ctx_kv, temb_shared=True)
             K.cfg_pndm_step(self.lat, out, self.guidance, self.a_t, self.a_p, self.step_idx, self.ets, self.cur,
                             self.next_in, c=self.cin)
         self.last_out = out

@@ -335,24 +335,47 @@ class UNet2DConditionModel(nn.Module):
                 kv[id(m.attn2)] = (k, v)
         return kv
 
+    def _shared_temb(self, temb_in):
+        """temb_projections() of a batch whose rows all embed ONE timestep (the denoising loops):
+        linear_1 -> SiLU -> linear_2 -> SiLU on row 0 alone (GEMVs with the SiLU epilogue), then the
+        resnets' stacked time_emb_proj on that row with the output stored to every row
+        (QD_EPI_ROWREP).  Row by row the same ops as the batched form (the activation fake-quants
+        reduce over identical rows); only the GEMMs' fp32 summation order differs.  None when the
+        shared form does not apply (calibration hooks, no stacked projection)."""
+        l1, l2 = self.time_embedding.linear_1, self.time_embedding.linear_2
+        op = self._temb_operand()
+        if op is None or temb_in.shape[0] < 2 or any(getattr(m, "_qd_hook", None) is not None for m in (l1, l2)):
+            return None
+        t = run_linear(l1, temb_in[:1], silu=True)
+        ts = run_linear(l2, t, silu=True)
+        w, fmt, sc, g, b, wf, slots = op
+        y = K.linear(ts, w, fmt, sc, g, bias=b, weight_f16=wf, rep_rows=temb_in.shape[0])
+        return {rid: y[:, off:off + co] for rid, off, co in slots}
+
     @torch.no_grad()
-    def fwd(self, x, temb_in, ctx_kv, add_emb_in=None):
+    def fwd(self, x, temb_in, ctx_kv, add_emb_in=None, temb_shared=False):
         """x: [2B, H, W, Cp] fp16 NHWC (Cp = in_channels padded to 8); temb_in: [2B, C0] fp16
-        sinusoidal timestep features; returns the noise prediction [2B, H, W, 8] (4 real ch)."""
+        sinusoidal timestep features; returns the noise prediction [2B, H, W, 8] (4 real ch).
+        temb_shared: every row of temb_in embeds the same timestep (the caller's guarantee: one
+        timestep per denoising step for the whole CFG batch) - the time embedding runs once."""
         cfg = self.config
-        # TimestepEmbedding linear_1 -> SiLU -> linear_2, then the resnets' silu(temb): the SiLUs
-        # ride in the GEMV epilogues where the CFG batch runs on the GEMV (M <= 4: SDXL / SD3 at
-        # one prompt per GPU), else separate passes (SD1.5's M = 8 stays on the tile GEMM)
-        t = run_linear(self.time_embedding.linear_1, temb_in, silu=True)
-        if self.add_embedding is not None:
-            if add_emb_in is None:
-                raise ValueError("SDXL UNet needs the text_time additional embedding input")
-            temb = run_linear(self.time_embedding.linear_2, t)
-            a = run_linear(self.add_embedding.linear_1, add_emb_in, silu=True)
-            temb_silu = run_linear(self.add_embedding.linear_2, a, residual=temb, silu=True)
+        tps = self._shared_temb(temb_in) if temb_shared and self.add_embedding is None else None
+        if tps is not None:
+            temb_silu = None  # (every resnet takes its slice of the stacked projection)
         else:
-            temb_silu = run_linear(self.time_embedding.linear_2, t, silu=True)
-        tps = self.temb_projections(temb_silu)
+            # TimestepEmbedding linear_1 -> SiLU -> linear_2, then the resnets' silu(temb): the SiLUs
+            # ride in the GEMV epilogues where the CFG batch runs on the GEMV (M <= 4: SDXL / SD3 at
+            # one prompt per GPU), else separate passes (SD1.5's M = 8 stays on the tile GEMM)
+            t = run_linear(self.time_embedding.linear_1, temb_in, silu=True)
+            if self.add_embedding is not None:
+                if add_emb_in is None:
+                    raise ValueError("SDXL UNet needs the text_time additional embedding input")
+                temb = run_linear(self.time_embedding.linear_2, t)
+                a = run_linear(self.add_embedding.linear_1, add_emb_in, silu=True)
+                temb_silu = run_linear(self.add_embedding.linear_2, a, residual=temb, silu=True)
+            else:
+                temb_silu = run_linear(self.time_embedding.linear_2, t, silu=True)
+            tps = self.temb_projections(temb_silu)
 
         h = run_conv(self.conv_in, x, c_valid=cfg.in_channels)
         skips = [h]

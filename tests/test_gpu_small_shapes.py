@@ -141,3 +141,74 @@ def test_act_fq_small_bit_exact(n, h, w, c, cv, dev):
     # and the two-pass form on the same input
     two = k.act_apply_nhwc(xd, k.act_absmax(xd, "per_channel", k.NHWC), 8, c_valid=cv).cpu()
     assert torch.equal(y.view(torch.int16), two.view(torch.int16))
+
+
+@pytest.mark.parametrize("fmt", ["f16", "i8", "i4"])
+@pytest.mark.parametrize("N,Kd,silu", [(1280, 320, True), (1280, 1280, True), (20160, 1280, False)])
+def test_gemv_row_replicating_epilogue(fmt, N, Kd, silu, dev):
+    """QD_EPI_ROWREP: one input row, the GEMV's output row stored to every row of [R, N] - each row
+    bit-identical to the one-row call."""
+    k = K()
+    g = torch.Generator().manual_seed(N + Kd)
+    x = torch.randn(1, Kd, generator=g).half().to(dev)
+    w = (torch.randn(N, Kd, generator=g) / math.sqrt(Kd)).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    wop, f, sc, gr, _ = _w_operand(k, w, fmt, 64)
+    one = k.linear(x, wop, f, sc, gr, bias=b, silu=silu)
+    rep = k.linear(x, wop, f, sc, gr, bias=b, silu=silu, rep_rows=8)
+    assert rep.shape == (8, N)
+    assert torch.equal(rep.view(torch.int16), one.expand(8, N).contiguous().view(torch.int16))
+
+
+def test_gemv_row_replicating_rejects(dev):
+    k = K()
+    w = torch.randn(1280, 320, device=dev).half()
+    with pytest.raises(ValueError):
+        k.linear(torch.randn(2, 320, device=dev).half(), w, rep_rows=8)
+    with pytest.raises(ValueError):
+        k.linear(torch.randn(1, 320, device=dev).half(), w, residual=torch.zeros(1, 1280, device=dev).half(),
+                 rep_rows=8)
+
+
+@pytest.mark.parametrize("qc", [None, dict(w_bit=8, a_bit=8, q_group_size=128, quantize_act=True)])
+def test_unet_shared_time_embedding(qc, dev):
+    """UNet fwd(temb_shared=True) - the denoising loops' one-timestep batch: the time embedding on
+    row 0 and the stacked time_emb_proj stored to every row - against the batched form: every
+    resnet's projection row within the GEMMs' summation-order bound (GEMV vs tile GEMM, through two
+    SiLUs), all rows identical; and the whole eval against the oracle under test_gpu_unet's
+    self-calibrated criterion."""
+    import test_gpu_unet as TU
+    from oracle.unet_ref import RefUNet
+    k = K()
+    model = TU._model(seed=3)
+    unet = model.pipeline.unet
+    cfg = unet.config
+    sd = {kk: v.detach().cpu() for kk, v in unet.state_dict().items()}
+    if qc is not None:
+        model.quantize(quant_config=dict(qc), quantUnet=True)
+    B = 8
+    ts = torch.tensor([601.0], device=dev)
+    temb = k.timestep_embedding(ts, None, B, cfg.block_out_channels[0])
+    shared = unet._shared_temb(temb)
+    assert shared is not None
+    t = unet.time_embedding
+    from qdiff.unet import run_linear
+    batched = unet.temb_projections(run_linear(t.linear_2, run_linear(t.linear_1, temb, silu=True), silu=True))
+    assert shared.keys() == batched.keys()
+    for rid, a in shared.items():
+        a, bb = a.float().cpu(), batched[rid].float().cpu()
+        assert (a == a[:1]).all(), "rows of the shared projection differ"
+        err = (a - bb).abs()
+        tol = 8 * ulp16(bb) + 1e-3 * bb.abs().max()
+        assert (err <= tol).all(), (err / tol).max().item()
+    # the whole eval (the loop's form) against the oracle
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(B, 4, cfg.sample_size, cfg.sample_size, generator=g).half()
+    ctx = torch.randn(B, 77, cfg.cross_attention_dim, generator=g).half()
+    kv = unet.prepare_context(ctx.to(dev))
+    out = unet.fwd(k.nchw_to_nhwc(x.to(dev), 8), temb, kv, temb_shared=True)
+    got = k.nhwc_to_nchw(out, 4).cpu()
+    q = None if qc is None else dict(qc)
+    ref = RefUNet(TU._cfgdict(cfg), sd, q).forward(x, 601, ctx)
+    ref32 = RefUNet(TU._cfgdict(cfg), sd, q, variant="fp32").forward(x, 601, ctx)
+    TU._check_parity(got, ref, ref32, f"tiny UNet shared-temb eval {qc}")
