@@ -63,7 +63,29 @@ def run(settings):
     lib.qd_gn_geom_force(0, 0)
 
 
+SMALL = [(8, 256, 640), (8, 256, 1280), (8, 256, 1920), (8, 64, 1280), (8, 64, 2560), (8, 256, 960)]
+
+
+def run_small():
+    """The single-kernel GroupNorm (hw <= 256): plain GroupNorm + SiLU + fake-quant, and the fq_in form
+    (the conv output's fake-quant + temb add recomputed on the fly)."""
+    for n, hw, c in SMALL:
+        g = torch.Generator(device=dev).manual_seed(0)
+        x = torch.randn(n, hw, c, device=dev, generator=g).half()
+        amax = x.float().abs().amax(dim=1).reshape(-1).contiguous()
+        temb = torch.randn(n, c, device=dev, generator=g).half()
+        gam = (1 + 0.1 * torch.randn(c, device=dev, generator=g)).half()
+        bet = (0.1 * torch.randn(c, device=dev, generator=g)).half()
+        pln = lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8)
+        fqi = lambda: K.groupnorm_nhwc(x, 32, 1e-5, gam, bet, silu=True, q_bits=8, fq_in=(amax, 8, temb))
+        print(f"small n={n} hw={hw:4d} c={c:5d}: plain {timeit(pln):6.1f} us  fq_in+temb {timeit(fqi):6.1f} us",
+              flush=True)
+
+
 if __name__ == "__main__":
+    if "--small" in sys.argv:
+        run_small()
+        sys.exit(0)
     if "--sweep" in sys.argv:
         run([(0, 0)] + [(s, a) for s in (4, 8, 16, 32) for a in (2, 4, 8, 16)])
     elif "--srpt" in sys.argv:  # statistics-pass rows per thread only (apply pass at its rule)
