@@ -2374,15 +2374,21 @@ __global__ void __launch_bounds__(512, 2) k_conv_halo(GemmArgs p) {
 // overwrites the slot of s-1, whose last reads fed MFMA(s-1, half 1) before barrier s; halo rows
 // of chunk c+1 go into chunk c-1's buffer after barrier (c, tap 0), after the last reads of chunk
 // c-1 (MFMA(c-1, tap 8, half 1)).  Same K order as the lock-step kernel: identical bits.
-template <int BN>
-__global__ void __launch_bounds__(512, 1) k_conv_halo2(GemmArgs p) {
-  constexpr int BM = 256, NT = 512, NW = 8, WGN = 2;
+// BM 128 (variants 204 / 205, W <= 32): 4 waves (2 x 2) on 128-pixel tiles.  At 32x32 x 640 channels
+// (CFG batch 8) the 256-pixel tiles make 32 x 5 = 160 tiles for 256 CUs; 128 x 160 tiles make 256.
+template <int BM>
+constexpr int halo2_rows() { return BM == 256 ? HALO_ROWS_MAX : 208; }  // (RB + 2) * (W + 2): 204 at W 32, 180 at W 16
+
+template <int BN, int BM = 256>
+__global__ void __launch_bounds__(2 * BM, 1) k_conv_halo2(GemmArgs p) {
+  constexpr int NT = 2 * BM, NW = NT / 64, WGN = 2;
   constexpr int WM = 64, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
-  constexpr int HSZ = HALO_ROWS_MAX * BK;
+  static_assert((NW / WGN) * WM == BM, "wave grid");
+  constexpr int HSZ = halo2_rows<BM>() * BK;
   constexpr int BSZ = BN * BK;
   constexpr int LDSZ = 2 * HSZ + 3 * BSZ > epi_lds_halves(BM, BN) ? 2 * HSZ + 3 * BSZ : epi_lds_halves(BM, BN);
   static_assert(LDSZ * 2 <= 163840, "halo + weight ring exceed the 160 KB of LDS");
-  constexpr int HG = HALO_ROWS_MAX / 8;
+  constexpr int HG = halo2_rows<BM>() / 8;
   constexpr int HL = (HG + NW - 1) / NW;
   static_assert(HL <= 8, "halo rows must stage within the 8 tap steps of a chunk");
   using BL = BDma<BN, NT, 64>;
@@ -2824,6 +2830,8 @@ static void launch_halo_i8(const GemmArgs& p, hipStream_t st) {
 // halo kernel applicability: 3x3 / stride 1 / pad 1, 64-channel chunks, whole-row bm-pixel tiles
 static bool halo_ok(const GemmArgs& p, int bn, int chunk = 64, int bm = 256) {
   const bool w_ok = bm == 64 ? (p.W == 8 && p.H == 8 && chunk == 32) : (p.W == 16 || p.W == 32 || p.W == 64);
+  // the fp16 split-phase kernel's 128-pixel tiles stage at most halo2_rows<128>() halo rows
+  if (chunk == 64 && bm == 128 && (bm / std::max(p.W, 1) + 2) * (p.W + 2) > halo2_rows<128>()) return false;
   return p.kh == 3 && p.kw == 3 && p.stride == 1 && p.pad == 1 && p.Cip % chunk == 0 && p.N % bn == 0 && w_ok &&
          p.Ho == p.H && p.Wo == p.W && p.H % (bm / p.W) == 0 && (p.rows_per_sample % 64 == 0);
 }
@@ -3352,10 +3360,10 @@ static bool forced_split(int nsteps, int s_min_steps, int& sp) {
 extern "C" int qd_gemm_force(int variant) {
   const int v = variant >= 1000 ? variant % 1000 : variant, sp = variant >= 1000 ? variant / 1000 : 0;
   QD_REQUIRE(v == -1 || (v >= 0 && v < 4) ||
-                 (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 203) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
+                 (v >= 100 && v < 100 + (int)(sizeof(kDmaC) / sizeof(kDmaC[0]))) || (v >= 200 && v <= 205) || (v >= 300 && v <= 304) || (v >= 120 && v <= 123) ||
                  (v >= 130 && v <= 134) || (v >= 140 && v <= 151) || (v >= 160 && v <= 167) || (v >= 170 && v <= 177) ||
                  (v >= 190 && v <= 192),
-             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..117, fp8: 120..123), 200-203 halo conv, "
+             "qd_gemm_force: -1, 0..3, 100 + DMA variant (int8: 110..117, fp8: 120..123), 200-205 halo conv, "
              "300-304 ping-pong (int8: 130-134, int8 halo conv 140-149, fused GEGLU codes 150 / 151, persistent "
              "int8 DMA linears 160-167 / 170-177: variants 10-17 with 2 / 4 tiles per block, A-stationary int8 "
              "linears 190-192); + 1000 * s: "
@@ -3400,14 +3408,15 @@ static Plan plan_gemm(int M, int N, int K, bool quant_w, int rows_per_sample, bo
       }
     }
   }
-  if (g_force >= 200 && g_force <= 203 && !quant_w && !geglu && K % 576 == 0) {
+  if (g_force >= 200 && g_force <= 205 && !quant_w && !geglu && K % 576 == 0) {
     // halo conv (applicability is checked at launch; the split only needs the chunk count):
-    // 200 / 201 BN 160 / 128 lock-step, 202 / 203 the same tiles split-phase
-    const int bn = (g_force & 1) ? 128 : 160;
-    if (N % bn == 0 && M % 256 == 0) {
-      const long tiles_mn = (long)(M / 256) * (N / bn);
+    // 200 / 201 BN 160 / 128 lock-step, 202 / 203 the same tiles split-phase, 204 / 205 split-phase
+    // on 128-pixel tiles (4 waves)
+    const int bn = (g_force & 1) ? 128 : 160, bm = g_force >= 204 ? 128 : 256;
+    if (N % bn == 0 && M % bm == 0) {
+      const long tiles_mn = (long)(M / bm) * (N / bn);
       const int nc = K / 576;
-      best = {2, 256, bn, g_force >= 202 ? 1 : 0, 1, nc};
+      best = {2, bm, bn, g_force >= 202 ? 1 : 0, 1, nc};
       int fsp;
       if (forced_split(nc, 1, fsp)) {
         best.splits = fsp;
@@ -3567,8 +3576,11 @@ static void launch_tile(const GemmArgs& p, const Plan& pl, int fmt, hipStream_t 
     else if (pl.bn == 160) k_gemm_pp<160, 4, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
     else k_gemm_pp<128, 4, AMODE, SPLIT><<<nwg, 512, 0, st>>>(p);
   } else if (pl.kind == 2) {
-    const int nwg = (p.M / 256) * (p.N / pl.bn) * p.splits;
-    if (pl.var == 1) {
+    const int nwg = (p.M / pl.bm) * (p.N / pl.bn) * p.splits;
+    if (pl.var == 1 && pl.bm == 128) {
+      if (pl.bn == 160) k_conv_halo2<160, 128><<<nwg, 256, 0, st>>>(p);
+      else k_conv_halo2<128, 128><<<nwg, 256, 0, st>>>(p);
+    } else if (pl.var == 1) {
       if (pl.bn == 160) k_conv_halo2<160><<<nwg, 512, 0, st>>>(p);
       else k_conv_halo2<128><<<nwg, 512, 0, st>>>(p);
     } else {
@@ -3804,7 +3816,7 @@ static void run_gemm(GemmArgs& p, int fmt, float* ws, long ws_elems, hipStream_t
   const int w4g = fmt == QD_WFMT_I4 && p.bscale_t != nullptr && AMODE == AM_LINEAR ? p.group : 0;
   Plan pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,
                       (p.epi & QD_EPI_GEGLU) != 0, post, w4g);
-  if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn))) {  // halo conv not applicable
+  if (pl.kind == 2 && (AMODE != AM_CONV || !halo_ok(p, pl.bn, 64, pl.bm))) {  // halo conv not applicable
     const int f = g_force;
     g_force = -1;
     pl = plan_gemm(p.M, p.N, p.K, fmt != QD_WFMT_F16, p.rows_per_sample, (p.epi & QD_EPI_AMAX) != 0,

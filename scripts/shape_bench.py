@@ -19,6 +19,8 @@ from qdiff import kernels as K  # noqa: E402
 CONVS = [(8, 64, 64, 320, 320, 3, 1, 7), (8, 32, 32, 640, 640, 3, 1, 6), (8, 16, 16, 1280, 1280, 3, 1, 7),
          (8, 8, 8, 1280, 1280, 3, 1, 8), (8, 64, 64, 640, 320, 3, 1, 2), (8, 64, 64, 960, 320, 3, 1, 1),
          (8, 32, 32, 1280, 640, 3, 1, 2), (8, 16, 16, 2560, 1280, 3, 1, 2), (8, 32, 32, 320, 640, 3, 1, 1)]
+# the down-block samplers (stride 2): --stride2 runs only these
+CONVS_S2 = [(8, 64, 64, 320, 320, 3, 2, 1), (8, 32, 32, 640, 640, 3, 2, 1), (8, 16, 16, 1280, 1280, 3, 2, 1)]
 # (M, N, K, geglu, count per eval)
 LINS = [(32768, 320, 320, False, 25), (32768, 960, 320, False, 5), (32768, 2560, 320, True, 5),
         (32768, 320, 1280, False, 5), (8192, 640, 640, False, 25), (8192, 5120, 640, True, 5),
@@ -79,6 +81,7 @@ def main():
     ap.add_argument("--amax", action="store_true")
     ap.add_argument("--w4", action="store_true")
     ap.add_argument("--mscale", type=int, default=1)
+    ap.add_argument("--stride2", action="store_true")
     a = ap.parse_args()
     if a.w4:
         return w4_linears(a)
@@ -89,7 +92,7 @@ def main():
     else:
         variants = list(K.REG_VARIANTS) + list(K.DMA_VARIANTS)
     if a.only != "linear":
-        for (n, h, w, ci, co, k, s, cnt) in CONVS:
+        for (n, h, w, ci, co, k, s, cnt) in (CONVS_S2 if a.stride2 else CONVS):
             x = torch.randn(n, h, w, ci, generator=g).half().to(dev)
             wt = (torch.randn(co, k, k, ci, generator=g) / (k * k * ci) ** 0.5).half().to(dev)
             b = torch.zeros(co, dtype=torch.float16, device=dev)
@@ -105,7 +108,7 @@ def main():
                 am = torch.zeros(n * co, dtype=torch.float32, device=dev) if a.amax else None
                 res = run_variants(lambda: K.conv2d_nhwc(x, wt, ci, s, k // 2, bias=b, amax=am), vs, a.iters)
             print(f"conv ({n},{h},{w},{ci},{co},{k}){' amax' if a.amax else ''} x{cnt}: " + fmt(res, flops), flush=True)
-    if a.only != "conv":
+    if a.only != "conv" and not a.stride2:
         for (m, nn, kk, geglu, cnt) in LINS:
             x = torch.randn(m, kk, generator=g).half().to(dev)
             wt = (torch.randn(nn, kk, generator=g) / kk ** 0.5).half().to(dev)

@@ -120,6 +120,9 @@ def main():
                     help="with --add: first drop the entries whose epilogue flags intersect this mask")
     ap.add_argument("--drop-conv-hw", type=int, default=0,
                     help="with --add: also drop the fp16 / int8 conv entries whose input side is <= this")
+    ap.add_argument("--drop-f16-halo-hw", type=int, default=0,
+                    help="with --add: also drop the fp16 3x3 stride-1 conv entries whose input side is <= this "
+                         "(new halo candidates: the 128-pixel tiles 204 / 205)")
     ap.add_argument("--retune-i8-linear", action="store_true",
                     help="keep the committed table, re-tune only the int8 linears (SD1.5, both modes run)")
     ap.add_argument("--retune-f16-linear", action="store_true",
@@ -178,6 +181,10 @@ def main():
                 dropped[key] = K._TUNE.pop(key)
         if a.drop_conv_hw:
             for key in [k for k in K.gemm_choices() if k[0] in ("conv", "conv_i8") and k[2] <= a.drop_conv_hw]:
+                dropped[key] = K._TUNE.pop(key)
+        if a.drop_f16_halo_hw:
+            for key in [k for k in K.gemm_choices() if k[0] == "conv" and k[6] == 3 and k[8] == 1 and
+                        k[2] <= a.drop_f16_halo_hw]:
                 dropped[key] = K._TUNE.pop(key)
         log(f"committed table ({n0} shapes)")
         for name in a.models.split(","):

@@ -774,7 +774,7 @@ def test_fast_reciprocal_fake_quant_is_exact(dev):
     assert counts.tolist() == [0, 0, 0]
 
 
-@pytest.mark.parametrize("variant", [200, 201, 202, 203])
+@pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205])
 def test_conv_halo_kernel(variant, forced_gemm, dev):
     """Halo-staged 3x3 conv: 16/32/64-wide images, fused 2x upsample, split-K over channel
     chunks (ragged 64-channel chunk counts), bias + amax + residual epilogues."""
@@ -809,14 +809,18 @@ def test_conv_halo_kernel(variant, forced_gemm, dev):
 def test_conv_halo_split_phase_bit_identical(forced_gemm, dev):
     """The split-phase halo conv (202 / 203) changes only when tiles are loaded and read, not the K
     order: its outputs equal the lock-step halo kernel's (200 / 201) bit for bit, on the SD1.5 64x64 shape at
-    full width (every pipeline position of a 5-chunk, 45-step K loop) and a split-K shape."""
+    full width (every pipeline position of a 5-chunk, 45-step K loop) and a split-K shape; so do its
+    128-pixel tiles (204 / 205, images up to 32 wide: the same K order per output pixel)."""
     k = K()
     g = torch.Generator().manual_seed(31)
-    for n, hw, cin, cout in ((8, 64, 320, 320), (2, 16, 1280, 1280), (2, 32, 640, 640)):
+    for n, hw, cin, cout in ((8, 64, 320, 320), (2, 16, 1280, 1280), (2, 32, 640, 640), (8, 32, 640, 640)):
         x = torch.randn(n, hw, hw, cin, generator=g).half().to(dev)
         wk = (torch.randn(cout, 3, 3, cin, generator=g) / (cin * 9) ** 0.5).half().to(dev)
         b = torch.randn(cout, generator=g).half().to(dev)
-        for vs in ((200, 202), (201, 203)):
+        # (the 128-pixel tiles against the others at one explicit split count, 1000 * s + variant: the
+        # planner's own split choice depends on the tile count)
+        pairs = ((200, 202), (201, 203)) + (((1200, 1202, 1204), (1201, 1203, 1205)) if hw <= 32 else ())
+        for vs in pairs:
             outs = []
             for v in vs:
                 forced_gemm(v)
