@@ -222,7 +222,10 @@ def conv_weight_khwc(w, ci_pad):
 REG_VARIANTS = (0, 1, 2, 3)                        # qd_gemm_force ids of the register tiles
 DMA_VARIANTS = (100, 101, 103, 104, 105, 106, 109, 114, 115, 116, 117,   # LDS-DMA variants (fp16 weights)
                 300, 301, 302, 303, 304)                        # ping-pong 256-row
-HALO_VARIANTS = (200, 201, 202, 203, 204, 205)  # 3x3 conv with the activation halo staged once per channel chunk
+HALO_VARIANTS = (200, 201, 202, 203)  # 3x3 conv with the activation halo staged once per channel chunk
+# (204 / 205, the split-phase kernel on 128-pixel tiles, stay forceable but are no tuner candidates: the
+# tuner times a shape on warm, repeated inputs, where they win at 32x32 (63.5 vs 70.7 us), while in the
+# captured step - cold inputs - they ran 3-45 % slower; profiles/r06t_halo128_in_step_rejected.log)
 # packed int4 through the lock-step LDS-DMA stages and the ping-pong tiles (BDma4 code stages,
 # dequantized per fragment)
 W4_VARIANTS = (100, 101, 102, 103, 104, 105, 109, 110, 111, 112, 113, 114, 115, 116, 117, 300, 301, 302, 303, 304)
