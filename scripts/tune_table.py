@@ -120,6 +120,8 @@ def main():
                     help="with --add: first drop the entries whose epilogue flags intersect this mask")
     ap.add_argument("--drop-conv-hw", type=int, default=0,
                     help="with --add: also drop the fp16 / int8 conv entries whose input side is <= this")
+    ap.add_argument("--drop-all", action="store_true",
+                    help="with --add: re-tune every shape the runs meet (the others keep their committed choice)")
     ap.add_argument("--drop-f16-halo-hw", type=int, default=0,
                     help="with --add: also drop the fp16 3x3 stride-1 conv entries whose input side is <= this "
                          "(new halo candidates: the 128-pixel tiles 204 / 205)")
@@ -182,6 +184,8 @@ def main():
         if a.drop_conv_hw:
             for key in [k for k in K.gemm_choices() if k[0] in ("conv", "conv_i8") and k[2] <= a.drop_conv_hw]:
                 dropped[key] = K._TUNE.pop(key)
+        if a.drop_all:
+            dropped.update({k: K._TUNE.pop(k) for k in list(K.gemm_choices())})
         if a.drop_f16_halo_hw:
             for key in [k for k in K.gemm_choices() if k[0] == "conv" and k[6] == 3 and k[8] == 1 and
                         k[2] <= a.drop_f16_halo_hw]:
