@@ -136,6 +136,9 @@ def build_model(args, dev):
     return model
 
 
+ROOF_FLUSH_MB = 0  # a cache-evicting write between the int8 roofline launches (MB; 0 = none, the default)
+
+
 def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320, int8=False):
     """Time the largest conv implicit GEMM of the UNet (SD1.5 at CFG batch 8: down/up block 0
     conv 320->320 3x3 @ 64x64, M = 32768, N = 320, K = 2880; SDXL at CFG batch 4: the same conv
@@ -167,13 +170,31 @@ def dominant_kernel_roofline(dev, iters=20, n=8, h=64, w=64, c=320, int8=False):
     for i in range(NROT):
         run(i)
     st = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for i in range(iters):
-        run(i)
-    e1.record(st)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / iters
+    # Timed so that avg_us agrees with the step sequence's durations of the same launches
+    # (scripts/roof_check.py, profiles/r06zb_roofline_forms.log): the int8 conv one launch per event
+    # pair right after a copy writes its input (as the GroupNorm apply does in the step: 39.2 us vs
+    # 38.4-40.2 in prof_r06z_int8; back to back on warm inputs it read 36.5); the fp16 conv back to
+    # back over the rotated inputs (59.3 us vs 55.1-57.8; after a producer copy it read 62.7).
+    if int8:
+        flush = torch.empty(max(ROOF_FLUSH_MB, 1) << 19, dtype=torch.float16, device=dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+        for i in range(iters):
+            if ROOF_FLUSH_MB:
+                flush.zero_()
+            xqs[i % NROT].copy_(xq)
+            ev[i][0].record(st)
+            run(i)
+            ev[i][1].record(st)
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in ev) / iters
+    else:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for i in range(iters):
+            run(i)
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / iters
     flops = 2.0 * (n * h * w) * c * (9 * c)
     tflops = flops / (ms * 1e-3) / 1e12
     peak = PEAK_I8_TOPS if int8 else PEAK_F16_TFLOPS
