@@ -9,8 +9,8 @@ KV=$1; shift
 # QD_COLMAX_*) are retired: an A/B on them would compare two identical builds.  Kernel-choice A/Bs go
 # through scripts/ab_flag.sh or the qd_*_force C-ABI knobs.
 case "${KV%%=*}" in
-  QD_GEMM_TABLE|QD_GEMM_TUNE|QD_LIB_PATH|QD_W4_OPERAND) ;;
-  *) echo "[ab_env] ${KV%%=*} is not read by the product (live: QD_GEMM_TABLE QD_GEMM_TUNE QD_LIB_PATH QD_W4_OPERAND)"; exit 2 ;;
+  QD_GEMM_TABLE|QD_GEMM_TUNE|QD_LIB_PATH|QD_W4_OPERAND|QD_TUNE_COLD) ;;
+  *) echo "[ab_env] ${KV%%=*} is not read by the product (live: QD_GEMM_TABLE QD_GEMM_TUNE QD_LIB_PATH QD_W4_OPERAND QD_TUNE_COLD)"; exit 2 ;;
 esac
 R=${1:-2}; shift
 for i in $(seq 1 "$R"); do
