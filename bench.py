@@ -61,6 +61,8 @@ def parse():
                     help="0: every usable core (sched_getaffinity, capped by the cgroup CPU quota)")
     ap.add_argument("--epi-lds", action="store_true",
                     help="measurement: every GEMM epilogue through the LDS C tile (qd_gemm_epi_lds, A/B runs)")
+    ap.add_argument("--gn-geom", default=None,
+                    help="measurement: GroupNorm statistics / apply rows per thread 'S,A' (qd_gn_geom_force, A/B runs)")
     ap.add_argument("--no-int8-mode", action="store_true",
                     help="skip the int8-MFMA mode object of the default SD1.5 W8A8 line")
     a = ap.parse_args()
@@ -452,6 +454,9 @@ def main():
     if args.epi_lds:
         from qdiff import _lib
         _lib.call("qd_gemm_epi_lds", 1)
+    if args.gn_geom:
+        from qdiff import _lib
+        _lib.call("qd_gn_geom_force", *[int(v) for v in args.gn_geom.split(",")])
     model = build_model(args, dev)
     log(f"model built + quantized ({args.model} {args.mode})")
     if args.model == "sd35":
