@@ -27,8 +27,9 @@ print("child finished: equal", bool(torch.equal(eager, got)))
 
 def main():
     r = subprocess.run([sys.executable, "-c", CHILD], capture_output=True, text=True, timeout=600)
-    tail = (r.stdout + r.stderr).strip().splitlines()[-12:]
-    print("\n".join(tail))
+    lines = (r.stdout + r.stderr).strip().splitlines()
+    cause = [l for l in lines if "rror" in l or "captur" in l.lower() or "what()" in l][:12]
+    print("\n".join(["-- the child's error lines:"] + cause + ["-- the child's last lines:"] + lines[-6:]))
     print(f"child exit status {r.returncode} (expected non-zero: the capture aborts without pipeline.py's "
           f"collect-before / collector-off-during capture)")
     sys.exit(0 if r.returncode != 0 else 1)
