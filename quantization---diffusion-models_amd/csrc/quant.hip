@@ -500,6 +500,10 @@ extern "C" int qd_conv_weight_khwc(const void* w, int co, int ci, int kh, int kw
 // ---------------------------------------------------------------------------------------
 // conv-output finalize: out = half(fq(y) + residual | + chan_add[n][c])
 // ---------------------------------------------------------------------------------------
+// Q / RES / CADD: the output fake-quant, the residual add and the per-(n, c) add as compile-time flags
+// (the host maps qmax > 0 / res / cadd onto them): no per-element uniform branch, so the 8 channels'
+// conversion chains interleave (as k_gn_stats<XF, F>).  RES and CADD exclude each other.
+template <bool Q, bool RES, bool CADD>
 __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, const float* __restrict__ amax,
                                                   int hw, int c, int qmax, int rows_per_block,
                                                   const f16* __restrict__ res,
@@ -513,16 +517,8 @@ __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, con
   float sc[8];
   double rs[8];
   f16x8 ca = {};
-  if (cadd && !res) ca = *reinterpret_cast<const f16x8*>(cadd + n * cadd_ld + ch);
-  if (qmax > 0) {
-    fq_scales8(amax + n * c + ch, qmax, sc, rs);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = 0.f;
-      rs[j] = 0.0;
-    }
-  }
+  if constexpr (CADD) ca = *reinterpret_cast<const f16x8*>(cadd + n * cadd_ld + ch);
+  if constexpr (Q) fq_scales8(amax + n * c + ch, qmax, sc, rs);
   const int by = blockDim.y;
   for (int rb = r0 + threadIdx.y; rb < r1; rb += 4 * by) {
     f16x8 v[4], rr[4];
@@ -530,28 +526,26 @@ __global__ void __launch_bounds__(256) k_finalize(const f16* __restrict__ y, con
     for (int u = 0; u < 4; ++u) {
       const long e = (n * hw + min(rb + u * by, r1 - 1)) * c + ch;
       v[u] = *reinterpret_cast<const f16x8*>(y + e);
-      rr[u] = *reinterpret_cast<const f16x8*>((res ? res : y) + e);
+      if constexpr (RES) rr[u] = *reinterpret_cast<const f16x8*>(res + e);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       QD_PIN(v[u]);
-      QD_PIN(rr[u]);
+      if constexpr (RES) QD_PIN(rr[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (rb + u * by >= r1) break;
       const long e = (n * hw + rb + u * by) * c + ch;
-      f16x8 o;
-      if (qmax > 0) {
+      f16x8 o = v[u];
+      if constexpr (Q) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = fq_apply_r((float)v[u][j], sc[j], rs[j]);
-      } else {
-        o = v[u];
       }
-      if (res) {
+      if constexpr (RES) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)rr[u][j]);
-      } else if (cadd) {
+      } else if constexpr (CADD) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (f16)((float)o[j] + (float)ca[j]);
       }
@@ -571,10 +565,23 @@ extern "C" int qd_fq_finalize(const void* y, const float* amax, int n, int hw, i
   QD_REQUIRE(n_bits == 0 || (amax && n_bits >= 2 && n_bits <= 16), "bad n_bits / amax");
   if ((long)n * hw * c == 0) return 0;
   const CrGeom g = cr_geom(n, hw, c);
-  k_finalize<<<dim3(g.gx, n, g.z), dim3(g.bx, g.by), 0, S(stream)>>>((const f16*)y, amax, hw, c,
-                                                                      n_bits ? qmax_of(n_bits) : 0, g.rpb,
-                                                                      (const f16*)residual, (const f16*)chan_add,
-                                                                      chan_add_ld, (f16*)out);
+  const dim3 gr(g.gx, n, g.z), bl(g.bx, g.by);
+  const int qm = n_bits ? qmax_of(n_bits) : 0;
+#define QD_FIN(QV, RV, CV)                                                                                    \
+  k_finalize<QV, RV, CV><<<gr, bl, 0, S(stream)>>>((const f16*)y, amax, hw, c, qm, g.rpb, (const f16*)residual, \
+                                                   (const f16*)chan_add, chan_add_ld, (f16*)out)
+  const bool q = qm > 0;
+  if (residual) {  // (a residual takes precedence over chan_add, as before)
+    if (q) QD_FIN(true, true, false);
+    else QD_FIN(false, true, false);
+  } else if (chan_add) {
+    if (q) QD_FIN(true, false, true);
+    else QD_FIN(false, false, true);
+  } else {
+    if (q) QD_FIN(true, false, false);
+    else QD_FIN(false, false, false);
+  }
+#undef QD_FIN
   QD_CHECK_LAUNCH();
   return 0;
 }
