@@ -1037,15 +1037,27 @@ __global__ void __launch_bounds__(256) k_sample_apply_i8(const f16* __restrict__
   if (blockIdx.x == 0 && threadIdx.x == 0) sa[n] = s;
   const f16* p = x + n * per_sample;
   int8_t* q = y + n * per_sample;
-  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < per_sample; i += (long)gridDim.x * 2048) {
-    const f16x8 v = *reinterpret_cast<const f16x8*>(p + i);
-    unsigned lo = 0, hi = 0;
+  // 4 independent 16-B loads in flight per thread per iteration (clamped, not guarded; the stores
+  // are guarded) instead of one dependent load per iteration
+  const long stride = (long)gridDim.x * 2048;
+  for (long i0 = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i0 < per_sample; i0 += 4 * stride) {
+    f16x8 v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lo |= (unsigned)(uint8_t)q_i8((float)v[j], s, rs) << (8 * j);
-      hi |= (unsigned)(uint8_t)q_i8((float)v[4 + j], s, rs) << (8 * j);
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f16x8*>(p + min(i0 + u * stride, per_sample - 8));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= per_sample) break;
+      unsigned lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lo |= (unsigned)(uint8_t)q_i8((float)v[u][j], s, rs) << (8 * j);
+        hi |= (unsigned)(uint8_t)q_i8((float)v[u][4 + j], s, rs) << (8 * j);
+      }
+      *reinterpret_cast<uint2*>(q + i) = make_uint2(lo, hi);
     }
-    *reinterpret_cast<uint2*>(q + i) = make_uint2(lo, hi);
   }
 }
 
@@ -1066,18 +1078,33 @@ __global__ void __launch_bounds__(256) k_cat_apply_i8(const f16* __restrict__ x,
   if (blockIdx.x == 0 && threadIdx.x == 0) sa[n] = s;
   const int cc = c / 8, c2 = c - c1;
   const long chunks = rows * cc;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < chunks; e += (long)gridDim.x * 256) {
-    const long r = e / cc;
-    const int ch = (int)(e - r * cc) * 8;
-    const long row = n * rows + r;
-    const f16x8 v = *reinterpret_cast<const f16x8*>(ch < c1 ? x + row * c1 + ch : x2 + row * c2 + (ch - c1));
-    unsigned lo = 0, hi = 0;
+  // 4 chunks' loads in flight per thread per iteration (chunk index clamped, stores guarded)
+  const long stride = (long)gridDim.x * 256;
+  for (long e0 = (long)blockIdx.x * 256 + threadIdx.x; e0 < chunks; e0 += 4 * stride) {
+    f16x8 v[4];
+    long row[4];
+    int chs[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lo |= (unsigned)(uint8_t)q_i8((float)v[j], s, rs) << (8 * j);
-      hi |= (unsigned)(uint8_t)q_i8((float)v[4 + j], s, rs) << (8 * j);
+    for (int u = 0; u < 4; ++u) {
+      const long e = min(e0 + u * stride, chunks - 1);
+      const long r = e / cc;
+      chs[u] = (int)(e - r * cc) * 8;
+      row[u] = n * rows + r;
+      v[u] = *reinterpret_cast<const f16x8*>(chs[u] < c1 ? x + row[u] * c1 + chs[u] : x2 + row[u] * c2 + (chs[u] - c1));
     }
-    *reinterpret_cast<uint2*>(y + row * c + ch) = make_uint2(lo, hi);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) QD_PIN(v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * stride >= chunks) break;
+      unsigned lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lo |= (unsigned)(uint8_t)q_i8((float)v[u][j], s, rs) << (8 * j);
+        hi |= (unsigned)(uint8_t)q_i8((float)v[u][4 + j], s, rs) << (8 * j);
+      }
+      *reinterpret_cast<uint2*>(y + row[u] * c + chs[u]) = make_uint2(lo, hi);
+    }
   }
 }
 
