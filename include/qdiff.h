@@ -158,7 +158,9 @@ int qd_linear_fwd(const void* x, int M, int K, int lda, const void* w, int wfmt,
  * following qd_linear_fwd / qd_conv2d_fwd.  -1 = planner's choice (default); 0..3 = the
  * register-staged tiles 128x160, 128x128, 128x64, 64x64; 100 + i = LDS-DMA variant i (F16
  * weights; packed int4 with wscale_t: the BK-32 variants 110..117 and ping-pong 300..304; other
- * quantized formats keep the planner's register-staged choice).  int8 (qd_linear_i8 / qd_conv2d_i8):
+ * quantized formats keep the planner's register-staged choice); 200..203 the fp16 halo conv (BN 160 /
+ * 128, lock-step / split-phase), 204 / 205 the split-phase halo conv on 128-pixel tiles (images
+ * <= 32 wide; forceable only, no tuner candidate).  int8 (qd_linear_i8 / qd_conv2d_i8):
  * 110..117 LDS-DMA, 130..134 ping-pong, 140..149 halo conv, 150 / 151 the fused GEGLU + codes kernel,
  * 160..167 / 170..177 persistent LDS-DMA linears (2 / 4 tiles per block), 190..192 A-stationary
  * linears.  + 1000 * s: explicit split-K count s (1 = unsplit).  Every int8 choice gives the same bits. */
