@@ -12,7 +12,8 @@ CFG = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 _lib.load().qd_attn_force(CFG)
 for (b, s, skv, heads, d, ld) in ((8, 4096, 4096, 8, 40, 960), (8, 1024, 1024, 10, 64, 1920), (2, 4429, 4429, 38, 64, 7296),
                                   (8, 4096, 77, 8, 40, 320), (8, 1024, 1024, 8, 80, 1920), (8, 256, 256, 8, 160, 3840),
-                                  (4, 4096, 4096, 10, 64, 1920), (4, 1024, 1024, 20, 64, 3840)):
+                                  (4, 4096, 4096, 10, 64, 1920), (4, 1024, 1024, 20, 64, 3840),
+                                  (8, 1024, 77, 8, 80, 640), (8, 256, 77, 8, 160, 1280), (8, 64, 77, 8, 160, 1280)):
     c = heads * d
     x = torch.randn(b, s, ld, device=dev).half()
     kv = torch.randn(b, skv, ld, device=dev).half()
