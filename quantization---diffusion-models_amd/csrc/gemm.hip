@@ -367,6 +367,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef f16 f16x2e __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ i32x8 f8_operand(f16x8 lo, f16x8 hi) {
   const i32x4 a = __builtin_bit_cast(i32x4, lo), b = __builtin_bit_cast(i32x4, hi);
@@ -432,7 +433,11 @@ constexpr int ln_per(int bn) { return ln_lpr(bn) ? bn / 8 / ln_lpr(bn) : 0; }
 // view of the tile (plain, bias, residual, pre-residual amax, GEGLU at TN % 4 == 0, GELU-tanh)
 template <int TM, int TN, bool DIRECT>
 constexpr bool epi_direct_ok() { return DIRECT && TN >= 2 && TN <= 5 && TM * ((TN + 1) / 2) <= 20; }
-template <int BN, int TM, int TN, bool CONV, bool DIRECT>
+// the post-residual amax in the direct path (column maxima of the final fp16 values kept packed,
+// TN / 2 + 1 f16x8 registers per lane): the tiles of at most 20 fragments only
+template <int TM, int TN, bool DIRECT, bool DPOSTK>
+constexpr bool epi_dpost_ok() { return DPOSTK && epi_direct_ok<TM, TN, DIRECT>() && TM * TN <= 20; }
+template <int BN, int TM, int TN, bool CONV, bool DIRECT, bool DPOSTK = false>
 __device__ __forceinline__ bool epi_direct(const GemmArgs& p) {
   const bool has_res = (p.epi & QD_EPI_RESIDUAL) && p.res;
   const bool do_amax = (p.epi & QD_EPI_AMAX) && p.amax;
@@ -442,10 +447,12 @@ __device__ __forceinline__ bool epi_direct(const GemmArgs& p) {
   const bool gn = (p.epi & QD_EPI_GNSTATS) && p.gnp && !geglu && !gtanh;
   const bool ln = BN == 320 && (p.epi & QD_EPI_LN) && !geglu && !gtanh;
   const bool cadd = (p.epi & QD_EPI_CADD) && p.cadd && !geglu && !gtanh;
-  return epi_direct_ok<TM, TN, DIRECT>() && !p.epi_lds && !gn && !ln && !cadd && !post && (!geglu || TN % 4 == 0);
+  return epi_direct_ok<TM, TN, DIRECT>() && !p.epi_lds && !gn && !ln && !cadd &&
+         (!post || epi_dpost_ok<TM, TN, DIRECT, DPOSTK>()) && (!geglu || TN % 4 == 0);
 }
 
-template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH, bool CONV = false, bool DIRECT = true>
+template <int BM, int BN, int NT, int TM, int TN, bool SPLIT, int LDSH, bool CONV = false, bool DIRECT = true,
+          bool DPOSTK = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM][TN], f16* smem, int m0, int n0,
                                               int wm0, int wn0, int split) {
   static_assert(SPLIT || epi_lds_halves(BM, BN) <= LDSH, "epilogue LDS exceeds the kernel's buffer");
@@ -499,7 +506,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     const bool blk_amax = do_amax && !geglu && WGM > 1 && p.rows_per_sample % BM == 0;
     const unsigned ybytes = (unsigned)min((long)p.M * p.ldy * 2, 2147483647L);
     const __amdgpu_buffer_rsrc_t yrs = rsrc(p.y, ybytes);
-    const __amdgpu_buffer_rsrc_t rrs = rsrc(has_res && !fres ? p.res : p.y, has_res && !fres ? ybytes : 0u);
+    // (the LDS path's fres forms load their residual in the fragment layout; the direct path - post
+    // included - through this descriptor)
+    const bool rdesc = has_res && (!fres || (DPOSTK && epi_direct<BN, TM, TN, CONV, DIRECT, DPOSTK>(p)));
+    const __amdgpu_buffer_rsrc_t rrs = rsrc(rdesc ? p.res : p.y, rdesc ? ybytes : 0u);
     // the residual tile of the coalesced pass is loaded first, all NR chunks per thread in flight
     // while the fragments go to LDS (a 2-deep load / add / store loop left the epilogue waiting on
     // HBM latency NR / 2 times)
@@ -512,13 +522,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
     // Same arithmetic per element as the LDS pass below, so the output bits are identical.
     // (an odd TN's last fragment stores its 4 columns as one 8-B store per lane)
     constexpr bool DIRECT_OK = epi_direct_ok<TM, TN, DIRECT>();
-    const bool direct = epi_direct<BN, TM, TN, CONV, DIRECT>(p);
+    const bool direct = epi_direct<BN, TM, TN, CONV, DIRECT, DPOSTK>(p);
     const bool pre_res = has_res && !fres && !geglu && !direct;
     // post-residual amax: the residual in the fragments' layout (4 consecutive columns of one row
     // per lane and fragment), all TM x TN 8-B loads issued before any is used
     constexpr bool PF_POST = TM * TN <= 20;  // (register budget: the 4 x 5 fragment tiles and smaller)
     f16x4 rf[PF_POST ? TM : 1][PF_POST ? TN : 1];
-    if (PF_POST && fres) {
+    if (PF_POST && fres && !(DPOSTK && direct)) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn0 + j * 16 + fq * 4;
@@ -588,7 +598,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           }
         };
         // prefetch distance in row blocks (the 256 x 128 tiles' 32 fragments leave room for one)
-        constexpr int PFD = TM * TN >= 32 ? 1 : 2;
+        constexpr int PFD = TM * TN >= 32 || DPOSTK ? 1 : 2;  // (DPOSTK: room for the packed column maxima)
         if (has_res) {
 #pragma unroll
           for (int i = 0; i < PFD && i < TM; ++i) load_res(i);
@@ -611,7 +621,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           for (int r = 0; r < 4; ++r) h[r] = (f16)(acc[i][j][r] + bq[j][r]);
           return h;
         };
-        if (do_amax && !gg) {
+        if (do_amax && !gg && !post) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int n = n0 + wn0 + j * 16 + fq * 4;
@@ -647,10 +657,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           }
           return o;
         };
+        // post-residual amax: |final| column maxima of this lane's rows, packed fp16 (max of fp16 values
+        // is exact, so the f32 maxima of the LDS path come out bit-identical): pair jp's 8 columns in
+        // pm[jp], the odd tail's 4 in pmt
+        constexpr bool DPOST = epi_dpost_ok<TM, TN, DIRECT, DPOSTK>();
+        f16x8 pm[DPOST ? (NJ > 0 ? NJ : 1) : 1];
+        f16x4 pmt = {};
+        if constexpr (DPOST) {
+#pragma unroll
+          for (int jp = 0; jp < NJ; ++jp) pm[jp] = f16x8{};
+        }
         // pair (a | b) -> 16-B store (+ residual: RES, a compile-time copy of has_res - the row loop is
-        // instantiated for both, so no per-element select) at output column n of row m
-        auto store_pair = [&](auto res_c, int i, int jp, f16x4 fa, f16x4 fb, int m, bool row_ok) {
+        // instantiated for both, so no per-element select; POST: the post-residual column maxima) at
+        // output column n of row m
+        auto store_pair = [&](auto res_c, auto post_c, int i, int jp, f16x4 fa, f16x4 fb, int m, bool row_ok) {
           constexpr bool RES = decltype(res_c)::value;
+          constexpr bool POST = DPOST && decltype(post_c)::value;
           u32x4 w;
           {
             const u32x2 a = __builtin_bit_cast(u32x2, fa), b = __builtin_bit_cast(u32x2, fb);
@@ -665,6 +687,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
             for (int r = 0; r < 8; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + jp][r]);
             w = __builtin_bit_cast(u32x4, v);
           }
+          if constexpr (POST) {
+            if (row_ok && n < oN)
+              pm[jp] = __builtin_elementwise_max(pm[jp], __builtin_bit_cast(f16x8, w & 0x7fff7fffu));
+          }
           const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
 #ifdef QD_ABLATE_EPI_STORES  // diagnostic build: the direct epilogue's stores dropped (values kept live)
           asm volatile("" ::"v"(w), "v"(off));
@@ -672,23 +698,25 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
           __builtin_amdgcn_raw_buffer_store_b128(w, yrs, (row_ok && n < oN) ? (int)off : (int)OOB, 0, 0);
 #endif
         };
-        auto rows = [&](auto res_c) {
+        auto rows = [&](auto res_c, auto post_c) {
           constexpr bool RES = decltype(res_c)::value;
+          constexpr bool POST = DPOST && decltype(post_c)::value;
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
             if (RES && i + PFD < TM) load_res(i + PFD);
             const int m = m0 + wm0 + i * 16 + fr;
             const bool row_ok = m < p.M;
-            if constexpr (TN % 4 == 0) {
+            if constexpr (TN % 4 == 0 && !POST) {
               if (gg) {
 #pragma unroll
                 for (int jp = 0; jp < TN / 4; ++jp)
-                  store_pair(res_c, i, jp, geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2), m, row_ok);
+                  store_pair(res_c, post_c, i, jp, geglu_frag(i, 4 * jp), geglu_frag(i, 4 * jp + 2), m, row_ok);
                 continue;
               }
             }
 #pragma unroll
-            for (int jp = 0; jp < NJ; ++jp) store_pair(res_c, i, jp, plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1), m, row_ok);
+            for (int jp = 0; jp < NJ; ++jp)
+              store_pair(res_c, post_c, i, jp, plain_frag(i, 2 * jp), plain_frag(i, 2 * jp + 1), m, row_ok);
             if constexpr (TAIL) {
               f16x4 v = plain_frag(i, TN - 1);
               if constexpr (RES) {
@@ -696,6 +724,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
                 for (int r = 0; r < 4; ++r) v[r] = (f16)((float)v[r] + (float)rq[i * NJT + NJ][r]);
               }
               const int n = n0 + wn0 + (TN - 1) * 16 + fq * 4;
+              if constexpr (POST) {
+                if (row_ok && n < p.N)
+                  pmt = __builtin_elementwise_max(
+                      pmt, __builtin_bit_cast(f16x4, __builtin_bit_cast(u32x2, v) & 0x7fff7fffu));
+              }
               const unsigned off = ((unsigned)m * (unsigned)p.ldy + (unsigned)n) * 2u;
               __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs,
                                                     (row_ok && n < p.N) ? (int)off : (int)OOB, 0, 0);
@@ -705,8 +738,53 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x4 (&acc)[TM
             __builtin_amdgcn_sched_barrier(0);
           }
         };
-        if (has_res) rows(std::true_type{});
-        else rows(std::false_type{});
+        if (DPOST && post) {
+          rows(std::true_type{}, std::true_type{});
+          if constexpr (DPOST) {
+            // the lane's maxima over its 16-row groups (lanes fr = 0..15 of each fq), then lane fr == 0
+            // commits them in the fragment column order of amax_commit
+            auto red = [&](unsigned u) {
+#pragma unroll
+              for (int o = 1; o < 16; o <<= 1) {
+                const unsigned t = (unsigned)__shfl_xor((int)u, o, 64);
+                u = __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(f16x2e, u),
+                                                                           __builtin_bit_cast(f16x2e, t)));
+              }
+              return u;
+            };
+            const int row0 = m0 + wm0;
+            auto commit = [&](int nl, float v) {
+              if (blk_amax) cmx[(wm0 / WM) * BN + nl] = v;
+              else if (n0 + nl < p.N && row0 < p.M)
+                atomic_max_pos(p.amax + (long)(row0 / p.rows_per_sample) * p.N + n0 + nl, v);
+            };
+#pragma unroll
+            for (int jp = 0; jp < NJ; ++jp) {
+              u32x4 u = __builtin_bit_cast(u32x4, pm[jp]);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) u[r] = red(u[r]);
+              const f16x8 h = __builtin_bit_cast(f16x8, u);
+              if (fr == 0) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) commit(wn0 + 32 * jp + cpart + e, (float)h[e]);
+              }
+            }
+            if constexpr (TAIL) {
+              u32x2 u = __builtin_bit_cast(u32x2, pmt);
+              u[0] = red(u[0]);
+              u[1] = red(u[1]);
+              const f16x4 h = __builtin_bit_cast(f16x4, u);
+              if (fr == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) commit(wn0 + (TN - 1) * 16 + fq * 4 + r, (float)h[r]);
+              }
+            }
+          }
+        } else if (has_res) {
+          rows(std::true_type{}, std::false_type{});
+        } else {
+          rows(std::false_type{}, std::false_type{});
+        }
         if (do_amax && !gg && blk_amax) {
           __syncthreads();
           for (int c = threadIdx.x; c < BN; c += NT) {
@@ -1554,7 +1632,7 @@ constexpr int dma_waves_per_eu_w4(int bm, int bn, int st, int nt, int bkt) {
 // state and the loop-invariant lane coordinates live through the epilogue: at the one-tile cap the
 // 128 x 160 tile spills ~50 VGPRs).
 template <int BM, int BN, int WGM, int WGN, int ST, int PIPE, int BKT, int AMODE, bool SPLIT, bool I8 = false,
-          bool F8 = false, bool W4 = false, bool PERSIST = false>
+          bool F8 = false, bool W4 = false, bool PERSIST = false, bool DPOSTK = false>
 __global__ void __launch_bounds__(64 * WGM * WGN,
                                   W4        ? dma_waves_per_eu_w4(BM, BN, ST, 64 * WGM * WGN, BKT)
                                   : PERSIST ? (dma_waves_per_eu(BM, BN, ST, 64 * WGM * WGN, BKT) / 2 > 0
@@ -1822,7 +1900,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN,
     nk = nkn;
     drain = true;
   } else {
-    gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, AMODE != AM_LINEAR>(p, acc, smem, m0, n0, wm0, wn0, split);
+    gemm_epilogue<BM, BN, NT, TM, TN, SPLIT, LDSZ, AMODE != AM_LINEAR, true, DPOSTK>(p, acc, smem, m0, n0, wm0, wn0,
+                                                                                     split);
     break;
   }
   }
@@ -3492,10 +3571,26 @@ static void launch_fmt(const GemmArgs& p, int fmt, hipStream_t st) {
   }
 }
 
+// the post-residual amax epilogue (QD_EPI_AMAX_POST with its amax and residual): the 128 x 160 linear
+// tiles (fp16 variant 0, int8 variant 10) run it in the direct-store path of their own instantiation
+// (DPOSTK), so the other epilogues' register allocation does not carry the packed column maxima
+static bool epi_post_direct(const GemmArgs& p) {
+  return (p.epi & QD_EPI_AMAX_POST) && (p.epi & QD_EPI_AMAX) && p.amax && (p.epi & QD_EPI_RESIDUAL) && p.res &&
+         !(p.epi & (QD_EPI_GEGLU | QD_EPI_GELU_TANH | QD_EPI_GNSTATS | QD_EPI_LN | QD_EPI_CADD)) && !p.epi_lds &&
+         p.pgrid <= 0;
+}
+
 template <int V, int AMODE, bool SPLIT>
 static void launch_dma_v(const GemmArgs& p, hipStream_t st) {
   constexpr DmaVar d = kDmaC[V];
   const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
+  if constexpr (AMODE == AM_LINEAR && !SPLIT && V == 0) {
+    if (epi_post_direct(p)) {
+      k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, false, false, false, false, false, true>
+          <<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+      return;
+    }
+  }
   k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
 }
 
@@ -4285,6 +4380,13 @@ static void launch_i8_v(const GemmArgs& p, hipStream_t st) {
     }
   }
   const int nwg = ((p.M + d.bm - 1) / d.bm) * ((p.N + d.bn - 1) / d.bn) * p.splits;
+  if constexpr (AMODE == AM_LINEAR && !SPLIT && V == 10) {
+    if (epi_post_direct(p)) {
+      k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, false, true, false, false, false, true>
+          <<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
+      return;
+    }
+  }
   k_gemm_dma<d.bm, d.bn, d.wgm, d.wgn, d.st, d.pipe, d.bkt, AMODE, SPLIT, true><<<nwg, 64 * d.wgm * d.wgn, 0, st>>>(p);
 }
 
